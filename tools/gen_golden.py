@@ -1,0 +1,377 @@
+#!/usr/bin/env python3
+"""Golden-vector generator — CONTAINER ONLY, never shipped to the GPU box.
+
+Imports the reference's own hot-path modules from /root/reference (read-only)
+and records their outputs on seeded inputs into tests/golden/*.npz.  The
+fixtures are data (inputs + expected outputs); no reference source is copied.
+
+Reference modules used (SURVEY.md §8c "How to import"):
+  * B/ = ppo-dash-study/001_baseline/ppo/{storage,model,distributions}.py and
+    ppo/algo/ppo.py — the vector-less CNN variant (T/ crashes when V=0,
+    T/a2c_ppo_acktr/storage.py:144).
+  * T/ = ppo-dash-training/pytorch-a2c-ppo-acktr-gail/a2c_ppo_acktr/... — the
+    recurrent (GRU) + vector-obs variant.
+A stub `<pkg>.envs` module stands in for the gym/baselines-backed envs.py,
+which only provides the VecNormalize type to utils.py.
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+"""
+import importlib
+import importlib.util
+import os
+import sys
+import types
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+
+import torch  # noqa: E402
+
+REF_ROOT = "/root/reference"
+B_DIR = f"{REF_ROOT}/ppo-dash-study/001_baseline"
+T_DIR = f"{REF_ROOT}/ppo-dash-training/pytorch-a2c-ppo-acktr-gail"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden")
+
+
+class Discrete:  # duck-typed gym.spaces.Discrete (storage.py:20, model.py:30)
+    def __init__(self, n):
+        self.n = n
+
+
+def load_ref(variant):
+    """Import (storage, model, distributions, ppo) of one reference tree."""
+    ref, pkg = (B_DIR, "ppo") if variant == "B" else (T_DIR, "a2c_ppo_acktr")
+    for k in list(sys.modules):
+        if k == pkg or k.startswith(pkg + "."):
+            del sys.modules[k]
+    while ref in sys.path:
+        sys.path.remove(ref)
+    for other in (B_DIR, T_DIR):
+        while other in sys.path:
+            sys.path.remove(other)
+    sys.path.insert(0, ref)
+    stub = types.ModuleType(pkg + ".envs")
+    stub.VecNormalize = type("VecNormalize", (), {})
+    sys.modules[pkg + ".envs"] = stub
+    S = importlib.import_module(pkg + ".storage")
+    M = importlib.import_module(pkg + ".model")
+    D = importlib.import_module(pkg + ".distributions")
+    spec = importlib.util.spec_from_file_location(f"refppo_{variant}", f"{ref}/{pkg}/algo/ppo.py")
+    P = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(P)
+    return S, M, D, P
+
+
+def flat_params(module):
+    return np.concatenate([p.detach().reshape(-1).numpy().astype(np.float32)
+                           for p in module.parameters()])
+
+
+def param_names(module):
+    return np.array([n for n, _ in module.named_parameters()])
+
+
+def save(name, **arrays):
+    os.makedirs(OUT, exist_ok=True)
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path}  ({os.path.getsize(path) / 1024:.1f} KiB)")
+
+
+# ---------------------------------------------------------------------------
+# (1) GAE / returns, all four compute_returns branches (storage.py:82-121)
+# ---------------------------------------------------------------------------
+def gen_gae(S):
+    out = {}
+    rng = np.random.default_rng(7)
+    T, N = 32, 64
+    r = rng.standard_normal((T, N, 1)).astype(np.float32)
+    v = (3.0 * rng.standard_normal((T + 1, N, 1))).astype(np.float32)
+    m = (rng.random((T + 1, N, 1)) < 0.95).astype(np.float32)
+    bm = (rng.random((T + 1, N, 1)) < 0.95).astype(np.float32)
+    nv = (3.0 * rng.standard_normal((N, 1))).astype(np.float32)
+    out.update(rewards=r, value_preds=v, masks=m, bad_masks=bm, next_value=nv)
+    for gi, (gamma, lam) in enumerate([(0.99, 0.95), (0.997, 0.9)]):
+        for use_gae in (True, False):
+            for ptl in (True, False):
+                st = S.RolloutStorage(T, N, (1,), [0], Discrete(2), 1)
+                st.rewards.copy_(torch.from_numpy(r))
+                st.value_preds.copy_(torch.from_numpy(v))
+                st.masks.copy_(torch.from_numpy(m))
+                st.bad_masks.copy_(torch.from_numpy(bm))
+                st.returns.fill_(-7.0)  # sentinel: GAE branches leave returns[T] untouched
+                st.compute_returns(torch.from_numpy(nv), use_gae, gamma, lam, ptl)
+                key = f"g{gi}_gae{int(use_gae)}_ptl{int(ptl)}"
+                out[key + "_returns"] = st.returns.numpy().copy()
+                out[key + "_value_preds"] = st.value_preds.numpy().copy()
+    out["gammas"] = np.array([0.99, 0.997])
+    out["lambdas"] = np.array([0.95, 0.9])
+    save("gae.npz", **out)
+
+
+# ---------------------------------------------------------------------------
+# (2) advantage normalisation as PPO.update computes it (ppo.py:35-37)
+#     captured by intercepting the `advantages` handed to the generator
+# ---------------------------------------------------------------------------
+def gen_advnorm(S, P):
+    out = {}
+    for ci, (T, N, scale) in enumerate([(32, 64, 3.0), (128, 256, 10.0), (7, 5, 1.0)]):
+        rng = np.random.default_rng(100 + ci)
+        st = S.RolloutStorage(T, N, (1,), [0], Discrete(2), 1)
+        ret = (scale * rng.standard_normal((T + 1, N, 1)) + 1.5).astype(np.float32)
+        val = (scale * rng.standard_normal((T + 1, N, 1))).astype(np.float32)
+        st.returns.copy_(torch.from_numpy(ret))
+        st.value_preds.copy_(torch.from_numpy(val))
+        captured = []
+
+        def fake_gen(advantages, num_mini_batch, _c=captured):
+            _c.append(advantages.clone())
+            return iter(())
+
+        st.feed_forward_generator = fake_gen
+
+        class _AC:
+            is_recurrent = False
+
+            def parameters(self):
+                return [torch.nn.Parameter(torch.zeros(1))]
+
+        agent = P.PPO(_AC(), 0.1, 1, 1, 0.5, 0.001, lr=1e-4, eps=1e-5, max_grad_norm=0.5)
+        agent.update(st)
+        out[f"c{ci}_returns"] = ret
+        out[f"c{ci}_value_preds"] = val
+        out[f"c{ci}_advantages"] = captured[0].numpy()
+    save("advnorm.npz", **out)
+
+
+# ---------------------------------------------------------------------------
+# (3) minibatch samplers (storage.py:123-223): indices recovered from a
+#     storage whose value_preds hold their own flat row index t*N+n
+# ---------------------------------------------------------------------------
+def gen_sampler(S):
+    out = {}
+    cases = [(0, 16, 8, 4), (1, 128, 32, 8), (1234, 64, 7, 3), (5, 128, 1024 // 128 * 4, 8)]
+    for ci, (seed, T, N, M) in enumerate(cases):
+        st = S.RolloutStorage(T, N, (1,), [0], Discrete(2), 1)
+        st.value_preds[:-1].copy_(torch.arange(T * N, dtype=torch.float32).view(T, N, 1))
+        adv = torch.zeros(T, N, 1)
+        torch.manual_seed(seed)
+        ff = [b[4].view(-1).long().numpy().copy() for b in st.feed_forward_generator(adv, M)]
+        out[f"c{ci}_meta"] = np.array([seed, T, N, M])
+        out[f"c{ci}_ff"] = np.stack(ff).astype(np.int64)
+        if N % M == 0:  # recurrent_generator indexes past perm otherwise (storage.py:181-182)
+            torch.manual_seed(seed)
+            rec = [b[4].view(-1).long().numpy().copy() for b in st.recurrent_generator(adv, M)]
+            out[f"c{ci}_rec"] = np.stack(rec).astype(np.int64)
+    save("sampler.npz", **out)
+
+
+# ---------------------------------------------------------------------------
+# (4) Categorical head: linear → FixedCategorical → sample/mode/log_probs/
+#     entropy (distributions.py:17-27,54-68); Exp(1) noise replayed from the
+#     generator state so argmax(probs/E) can be checked bit-exactly
+# ---------------------------------------------------------------------------
+def gen_categorical(D):
+    out = {}
+    torch.manual_seed(3)
+    Nrow, Hd, A = 4096, 16, 8
+    head = D.Categorical(Hd, A)
+    # gain-0.01 init makes near-uniform probs; widen the spread so that
+    # sampling is non-trivial, still through the module's own forward
+    with torch.no_grad():
+        head.linear.weight.mul_(150.0)
+        head.linear.bias.uniform_(-0.5, 0.5)
+    feats = torch.randn(Nrow, Hd)
+    with torch.no_grad():
+        dist = head(feats)
+        st = torch.get_rng_state()
+        action = dist.sample()
+        st_after = torch.get_rng_state()
+        torch.set_rng_state(st)
+        E = torch.empty(Nrow, A).exponential_(1)
+        assert torch.equal(torch.get_rng_state(), st_after), "sample consumed more than one exponential_ draw"
+        logp = dist.log_probs(action)
+        ent = dist.entropy()
+        mode = dist.mode()
+    out.update(features=feats.numpy(), weight=head.linear.weight.detach().numpy(),
+               bias=head.linear.bias.detach().numpy(), logits_raw=(feats @ head.linear.weight.t() + head.linear.bias).detach().numpy(),
+               norm_logits=dist.logits.numpy(), probs=dist.probs.numpy(), exp_noise=E.numpy(),
+               action=action.numpy().astype(np.int64), log_probs=logp.numpy(),
+               entropy=ent.numpy(), mode=mode.numpy().astype(np.int64))
+    save("categorical.npz", **out)
+
+
+# ---------------------------------------------------------------------------
+# (5) one full CNN iteration, run.py:134-248 ordering:
+#     act → env → insert ×T, get_value, compute_returns, update, after_update
+# ---------------------------------------------------------------------------
+def gen_cnn_update(S, M, P, *, hidden, N, T, E, Mb, lr, fname):
+    torch.manual_seed(1)
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase,
+                   base_kwargs={"recurrent": False, "hidden_size": hidden}, vector_obs_len=0)
+    agent = P.PPO(pol, 0.1, E, Mb, 0.5, 0.001, lr=lr, eps=1e-5, max_grad_norm=0.5)
+    st = S.RolloutStorage(T, N, (4, 84, 84), [0], Discrete(8), pol.recurrent_hidden_state_size)
+    init = flat_params(pol)
+    genv = torch.Generator().manual_seed(123)
+    obs_u8 = np.zeros((T + 1, N, 4, 84, 84), np.uint8)
+    o0 = torch.randint(0, 256, (N, 4, 84, 84), dtype=torch.uint8, generator=genv)
+    obs_u8[0] = o0.numpy()
+    st.obs[0].copy_(o0.float() / 255.0)
+    noise, values, actions, logps, rewards, masks = [], [], [], [], [], []
+    for step in range(T):
+        with torch.no_grad():
+            rs = torch.get_rng_state()
+            value, action, logp, hxs = pol.act(st.obs[step], st.vector_obs[step],
+                                               st.recurrent_hidden_states[step], st.masks[step])
+            after = torch.get_rng_state()
+            torch.set_rng_state(rs)
+            En = torch.empty(N, 8).exponential_(1)
+            assert torch.equal(torch.get_rng_state(), after)
+        o = torch.randint(0, 256, (N, 4, 84, 84), dtype=torch.uint8, generator=genv)
+        rew = torch.rand(N, 1, generator=genv)
+        done = torch.rand(N, generator=genv) < 0.3
+        mk = torch.FloatTensor([[0.0] if d else [1.0] for d in done])
+        bmk = torch.ones(N, 1)
+        obs_u8[step + 1] = o.numpy()
+        st.insert(o.float() / 255.0, torch.zeros(N, 0), hxs, action, logp, value, rew, mk, bmk)
+        noise.append(En.numpy()); values.append(value.numpy()); actions.append(action.numpy())
+        logps.append(logp.numpy()); rewards.append(rew.numpy()); masks.append(mk.numpy())
+    with torch.no_grad():
+        next_value = pol.get_value(st.obs[-1], st.vector_obs[-1], st.recurrent_hidden_states[-1],
+                                   st.masks[-1]).detach()
+    st.compute_returns(next_value, True, 0.99, 0.95, False)
+    returns = st.returns.numpy().copy()
+    vpreds = st.value_preds.numpy().copy()
+
+    # capture: minibatch permutations (replayed from the generator state),
+    # the first minibatch's outputs and clipped grads, the loss triple
+    rng_before_update = torch.get_rng_state()
+    mb_records = []
+    orig_eval = pol.evaluate_actions
+
+    def eval_wrap(*a, **k):
+        res = orig_eval(*a, **k)
+        mb_records.append({"values": res[0].detach().numpy().copy(),
+                           "logp": res[1].detach().numpy().copy(),
+                           "entropy": float(res[2].detach())})
+        return res
+
+    pol.evaluate_actions = eval_wrap
+    grads = []
+    orig_step = agent.optimizer.step
+
+    def step_wrap(*a, **k):
+        grads.append(np.concatenate([p.grad.reshape(-1).numpy().copy() for p in pol.parameters()]))
+        return orig_step(*a, **k)
+
+    agent.optimizer.step = step_wrap
+    vl, al, ent = agent.update(st)
+    pol.evaluate_actions = orig_eval
+    rng_after_update = torch.get_rng_state()
+    torch.set_rng_state(rng_before_update)
+    perms = np.stack([torch.randperm(N * T).numpy() for _ in range(E)]).astype(np.int64)
+    assert torch.equal(torch.get_rng_state(), rng_after_update)
+    final = flat_params(pol)
+    st.after_update()
+    save(fname, init_params=init, final_params=final, names=param_names(pol),
+         obs_u8=obs_u8, exp_noise=np.stack(noise), values=np.stack(values),
+         actions=np.stack(actions).astype(np.int64), action_log_probs=np.stack(logps),
+         rewards=np.stack(rewards), masks=np.stack(masks), next_value=next_value.numpy(),
+         returns=returns, value_preds_after=vpreds, perms=perms,
+         mb0_values=mb_records[0]["values"], mb0_logp=mb_records[0]["logp"],
+         mb_entropy=np.array([r["entropy"] for r in mb_records]),
+         mb0_clipped_grad=grads[0], last_clipped_grad=grads[-1],
+         losses=np.array([vl, al, ent]),
+         meta=np.array([hidden, N, T, E, Mb]), lr=np.array([lr]))
+
+
+# ---------------------------------------------------------------------------
+# (6) GRU + vector obs evaluate_actions / act (T/ model.py:111-166,192-199)
+# ---------------------------------------------------------------------------
+def gen_gru(S, M, P):
+    torch.manual_seed(11)
+    hidden, V, N, T = 32, 14, 4, 8
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase,
+                   base_kwargs={"recurrent": True, "hidden_size": hidden}, vector_obs_len=V)
+    g = torch.Generator().manual_seed(5)
+    obs_u8 = torch.randint(0, 256, (T, N, 4, 84, 84), dtype=torch.uint8, generator=g)
+    vec = torch.rand(T, N, V, generator=g)
+    masks = (torch.rand(T, N, 1, generator=g) > 0.25).float()
+    masks[0] = 1.0
+    h0 = torch.randn(N, hidden, generator=g)
+    actions = torch.randint(0, 8, (T * N, 1), generator=g)
+    with torch.no_grad():
+        val, logp, ent, hT = pol.evaluate_actions((obs_u8.float() / 255.0).view(T * N, 4, 84, 84),
+                                                  vec.view(T * N, V), h0, masks.view(T * N, 1), actions)
+        # single-step act path (x.size(0) == hxs.size(0) branch)
+        v1, f1, h1 = pol.base((obs_u8[0].float() / 255.0), vec[0], h0, masks[0])
+    save("gru_eval.npz", params=flat_params(pol), names=param_names(pol),
+         obs_u8=obs_u8.numpy(), vector_obs=vec.numpy(), masks=masks.numpy(), h0=h0.numpy(),
+         actions=actions.numpy(), values=val.numpy(), log_probs=logp.numpy(),
+         entropy=np.array([float(ent)]), hT=hT.numpy(), step_value=v1.numpy(),
+         step_features=f1.numpy(), step_h=h1.numpy(), meta=np.array([hidden, V, N, T]))
+
+
+# ---------------------------------------------------------------------------
+# (7) clip_grad_norm_ + Adam.step (ppo.py:82-84; torch 2.10 semantics)
+# ---------------------------------------------------------------------------
+def gen_adam():
+    torch.manual_seed(21)
+    shapes = [(32, 4, 8, 8), (32,), (64, 50), (1,)]
+    params = [torch.nn.Parameter(torch.randn(s) * 0.1) for s in shapes]
+    init = np.concatenate([p.detach().reshape(-1).numpy() for p in params])
+    opt = torch.optim.Adam(params, lr=1e-3, eps=1e-5)
+    grads, clipped, after, norms = [], [], [], []
+    for k in range(4):
+        g = [torch.randn(s) * (3.0 if k % 2 == 0 else 0.01) for s in shapes]
+        for p, gi in zip(params, g):
+            p.grad = gi.clone()
+        grads.append(np.concatenate([x.reshape(-1).numpy() for x in g]))
+        tn = torch.nn.utils.clip_grad_norm_(params, 0.5)
+        norms.append(float(tn))
+        clipped.append(np.concatenate([p.grad.reshape(-1).numpy().copy() for p in params]))
+        opt.step()
+        after.append(np.concatenate([p.detach().reshape(-1).numpy().copy() for p in params]))
+    save("adam_clip.npz", init=init, grads=np.stack(grads), clipped=np.stack(clipped),
+         after=np.stack(after), total_norms=np.array(norms),
+         sizes=np.array([int(np.prod(s)) for s in shapes]), lr=np.array([1e-3]),
+         eps=np.array([1e-5]), max_norm=np.array([0.5]))
+
+
+# ---------------------------------------------------------------------------
+# (8) MLPBase submodules (c1; model.py:202-234 — forward itself is broken,
+#     so the submodules are driven directly)
+# ---------------------------------------------------------------------------
+def gen_mlp(M, D):
+    torch.manual_seed(4)
+    base = M.MLPBase(4, recurrent=False, hidden_size=64)
+    head = D.Categorical(64, 2)
+    x = torch.randn(8, 4)
+    with torch.no_grad():
+        value = base.critic_linear(base.critic(x))
+        feat = base.actor(x)
+        dist = head(feat)
+    save("mlp.npz", base_params=flat_params(base), base_names=param_names(base),
+         head_params=flat_params(head), x=x.numpy(), value=value.numpy(),
+         actor_features=feat.numpy(), norm_logits=dist.logits.numpy(),
+         entropy=dist.entropy().numpy())
+
+
+def main():
+    torch.set_num_threads(1)  # as T/run.py:55
+    S, M, D, P = load_ref("B")
+    gen_gae(S)
+    gen_advnorm(S, P)
+    gen_sampler(S)
+    gen_categorical(D)
+    gen_cnn_update(S, M, P, hidden=64, N=4, T=4, E=2, Mb=2, lr=1e-3, fname="cnn_update.npz")
+    gen_adam()
+    gen_mlp(M, D)
+    S, M, D, P = load_ref("T")
+    gen_gru(S, M, P)
+
+
+if __name__ == "__main__":
+    main()
