@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of the full PPO iteration (rollout + GAE + update),
+BASELINE.json configs[2]: CNNBase (H=512), 4096 env lanes x 128 steps per GPU,
+PPO 3 epochs x 8 minibatches, synthetic 84x84x4 u8 observations.
+
+One bench "step" = one whole T/run.py:168-248 iteration on every rank:
+  128 x (Policy.act -> synthetic env step -> RolloutStorage.insert),
+  get_value, compute_returns (GAE), PPO.update (24 minibatches of fwd + bwd +
+  [RCCL grad all-reduce] + clip + Adam), after_update.
+value = envs_per_gpu * 128 * world * K / max-over-ranks(wall time of K steps).
+
+Multi-GPU (launched by torch.distributed.run, one rank per GPU): env lanes are
+sharded (weak scaling); each minibatch's flat gradient is all-reduced over RCCL.
+
+Also reported on rank 0:
+  roofline      the dominant kernel's achieved FLOP/s from HIP events recorded
+                around each of its launches during the timed region
+  gae_roofline  fused GAE + advantage kernel on a 1M-lane buffer (> Infinity Cache)
+  cpu_baseline  the oracle's numpy port of the reference CPU path, bounded sample
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "ppo-dash_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "env-steps/sec (rollout+GAE+PPO update) at 4096 envs×128 steps, 1/2/4/8 MI355X"
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA = vector peak (dense)
+PEAK_HBM_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--envs", type=int, default=4096, help="env lanes per GPU")
+    p.add_argument("--num-steps", type=int, default=128)
+    p.add_argument("--ppo-epoch", type=int, default=3)
+    p.add_argument("--num-mini-batch", type=int, default=8)
+    p.add_argument("--hidden", type=int, default=512)
+    p.add_argument("--profile-kernel", default="conv1_fwd_u8")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-envs", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-gae-roofline", action="store_true")
+    p.add_argument("--gae-lanes", type=int, default=1 << 20)
+    return p.parse_args()
+
+
+def gae_roofline(device, lanes, T=128, reps=10):
+    """Fused GAE + advantage difference + moment partials on [T, lanes] planes.
+    Algorithmic bytes per (t, lane): read r, v_t, m_{t+1} (12 B) + write ret, adv (8 B)."""
+    from a2c_ppo_acktr._hip import call, stream
+    g = torch.Generator(device=device).manual_seed(0)
+    r = torch.rand(T, lanes, device=device, generator=g)
+    v = torch.randn(T + 1, lanes, device=device, generator=g)
+    m = (torch.rand(T + 1, lanes, device=device, generator=g) > 0.01).float()
+    nv = torch.randn(lanes, device=device, generator=g)
+    ret = torch.empty(T + 1, lanes, device=device)
+    adv = torch.empty(T, lanes, device=device)
+    parts = torch.empty(2 * call("ppo_gae_partials_count", lanes), dtype=torch.float64, device=device)
+    s = stream()
+    args = (r.data_ptr(), v.data_ptr(), m.data_ptr(), m.data_ptr(), nv.data_ptr(), ret.data_ptr(), adv.data_ptr(),
+            parts.data_ptr(), T, lanes, 0.99, 0.95, 1, 0, s)
+    call("ppo_compute_returns", *args)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        call("ppo_compute_returns", *args)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = 20.0 * T * lanes
+    gbps = nbytes / (ms * 1e-3) / 1e9
+    del r, v, m, nv, ret, adv, parts
+    torch.cuda.empty_cache()
+    return {"bound": "hbm", "achieved": round(gbps, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+            "frac": round(gbps / PEAK_HBM_GBPS, 4), "traffic": None,
+            "config": f"T={T} x {lanes} lanes (fp32 planes, {nbytes / 1e9:.2f} GB algorithmic per launch)",
+            "ms_per_launch": round(ms, 4)}
+
+
+def cpu_baseline(envs, T, E, M, hidden, threads):
+    """The oracle's numpy (fp32) restatement of the reference CPU path, timed on a
+    bounded sample: `envs` lanes x T steps, E x M minibatches."""
+    from threadpoolctl import threadpool_limits
+    from oracle import ppo_oracle as O
+    rng = np.random.default_rng(1)
+    shapes = O.cnn_param_shapes(hidden)
+    flat = np.concatenate([rng.standard_normal(int(np.prod(s))).astype(np.float32) * 0.05 for _, s in shapes])
+    obs = rng.integers(0, 256, (T + 1, envs, 4, 84, 84), dtype=np.uint8)
+    noise = rng.exponential(1.0, (T, envs, 8)).astype(np.float32)
+    rewards = rng.random((T, envs), np.float32)
+    masks = (rng.random((T, envs)) > 0.01).astype(np.float32)
+    perms = np.stack([rng.permutation(envs * T) for _ in range(E)])
+    with threadpool_limits(limits=threads):
+        t0 = time.perf_counter()
+        O.run_iteration(flat, shapes, obs, noise, rewards, masks, perms, num_mini_batch=M, dtype=np.float32)
+        dt = time.perf_counter() - t0
+    return {"value": round(envs * T / dt, 2), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle numpy fp32 port of the reference CPU path (T/run.py:168-248), CNNBase H={hidden}, "
+                      f"{envs} envs x {T} steps, {E} epochs x {M} minibatches, one iteration, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from a2c_ppo_acktr import _hip
+    from a2c_ppo_acktr.algo import PPO
+    from a2c_ppo_acktr.model import CNNBase, Policy
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import SyntheticVecEnv
+
+    N, T, E, M, H = args.envs, args.num_steps, args.ppo_epoch, args.num_mini_batch, args.hidden
+    torch.manual_seed(1)
+    env = SyntheticVecEnv(N, seed=123 + 7919 * rank, p_done=0.01, device=device)
+    policy = Policy((4, 84, 84), env.action_space, base=CNNBase, base_kwargs={"recurrent": False, "hidden_size": H})
+    policy.to(device)
+    agent = PPO(policy, 0.1, E, M, 0.5, 0.001, lr=1e-4, eps=1e-5, max_grad_norm=0.5)
+    rollouts = RolloutStorage(T, N, (4, 84, 84), [0], env.action_space, policy.recurrent_hidden_state_size,
+                              obs_dtype=torch.uint8, device=device)
+    env.reset_into(rollouts.obs[0])
+
+    def iteration():
+        for step in range(T):
+            with torch.no_grad():
+                value, action, logp, hxs = policy.act(rollouts.obs[step], rollouts.vector_obs[step],
+                                                      rollouts.recurrent_hidden_states[step], rollouts.masks[step])
+            slot = rollouts.obs[step + 1]
+            reward, masks, bad_masks = env.step_into(slot, action)
+            rollouts.insert(slot, rollouts.vector_obs[step + 1], hxs, action, logp, value, reward, masks, bad_masks)
+        with torch.no_grad():
+            next_value = policy.get_value(rollouts.obs[-1], rollouts.vector_obs[-1],
+                                          rollouts.recurrent_hidden_states[-1], rollouts.masks[-1])
+        rollouts.compute_returns(next_value, True, 0.99, 0.95, False)
+        losses = agent.update(rollouts)
+        rollouts.after_update()
+        return losses
+
+    for _ in range(args.warmup):
+        iteration()
+    torch.cuda.synchronize()
+
+    gae = None
+    if rank == 0 and not args.no_gae_roofline:
+        gae = gae_roofline(device, args.gae_lanes)
+
+    cap = args.steps * (T + 2 * E * M + 8) + 16
+    _hip.call("ppo_prof_enable", args.profile_kernel.encode(), cap)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    losses = None
+    for _ in range(args.steps):
+        losses = iteration()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = (torch.zeros(3, dtype=torch.float64))
+    _hip.call("ppo_prof_collect", prof.data_ptr())
+    _hip.call("ppo_prof_enable", None, 0)
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    launches, ms_total, flops = prof.tolist()
+    roof = None
+    if launches > 0 and ms_total > 0:
+        tflops = flops / (ms_total * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(tflops / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                "kernel": args.profile_kernel, "launches": int(launches),
+                "avg_launch_ms": round(ms_total / launches, 4),
+                "flop_per_launch": round(flops / launches)}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_envs, T, E, M, H, args.cpu_threads)
+    value = N * T * world * args.steps / elapsed
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: counter-hash u8 4x84x84 obs, U[0,1) rewards, Bernoulli(0.01) dones; random-init weights",
+        "config": {"workload": f"c3: CNNBase H={H}, {N} env lanes x {T} steps per GPU, PPO {E} epochs x {M} "
+                               f"minibatches (rollout + GAE + update, fp32)",
+                   "envs_per_gpu": N, "num_steps": T, "ppo_epoch": E, "num_mini_batch": M, "hidden": H,
+                   "global_batch": N * T * world, "parallelism": f"dp{world}"},
+        "roofline": roof, "cpu_baseline": cpu, "gae_roofline": gae,
+        "losses": [round(x, 6) for x in losses],
+    }
+    print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

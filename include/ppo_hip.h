@@ -1,0 +1,143 @@
+/*
+ * ppo_hip.h — C ABI of libppo_hip.so, the MI355X (gfx950) engine behind the
+ * a2c_ppo_acktr Policy / RolloutStorage / PPO.update() API of ppo-dash.
+ *
+ * The reference has no native code and no FFI: its
+ * boundary is the Python class API of ppo-dash-training/pytorch-a2c-ppo-acktr-gail/
+ * a2c_ppo_acktr/{storage,model,distributions}.py and algo/ppo.py, and every
+ * hot-path op is a stock PyTorch call.  Each entry point below replaces one of
+ * those calls; the citation names the reference line it stands in for
+ * (paths relative to that a2c_ppo_acktr/ directory).
+ *
+ * Conventions
+ *   - every pointer is a device pointer owned by the caller (the library never
+ *     allocates or frees caller memory); `stream` is a hipStream_t;
+ *   - calls are asynchronous on `stream`, never synchronise, and are safe from
+ *     several host threads on distinct streams;
+ *   - return 0 on success, a hipError_t or a PPO_E* code otherwise;
+ *     ppo_last_error() returns the message of the calling thread's last error;
+ *   - storage planes are [T(+1)][N] fp32 (time-major, env-minor), actions i64,
+ *     observations u8 (or f32) [rows][C][84][84]; activations NHWC fp32.
+ */
+#ifndef PPO_HIP_H
+#define PPO_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PPO_EARG 1001
+#define PPO_ESHAPE 1002
+
+const char* ppo_last_error(void);
+int ppo_abi_version(void);
+/* launch-level event profiler used by bench.py: time every launch of the named
+ * kernel (NULL disables); collect -> {launches, Σ ms, Σ algorithmic FLOP} */
+int ppo_prof_enable(const char* name, int capacity);
+int ppo_prof_collect(double* out3);
+
+/* ---------------- returns / advantages ------------------------------------ */
+/* storage.py:82-121 RolloutStorage.compute_returns (all four branches,
+ * bit-identical).  adv/partials (both or neither): also write
+ * adv = returns[:-1] - value_preds[:-1] (algo/ppo.py:35) and per-block
+ * (Σadv, Σadv²) partials, 2*ppo_gae_partials_count(N) doubles. */
+int ppo_gae_partials_count(int N);
+int ppo_compute_returns(const float* rewards, float* value_preds, const float* masks, const float* bad_masks,
+                        const float* next_value, float* returns, float* adv, double* partials, int T, int N,
+                        double gamma, double gae_lambda, int use_gae, int use_proper_time_limits, void* stream);
+/* algo/ppo.py:35 advantages = returns[:-1] - value_preds[:-1] (+ partials) */
+int ppo_adv_diff_partials_count(long long n);
+int ppo_adv_diff(const float* returns, const float* value_preds, float* adv, double* partials, long long n,
+                 void* stream);
+/* algo/ppo.py:36 advantages.mean()/std(): stats = {count, Σ, Σ²} (all-reducible) */
+int ppo_adv_finalize(const double* partials, int nparts, double count, double* stats, void* stream);
+/* algo/ppo.py:36-37 (adv - mean) / (std + 1e-5), std unbiased */
+int ppo_adv_normalize(float* adv, long long n, const double* stats, void* stream);
+
+/* ---------------- rollout storage ----------------------------------------- */
+/* storage.py:62-80 copy_ of bulk rows (insert / after_update) */
+int ppo_copy(void* dst, const void* src, long long bytes, void* stream);
+int ppo_fill_f32(float* p, long long n, float v, void* stream);
+/* storage.py:66-71 insert of the per-env scalars; any source may be NULL */
+int ppo_storage_insert_scalars(int N, int step, const int64_t* action, const float* logp, const float* value,
+                               const float* reward, const float* mask, const float* bad_mask, int64_t* actions,
+                               float* action_log_probs, float* value_preds, float* rewards, float* masks,
+                               float* bad_masks, void* stream);
+/* storage.py:143-157 feed_forward_generator `[indices]` row gathers */
+int ppo_gather_rows(const void* src, const int64_t* idx, void* dst, long long nrows, long long row_bytes,
+                    void* stream);
+/* storage.py:181-205 recurrent_generator env-column stacking */
+int ppo_gather_env_columns(const void* src, const int64_t* envs, void* dst, int T, int N, int nsel,
+                           long long row_bytes, void* stream);
+/* stands in for VecPyTorch.step + the simulator (make_env.py:58-114): u8 obs
+ * written into the storage slot, reward U[0,1), done ~ Bernoulli(p_done) */
+int ppo_synth_env_step(uint8_t* obs, int N, long long obs_bytes, float* reward, float* mask, float* bad_mask,
+                       unsigned long long seed, unsigned long long step, float p_done, void* stream);
+
+/* ---------------- CNNBase trunk (model.py:176-180) ------------------------- */
+long long ppo_packed_weights_size(int H);
+int ppo_packed_offsets(int H, long long* off6);
+/* once per optimizer step: torch-layout conv2/conv3/fc weights -> loader orders */
+int ppo_pack_weights(const float* w2, const float* w3, const float* w4, int H, float* packed, void* stream);
+/* model.py:177 Conv2d(C,32,8,s4)+ReLU over obs rows (idx: storage-row gather,
+ * storage.py:143; NULL: rows row0..row0+B-1); u8 decoded as u8/255 */
+int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B, const float* w1,
+                  const float* b1, float* out, void* stream);
+/* model.py:178 Conv2d(32,64,4,s2)+ReLU */
+int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream);
+/* model.py:179 Conv2d(64,32,3,s1)+ReLU */
+int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream);
+/* model.py:180 Linear(1568,H)+ReLU (generic Linear+ReLU) */
+int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, const float* b, int N, float* out,
+                        void* stream);
+/* algo/ppo.py:80-81 loss.backward() through the trunk: dgrad with the ReLU mask
+ * of the layer below fused, wgrad as split-K partial slabs + deterministic reduce */
+int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
+                          void* stream);
+int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream);
+int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const float* a1, float* dz1, void* stream);
+int ppo_wgrad_splits(long long R, int tiles, int target_blocks, int min_ktiles);
+int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C,
+                    int B, int Z, float* slab, float* slab_bias, void* stream);
+int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, float* slab, float* slab_bias, void* stream);
+int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, float* slab, float* slab_bias, void* stream);
+int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int K, int Z, float* slab, float* slab_bias,
+                     void* stream);
+int ppo_wgrad_reduce(const float* slab, const float* slab_bias, int Z, int M, int NW, int kind, int a, int b,
+                     float* gw, float* gb, float scale, int accumulate, void* stream);
+
+/* ---------------- heads, distribution, loss -------------------------------- */
+/* model.py:54-79 act / get_value / evaluate_actions heads + distributions.py:17-27
+ * FixedCategorical: value, logits, logsumexp, sample = argmax(probs/E) (noise =
+ * E, host replay) or counter-RNG Exp(1) (noise NULL), mode, log_probs, entropy */
+int ppo_heads_act(const float* feat, int N, int H, const float* wc, const float* bc, const float* wa,
+                  const float* ba, int A, const float* noise, unsigned long long seed, unsigned long long counter,
+                  int deterministic, const int64_t* given, float* value, int64_t* action, float* logp,
+                  float* entropy, void* stream);
+/* algo/ppo.py:57-81 evaluate_actions + clipped surrogate + clipped value loss +
+ * entropy, forward and analytic backward to dL/dfeature, head-gradient partials */
+int ppo_heads_train_blocks(int B);
+int ppo_heads_train(const float* feat, int B, int H, const float* wc, const float* bc, const float* wa,
+                    const float* ba, int A, const int64_t* idx, long long row0, const int64_t* actions,
+                    const float* old_logp, const float* adv, const float* vpred, const float* ret, float clip,
+                    float value_coef, float entropy_coef, float inv_b, int use_clipped_value_loss, float* dfeat,
+                    float* part_w, float* part_b, float* part_loss, void* stream);
+int ppo_heads_reduce(const float* part_w, const float* part_b, const float* part_loss, int nblk, int H, int A,
+                     float* g_wc, float* g_bc, float* g_wa, float* g_ba, double* loss_acc, double inv_b, float scale,
+                     int use_clipped_value_loss, void* stream);
+/* model.py:77 dist.entropy().mean() */
+int ppo_mean_f32(const float* x, long long n, float* out, void* stream);
+
+/* ---------------- clip + Adam (algo/ppo.py:82-84) -------------------------- */
+int ppo_grad_partials_count(long long n);
+int ppo_grad_sumsq(const float* g, long long n, float scale, double* partials, void* stream);
+int ppo_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, long long n,
+                  const double* partials, float scale, double max_norm, double lr, double beta1, double beta2,
+                  double eps, long long step, double* norm_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPO_HIP_H */

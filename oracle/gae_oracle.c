@@ -94,3 +94,15 @@ void oracle_adv_stats(const float *returns, const float *value_preds, int T, int
     out[0] = mean;
     out[1] = n > 1 ? sqrt(m2 / (double)(n - 1)) : NAN;
 }
+
+/* The device decode of u8 observations (common.h decode_u8): q = u*(1/255),
+ * one residual FMA correction.  Exposed so the CPU tests can check it against
+ * IEEE u/255.0f for all 256 codes. */
+float oracle_decode_u8_fma(unsigned u)
+{
+    const float r = 1.0f / 255.0f;
+    const float x = (float)u;
+    const float q = x * r;
+    const float res = fmaf(-q, 255.0f, x);
+    return fmaf(res, r, q);
+}

@@ -231,7 +231,7 @@ def _conv_bwd(dz, cols, w, x_shape, stride, need_dx=True):
 
 def cnn_trunk(p, x):
     """CNNBase.main (model.py:176-180): returns features [B,H] and the cache."""
-    x = np.asarray(x, np.float64)
+    x = np.asarray(x, p["base.main.0.weight"].dtype)
     z1, c1 = _conv_fwd(x, p["base.main.0.weight"], p["base.main.0.bias"], 4)
     a1 = np.maximum(z1, 0)
     z2, c2 = _conv_fwd(a1, p["base.main.2.weight"], p["base.main.2.bias"], 2)
@@ -356,6 +356,8 @@ def loss_head_grads(value, logits, actions, old_logp, adv, vpred_old, returns, c
 def cnn_backward(p, cache, g_value, g_logits):
     """Backward of cnn_forward for dL/dvalue [B], dL/dlogits [B,A] → grads dict."""
     h = cache["h"]
+    g_value = np.asarray(g_value, h.dtype)
+    g_logits = np.asarray(g_logits, h.dtype)
     g = {}
     g["base.critic_linear.weight"] = g_value[None, :] @ h
     g["base.critic_linear.bias"] = np.array([g_value.sum()])
@@ -395,13 +397,13 @@ def clip_adam(params, grads, m, v, step, lr, eps, max_norm, beta1=0.9, beta2=0.9
 
 def run_iteration(flat_params, shapes, obs_u8, exp_noise, rewards, masks, perms, *, num_mini_batch,
                   clip=0.1, value_coef=0.5, entropy_coef=0.001, lr=1e-4, eps=1e-5, max_grad_norm=0.5,
-                  gamma=0.99, gae_lambda=0.95):
+                  gamma=0.99, gae_lambda=0.95, dtype=np.float64):
     """One T/run.py:168-248 iteration (feed-forward CNN) replayed on recorded env
     data: obs_u8 [T+1,N,C,84,84], exp_noise [T,N,A], rewards/masks [T,N],
     perms [E, N*T] (the randperms the update draws).  Returns a dict."""
     T1, N = obs_u8.shape[:2]
     T = T1 - 1
-    p = unflatten(flat_params, shapes)
+    p = unflatten(flat_params, shapes, dtype)
     vals, acts, logps = np.zeros((T, N)), np.zeros((T, N), np.int64), np.zeros((T, N))
     for t in range(T):
         value, logits, _ = cnn_forward(p, decode_obs(obs_u8[t]))
@@ -415,7 +417,7 @@ def run_iteration(flat_params, shapes, obs_u8, exp_noise, rewards, masks, perms,
     ret, vp = compute_returns(np.asarray(rewards, np.float32).reshape(T, N), vp, mk, np.ones_like(mk),
                               nv.astype(np.float32), True, gamma, gae_lambda, False)
     adv = normalize_advantages(ret, vp)
-    flat = np.asarray(flat_params, np.float64).copy()
+    flat = np.asarray(flat_params, dtype).copy()
     m = np.zeros_like(flat)
     v = np.zeros_like(flat)
     step = 0
@@ -424,18 +426,18 @@ def run_iteration(flat_params, shapes, obs_u8, exp_noise, rewards, masks, perms,
     obs_rows = obs_u8[:T].reshape(T * N, *obs_u8.shape[2:])
     for perm in perms:
         for idx in ff_minibatches(perm, num_mini_batch):
-            p = unflatten(flat, shapes)
+            p = unflatten(flat, shapes, dtype)
             value, logits, cache = cnn_forward(p, decode_obs(obs_rows[idx]))
             lg = loss_head_grads(value, logits, acts.reshape(-1)[idx], logps.reshape(-1)[idx],
                                  adv.reshape(-1)[idx], vp[:T].reshape(-1)[idx], ret[:T].reshape(-1)[idx],
                                  clip, value_coef, entropy_coef)
-            g = flatten(cnn_backward(p, cache, lg["g_value"], lg["g_logits"]), shapes)
+            g = flatten(cnn_backward(p, cache, lg["g_value"], lg["g_logits"]), shapes).astype(dtype)
             step += 1
             flat, m, v, gc, _ = clip_adam(flat, g, m, v, step, lr, eps, max_grad_norm)
             if first is None:
                 first = dict(values=value, logp=lg["logp"], clipped_grad=gc)
             losses += [lg["value_loss"], lg["action_loss"], lg["entropy"]]
-    losses /= step
+    losses /= len(perms) * num_mini_batch   # ppo.py:90 divides by epochs x num_mini_batch
     return dict(values=vals, actions=acts, log_probs=logps, next_value=nv, returns=ret,
                 value_preds=vp, advantages=adv, final_params=flat, losses=losses, first=first,
                 last_clipped_grad=gc)

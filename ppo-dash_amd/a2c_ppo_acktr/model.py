@@ -1,0 +1,205 @@
+"""Actor-critic networks — drop-in for a2c_ppo_acktr/model.py (reference
+ppo-dash-training/pytorch-a2c-ppo-acktr-gail/a2c_ppo_acktr/model.py:10-234).
+
+The modules are built exactly as the reference builds them (same layer
+constructors, same init calls, same order), so under the same
+torch.manual_seed the initial parameters are identical.  The layers are only
+parameter containers: act / get_value / evaluate_actions run on the MI355X
+through libppo_hip.so (see _engine.py); there is no CPU compute path.
+
+Differences from the reference, all documented in DESIGN.md:
+  * CNNBase accepts uint8 observations and decodes u8/255 inside conv1.
+  * MLPBase's constructor takes (num_inputs, vector_obs_len, ...) so that
+    Policy can build it (the reference mis-calls it, model.py:28 vs :203).
+  * evaluate_actions returns values without an autograd graph; PPO.update runs
+    its own fused HIP backward.
+  * Recurrent (GRU) and MLP forward passes are not on the HIP path yet.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ._hip import require_device
+from .distributions import Bernoulli, Categorical, DiagGaussian
+from .utils import init
+
+
+class Flatten(nn.Module):
+    def forward(self, x):
+        return x.view(x.size(0), -1)
+
+
+_SAMPLING = {"mode": "device"}
+
+
+def set_sampling_mode(mode):
+    """'device' (default): Exp(1) sampling noise from a counter-based RNG on the GPU.
+    'host': draw it with torch.empty(N, A).exponential_(1) on the default CPU
+    generator — the draw torch.multinomial makes on the reference CPU path — so a
+    seeded run consumes the host generator exactly like the reference does."""
+    if mode not in ("device", "host"):
+        raise ValueError(mode)
+    _SAMPLING["mode"] = mode
+
+
+class Policy(nn.Module):
+    def __init__(self, obs_shape, action_space, base=None, base_kwargs=None, vector_obs_len=0):
+        super(Policy, self).__init__()
+        if base_kwargs is None:
+            base_kwargs = {}
+        if base is None:
+            if len(obs_shape) == 3:
+                base = CNNBase
+            elif len(obs_shape) == 1:
+                base = MLPBase
+            else:
+                raise NotImplementedError
+        self.base = base(obs_shape[0], vector_obs_len, **base_kwargs)
+        if action_space.__class__.__name__ == "Discrete":
+            num_outputs = action_space.n
+            self.dist = Categorical(self.base.output_size, num_outputs)
+        elif action_space.__class__.__name__ == "Box":
+            num_outputs = action_space.shape[0]
+            self.dist = DiagGaussian(self.base.output_size, num_outputs)
+        elif action_space.__class__.__name__ == "MultiBinary":
+            num_outputs = action_space.shape[0]
+            self.dist = Bernoulli(self.base.output_size, num_outputs)
+        else:
+            raise NotImplementedError
+        self._engine = None
+
+    @property
+    def is_recurrent(self):
+        return self.base.is_recurrent
+
+    @property
+    def recurrent_hidden_state_size(self):
+        """Size of rnn_hx."""
+        return self.base.recurrent_hidden_state_size
+
+    def forward(self, visual_inputs, vector_inputs, rnn_hxs, masks):
+        raise NotImplementedError
+
+    # ------------------------------------------------------------- engine
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st["_engine"] = None   # torch.save([actor_critic, ob_rms]) pickles the module, not the engine
+        return st
+
+    def hip_engine(self, device=None):
+        require_device()
+        if not isinstance(self.base, CNNBase) or self.base.is_recurrent:
+            raise NotImplementedError("the MI355X engine currently runs the feed-forward CNNBase policy; "
+                                      "recurrent (GRU) and MLPBase policies are on the roadmap (DESIGN.md)")
+        if not isinstance(self.dist, Categorical):
+            raise NotImplementedError("only Discrete action spaces run on the MI355X engine")
+        if device is None:
+            p = next(self.parameters())
+            device = p.device if p.is_cuda else torch.device("cuda", torch.cuda.current_device())
+        if self._engine is None or self._engine.device != device:
+            from ._engine import CNNEngine
+            if not next(self.parameters()).is_cuda:
+                self.to(device)
+            self._engine = CNNEngine(self, device)
+        self._engine.ensure_bound()
+        return self._engine
+
+    def _noise(self, n):
+        if _SAMPLING["mode"] == "host":
+            return torch.empty(n, self.dist.linear.weight.shape[0]).exponential_(1)
+        return None
+
+    # ----------------------------------------------------------------- API
+    def act(self, visual_inputs, vector_inputs, rnn_hxs, masks, deterministic=False):
+        """model.py:54-66 -> (value [N,1], action [N,1] int64, action_log_probs [N,1], rnn_hxs)."""
+        eng = self.hip_engine()
+        n = visual_inputs.shape[0]
+        noise = None if deterministic else self._noise(n)
+        value, action, logp, _ = eng.act(visual_inputs, deterministic=deterministic, noise=noise)
+        return value, action, logp, rnn_hxs
+
+    def get_value(self, visual_inputs, vector_inputs, rnn_hxs, masks):
+        """model.py:68-70."""
+        value, _, _, _ = self.hip_engine().act(visual_inputs, value_only=True)
+        return value
+
+    def evaluate_actions(self, visual_inputs, vector_inputs, rnn_hxs, masks, action):
+        """model.py:72-79 -> (value [B,1], action_log_probs [B,1], dist_entropy (0-d), rnn_hxs)."""
+        eng = self.hip_engine()
+        action = action.to(eng.device, torch.int64)
+        value, _, logp, ent = eng.act(visual_inputs, given=action, want_entropy=True)
+        return value, logp, ent.mean(), rnn_hxs
+
+
+class NNBase(nn.Module):
+    def __init__(self, recurrent, recurrent_input_size, hidden_size):
+        super(NNBase, self).__init__()
+        self._hidden_size = hidden_size
+        self._recurrent = recurrent
+        if recurrent:
+            self.gru = nn.GRU(recurrent_input_size, hidden_size)
+            for name, param in self.gru.named_parameters():
+                if 'bias' in name:
+                    nn.init.constant_(param, 0)
+                elif 'weight' in name:
+                    nn.init.orthogonal_(param)
+
+    @property
+    def is_recurrent(self):
+        return self._recurrent
+
+    @property
+    def recurrent_hidden_state_size(self):
+        if self._recurrent:
+            return self._hidden_size
+        return 1
+
+    @property
+    def output_size(self):
+        return self._hidden_size
+
+
+class CNNBase(NNBase):
+    """model.py:169-199: conv 8/4 -> conv 4/2 -> conv 3/1 -> fc(1568, H), ReLU after each."""
+
+    def __init__(self, num_inputs, vector_obs_len=0, recurrent=False, hidden_size=512):
+        super(CNNBase, self).__init__(recurrent, hidden_size + vector_obs_len, hidden_size)
+        init_ = lambda m: init(m, nn.init.orthogonal_, lambda x: nn.init.constant_(x, 0),
+                               nn.init.calculate_gain('relu'))
+        self.main = nn.Sequential(
+            init_(nn.Conv2d(num_inputs, 32, 8, stride=4)), nn.ReLU(),
+            init_(nn.Conv2d(32, 64, 4, stride=2)), nn.ReLU(),
+            init_(nn.Conv2d(64, 32, 3, stride=1)), nn.ReLU(), Flatten(),
+            init_(nn.Linear(32 * 7 * 7, hidden_size)), nn.ReLU())
+        init_ = lambda m: init(m, nn.init.orthogonal_, lambda x: nn.init.constant_(x, 0))
+        if recurrent:
+            self.critic_linear = init_(nn.Linear(hidden_size, 1))
+        else:
+            self.critic_linear = init_(nn.Linear(hidden_size + vector_obs_len, 1))
+        self.vector_obs_len = vector_obs_len
+        self.train()
+
+    def forward(self, visual_inputs, vector_inputs, rnn_hxs, masks):
+        raise NotImplementedError("CNNBase runs through Policy.act/get_value/evaluate_actions on the HIP engine")
+
+
+class MLPBase(NNBase):
+    """model.py:202-234 (constructor signature fixed so Policy can build it)."""
+
+    def __init__(self, num_inputs, vector_obs_len=0, recurrent=False, hidden_size=64):
+        super(MLPBase, self).__init__(recurrent, num_inputs + vector_obs_len, hidden_size)
+        num_inputs = num_inputs + vector_obs_len
+        if recurrent:
+            num_inputs = hidden_size
+        init_ = lambda m: init(m, nn.init.orthogonal_, lambda x: nn.init.constant_(x, 0), np.sqrt(2))
+        self.actor = nn.Sequential(
+            init_(nn.Linear(num_inputs, hidden_size)), nn.Tanh(),
+            init_(nn.Linear(hidden_size, hidden_size)), nn.Tanh())
+        self.critic = nn.Sequential(
+            init_(nn.Linear(num_inputs, hidden_size)), nn.Tanh(),
+            init_(nn.Linear(hidden_size, hidden_size)), nn.Tanh())
+        self.critic_linear = init_(nn.Linear(hidden_size, 1))
+        self.train()
+
+    def forward(self, visual_inputs, vector_inputs, rnn_hxs, masks):
+        raise NotImplementedError("MLPBase is not on the HIP path yet (DESIGN.md roadmap)")

@@ -1,0 +1,91 @@
+// Shared helpers for libppo_hip.so (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/ppo_hip.h"  // every PPO_API definition must match its declaration
+
+#define PPO_API extern "C" __attribute__((visibility("default")))
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Error plumbing: every C-ABI entry point returns 0 on success, a hipError_t
+// value or a library code otherwise; ppo_last_error() returns the message.
+void ppo_set_error(const char* fmt, ...);
+
+#define PPO_REQUIRE(cond, ...)                                                       \
+  do {                                                                               \
+    if (!(cond)) {                                                                   \
+      ppo_set_error(__VA_ARGS__);                                                    \
+      return PPO_EARG;                                                               \
+    }                                                                                \
+  } while (0)
+
+#define PPO_LAUNCH_CHECK(name)                                                       \
+  do {                                                                               \
+    hipError_t _e = hipGetLastError();                                               \
+    if (_e != hipSuccess) {                                                          \
+      ppo_set_error("%s: launch failed: %s", name, hipGetErrorString(_e));           \
+      return (int)_e;                                                                \
+    }                                                                                \
+  } while (0)
+
+#define PPO_HIP_CHECK(expr, name)                                                    \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess) {                                                          \
+      ppo_set_error("%s: %s", name, hipGetErrorString(_e));                          \
+      return (int)_e;                                                                \
+    }                                                                                \
+  } while (0)
+
+// Launch-level event profiler (bench.py roofline): launches whose name matches
+// the enabled one are bracketed by hipEventRecord on their stream and tagged
+// with their algorithmic FLOP (or byte) count.
+bool ppo_prof_begin(const char* name, hipStream_t st, int* slot);
+void ppo_prof_end(int slot, hipStream_t st, double work);
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline unsigned ceil_div(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// u8 -> fp32 decode, bit-identical to (float)u / 255.0f (IEEE divide), which is
+// the oracle's input convention u8.float()/255.0.  q = u*(1/255)
+// is wrong for 126 of the 256 codes; one residual FMA correction makes all 256
+// exact (checked exhaustively on the host, tests/test_host_logic.py).
+__device__ __forceinline__ float decode_u8(uint32_t u) {
+  const float r = 1.0f / 255.0f;
+  const float x = (float)u;
+  const float q = x * r;
+  const float res = __builtin_fmaf(-q, 255.0f, x);
+  return __builtin_fmaf(res, r, q);
+}
+
+// Counter-based hash RNG (splitmix64 finaliser) for the device sampling noise
+// and the synthetic environment.
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// uniform in (0, 1]: 24 random bits
+__host__ __device__ __forceinline__ float u01_open0(uint64_t h) {
+  return ((float)((uint32_t)(h >> 40)) + 1.0f) * (1.0f / 16777216.0f);
+}

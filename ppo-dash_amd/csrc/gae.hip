@@ -1,0 +1,248 @@
+// GAE-λ / discounted returns (K3) fused with the advantage difference and its
+// moment partials (K4).  Compiled with -ffp-contract=off: results are
+// bit-identical to the reference CPU path (tests/golden/gae.npz).
+//
+// Reference: RolloutStorage.compute_returns,
+//   ppo-dash-training/pytorch-a2c-ppo-acktr-gail/a2c_ppo_acktr/storage.py:82-121
+// Advantages: algo/ppo.py:35-37.
+//
+// Layout (HBM): every per-step scalar lives in its own [T(+1)][N] fp32 plane
+// (time-major, env-minor — the reference's [T(+1), N, 1] tensors), so lane n of
+// a wave reads/writes element n of a row: 256-B coalesced per wave per plane.
+//
+// One thread owns one env lane and walks time backwards (the recurrence is
+// sequential in t).  Loads for U future steps are issued before the dependent
+// arithmetic so each wave keeps 3-4·U loads in flight; with ≥16k lanes per
+// launch this streams at the HBM rate (bench.py gae roofline).
+#include "common.h"
+
+namespace {
+
+constexpr int GAE_THREADS = 256;
+constexpr int GAE_U = 8;  // time steps prefetched per chunk
+
+template <bool USE_GAE, bool PTL, bool FUSE_ADV>
+__global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
+    const float* __restrict__ rewards, float* __restrict__ value_preds,
+    const float* __restrict__ masks, const float* __restrict__ bad_masks,
+    const float* __restrict__ next_value, float* __restrict__ returns,
+    float* __restrict__ adv, double* __restrict__ partials, int T, int N, float g, float gl) {
+  const int n = blockIdx.x * GAE_THREADS + threadIdx.x;
+  double s = 0.0, q = 0.0;
+  if (n < N) {
+    const size_t NN = (size_t)N;
+    const float nv = next_value[n];
+    float carry;  // gae (USE_GAE) or returns[t+1] (non-GAE)
+    float vnext = nv;
+    if (USE_GAE) {
+      value_preds[(size_t)T * NN + n] = nv;  // storage.py:90/:108
+      carry = 0.0f;
+    } else {
+      returns[(size_t)T * NN + n] = nv;      // storage.py:101/:118
+      carry = nv;
+    }
+    for (int t0 = T - 1; t0 >= 0; t0 -= GAE_U) {
+      float rr[GAE_U], vv[GAE_U], mm[GAE_U], bb[GAE_U];
+#pragma unroll
+      for (int j = 0; j < GAE_U; ++j) {
+        const int t = t0 - j;
+        if (t >= 0) {
+          rr[j] = rewards[(size_t)t * NN + n];
+          mm[j] = masks[(size_t)(t + 1) * NN + n];
+          vv[j] = (USE_GAE || PTL || FUSE_ADV) ? value_preds[(size_t)t * NN + n] : 0.0f;
+          bb[j] = PTL ? bad_masks[(size_t)(t + 1) * NN + n] : 1.0f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < GAE_U; ++j) {
+        const int t = t0 - j;
+        if (t >= 0) {
+          float out;
+          if (USE_GAE) {
+            float a = g * vnext;               // gamma * value_preds[t+1]
+            a = a * mm[j];                     //   * masks[t+1]
+            float delta = rr[j] + a;           // rewards[t] + ...
+            delta = delta - vv[j];             //   - value_preds[t]
+            float b = gl * mm[j];              // (gamma*gae_lambda) * masks[t+1]
+            b = b * carry;                     //   * gae
+            carry = delta + b;
+            if (PTL) carry = carry * bb[j];    // gae * bad_masks[t+1]
+            out = carry + vv[j];               // returns[t] = gae + value_preds[t]
+            vnext = vv[j];
+          } else {
+            float x = carry * g;               // returns[t+1] * gamma
+            x = x * mm[j];                     //   * masks[t+1]
+            x = x + rr[j];                     //   + rewards[t]
+            if (PTL) {
+              x = x * bb[j];
+              float keep = 1.0f - bb[j];
+              keep = keep * vv[j];
+              x = x + keep;
+            }
+            out = x;
+            carry = x;
+          }
+          returns[(size_t)t * NN + n] = out;
+          if (FUSE_ADV) {
+            const float d = out - vv[j];       // returns[:-1] - value_preds[:-1]
+            adv[(size_t)t * NN + n] = d;
+            s += (double)d;
+            q += (double)d * (double)d;
+          }
+        }
+      }
+    }
+  }
+  if (FUSE_ADV) {
+    __shared__ double red[2][GAE_THREADS / 64];
+    s = wave_sum_d(s);
+    q = wave_sum_d(q);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = s; red[1][w] = q; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double ss = 0.0, qq = 0.0;
+      for (int i = 0; i < GAE_THREADS / 64; ++i) { ss += red[0][i]; qq += red[1][i]; }
+      partials[2 * blockIdx.x] = ss;
+      partials[2 * blockIdx.x + 1] = qq;
+    }
+  }
+}
+
+// adv = returns - value_preds over the first T rows, plus moment partials
+// (used when storage was modified after compute_returns).
+__global__ __launch_bounds__(256) void adv_diff_kernel(const float* __restrict__ returns,
+                                                       const float* __restrict__ value_preds,
+                                                       float* __restrict__ adv,
+                                                       double* __restrict__ partials, long long n) {
+  double s = 0.0, q = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float d = returns[i] - value_preds[i];
+    adv[i] = d;
+    s += (double)d;
+    q += (double)d * (double)d;
+  }
+  __shared__ double red[2][4];
+  s = wave_sum_d(s);
+  q = wave_sum_d(q);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = s; red[1][w] = q; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    partials[2 * blockIdx.x + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
+// Deterministic fixed-order sum of the block partials -> stats {count, S, Q}.
+__global__ __launch_bounds__(256) void adv_finalize_kernel(const double* __restrict__ partials, int nparts,
+                                                           double count, double* __restrict__ stats) {
+  double s = 0.0, q = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) {
+    s += partials[2 * i];
+    q += partials[2 * i + 1];
+  }
+  __shared__ double rs[256], rq[256];
+  rs[threadIdx.x] = s;
+  rq[threadIdx.x] = q;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      rs[threadIdx.x] += rs[threadIdx.x + o];
+      rq[threadIdx.x] += rq[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    stats[0] = count;
+    stats[1] = rs[0];
+    stats[2] = rq[0];
+  }
+}
+
+// adv = (adv - mean) / (std + 1e-5) in fp32, mean/std from the (possibly
+// all-reduced) stats {count, S, Q}; std is unbiased (torch.std default).
+__global__ __launch_bounds__(256) void adv_normalize_kernel(float* __restrict__ adv, long long n,
+                                                            const double* __restrict__ stats) {
+  const double cnt = stats[0];
+  const double mean = stats[1] / cnt;
+  double var = (stats[2] - stats[1] * mean) / (cnt - 1.0);
+  if (var < 0.0) var = 0.0;
+  const float mf = (float)mean;
+  const float den = (float)sqrt(var) + 1e-5f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float a = adv[i] - mf;
+    adv[i] = a / den;
+  }
+}
+
+template <bool G, bool P, bool F>
+int launch_gae(const float* r, float* v, const float* m, const float* bm, const float* nv, float* ret,
+               float* adv, double* partials, int T, int N, float g, float gl, hipStream_t st) {
+  gae_kernel<G, P, F><<<ceil_div(N, GAE_THREADS), GAE_THREADS, 0, st>>>(r, v, m, bm, nv, ret, adv, partials,
+                                                                       T, N, g, gl);
+  PPO_LAUNCH_CHECK("gae_kernel");
+  return 0;
+}
+
+}  // namespace
+
+PPO_API int ppo_gae_partials_count(int N) { return (int)ceil_div(N, GAE_THREADS); }
+
+// storage.py:82-121 (+ ppo.py:35 when adv != NULL).  value_preds[T] is
+// overwritten with next_value in the GAE branches, returns[T] with next_value
+// otherwise — exactly the reference's side effects.
+PPO_API int ppo_compute_returns(const float* rewards, float* value_preds, const float* masks,
+                                const float* bad_masks, const float* next_value, float* returns, float* adv,
+                                double* partials, int T, int N, double gamma, double gae_lambda, int use_gae,
+                                int use_proper_time_limits, void* stream) {
+  PPO_REQUIRE(T > 0 && N > 0, "ppo_compute_returns: bad shape T=%d N=%d", T, N);
+  PPO_REQUIRE(rewards && value_preds && masks && next_value && returns, "ppo_compute_returns: null pointer");
+  PPO_REQUIRE(!use_proper_time_limits || bad_masks, "ppo_compute_returns: bad_masks required");
+  PPO_REQUIRE((adv == nullptr) == (partials == nullptr), "ppo_compute_returns: adv and partials go together");
+  const float g = (float)gamma;
+  const float gl = (float)(gamma * gae_lambda);  // Python double product, then fp32
+  hipStream_t st = as_stream(stream);
+  const bool F = adv != nullptr;
+  if (use_gae) {
+    if (use_proper_time_limits)
+      return F ? launch_gae<true, true, true>(rewards, value_preds, masks, bad_masks, next_value, returns, adv, partials, T, N, g, gl, st)
+               : launch_gae<true, true, false>(rewards, value_preds, masks, bad_masks, next_value, returns, adv, partials, T, N, g, gl, st);
+    return F ? launch_gae<true, false, true>(rewards, value_preds, masks, bad_masks, next_value, returns, adv, partials, T, N, g, gl, st)
+             : launch_gae<true, false, false>(rewards, value_preds, masks, bad_masks, next_value, returns, adv, partials, T, N, g, gl, st);
+  }
+  if (use_proper_time_limits)
+    return F ? launch_gae<false, true, true>(rewards, value_preds, masks, bad_masks, next_value, returns, adv, partials, T, N, g, gl, st)
+             : launch_gae<false, true, false>(rewards, value_preds, masks, bad_masks, next_value, returns, adv, partials, T, N, g, gl, st);
+  return F ? launch_gae<false, false, true>(rewards, value_preds, masks, bad_masks, next_value, returns, adv, partials, T, N, g, gl, st)
+           : launch_gae<false, false, false>(rewards, value_preds, masks, bad_masks, next_value, returns, adv, partials, T, N, g, gl, st);
+}
+
+PPO_API int ppo_adv_diff_partials_count(long long n) {
+  long long b = (n + 255) / 256;
+  return (int)(b < 2048 ? b : 2048);
+}
+
+PPO_API int ppo_adv_diff(const float* returns, const float* value_preds, float* adv, double* partials,
+                         long long n, void* stream) {
+  PPO_REQUIRE(n > 0, "ppo_adv_diff: n=%lld", n);
+  const int blocks = ppo_adv_diff_partials_count(n);
+  adv_diff_kernel<<<blocks, 256, 0, as_stream(stream)>>>(returns, value_preds, adv, partials, n);
+  PPO_LAUNCH_CHECK("adv_diff_kernel");
+  return 0;
+}
+
+PPO_API int ppo_adv_finalize(const double* partials, int nparts, double count, double* stats, void* stream) {
+  PPO_REQUIRE(nparts > 0, "ppo_adv_finalize: nparts=%d", nparts);
+  adv_finalize_kernel<<<1, 256, 0, as_stream(stream)>>>(partials, nparts, count, stats);
+  PPO_LAUNCH_CHECK("adv_finalize_kernel");
+  return 0;
+}
+
+PPO_API int ppo_adv_normalize(float* adv, long long n, const double* stats, void* stream) {
+  PPO_REQUIRE(n > 0, "ppo_adv_normalize: n=%lld", n);
+  long long b = (n + 255) / 256;
+  adv_normalize_kernel<<<(unsigned)(b < 4096 ? b : 4096), 256, 0, as_stream(stream)>>>(adv, n, stats);
+  PPO_LAUNCH_CHECK("adv_normalize_kernel");
+  return 0;
+}

@@ -1,0 +1,456 @@
+// Actor-critic heads, Categorical distribution and the PPO loss (K13-K15).
+//
+// Reference:
+//   critic_linear / Categorical.linear  model.py:182-199, distributions.py:54-68
+//   FixedCategorical sample / log_probs / mode / entropy  distributions.py:17-27
+//     (torch Categorical: logits -= logsumexp; probs = softmax(logits);
+//      sample = multinomial(probs,1) = argmax(probs / E), E ~ Exp(1);
+//      entropy = -Σ logits*probs)
+//   Policy.act / evaluate_actions  model.py:54-79
+//   PPO clipped surrogate + clipped value loss + entropy  algo/ppo.py:61-81
+//
+// One wave owns one row at a time.  Lane l holds hidden features
+// j = l + 64c (c < HC, H = 64·HC); the head weights for those columns stay in
+// registers for all rows the wave processes.  The 1+A head dot products are
+// wave-reduced with xor shuffles, so every lane holds value and logits and the
+// softmax/sampling/loss arithmetic is computed redundantly (no LDS traffic).
+//
+// The training kernel is the fused forward + backward of everything above the
+// fc layer: loss terms, dL/dlogits and dL/dvalue (analytic, with autograd's
+// tie conventions), dL/dfeature masked by the fc ReLU, and per-block partial
+// sums of the head weight/bias gradients (deterministic reduce afterwards).
+#include "common.h"
+
+namespace {
+
+constexpr int HW = 4;  // waves per block
+
+template <int HC, int AMAX>
+struct HeadW {
+  float wc[HC];
+  float wa[AMAX][HC];
+};
+
+template <int HC, int AMAX>
+__device__ __forceinline__ void load_head_w(HeadW<HC, AMAX>& w, const float* __restrict__ wc,
+                                            const float* __restrict__ wa, int A, int H, int lane) {
+#pragma unroll
+  for (int c = 0; c < HC; ++c) w.wc[c] = wc[lane + 64 * c];
+#pragma unroll
+  for (int o = 0; o < AMAX; ++o)
+#pragma unroll
+    for (int c = 0; c < HC; ++c) w.wa[o][c] = o < A ? wa[o * H + lane + 64 * c] : 0.f;
+}
+
+// value and logits of one row (all lanes end up with the totals)
+template <int HC, int AMAX>
+__device__ __forceinline__ void head_dots(const HeadW<HC, AMAX>& w, const float (&f)[HC], float& value,
+                                          float (&z)[AMAX], float bc, const float* __restrict__ ba, int A) {
+  float v = 0.f;
+#pragma unroll
+  for (int c = 0; c < HC; ++c) v += f[c] * w.wc[c];
+  value = wave_sum(v) + bc;
+#pragma unroll
+  for (int o = 0; o < AMAX; ++o) {
+    if (o < A) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < HC; ++c) s += f[c] * w.wa[o][c];
+      z[o] = wave_sum(s) + ba[o];
+    } else {
+      z[o] = -INFINITY;
+    }
+  }
+}
+
+// torch Categorical(logits=z): nl = z - logsumexp(z); p = softmax(nl)
+template <int AMAX>
+__device__ __forceinline__ void categorical(const float (&z)[AMAX], int A, float (&nl)[AMAX], float (&p)[AMAX]) {
+  float mx = z[0];
+#pragma unroll
+  for (int o = 1; o < AMAX; ++o)
+    if (o < A) mx = fmaxf(mx, z[o]);
+  float se = 0.f;
+#pragma unroll
+  for (int o = 0; o < AMAX; ++o)
+    if (o < A) se += expf(z[o] - mx);
+  const float lse = mx + logf(se);
+  float m2 = -INFINITY;
+#pragma unroll
+  for (int o = 0; o < AMAX; ++o) {
+    nl[o] = o < A ? z[o] - lse : -INFINITY;
+    if (o < A) m2 = fmaxf(m2, nl[o]);
+  }
+  float s2 = 0.f;
+#pragma unroll
+  for (int o = 0; o < AMAX; ++o) {
+    p[o] = o < A ? expf(nl[o] - m2) : 0.f;
+    s2 += p[o];
+  }
+#pragma unroll
+  for (int o = 0; o < AMAX; ++o) p[o] = p[o] / s2;
+}
+
+__device__ __forceinline__ float exp_noise(uint64_t seed, uint64_t counter, long long row, int o, int A) {
+  const uint64_t h = mix64(seed ^ mix64(counter * 0x2545F4914F6CDD1Dull + (uint64_t)(row * A + o)));
+  return -logf(u01_open0(h));
+}
+
+// act / evaluate: value, action (sample | mode | given), log_prob, entropy
+template <int HC, int AMAX>
+__global__ __launch_bounds__(64 * HW) void heads_act_kernel(
+    const float* __restrict__ feat, int N, int H, const float* __restrict__ wc, const float* __restrict__ bc,
+    const float* __restrict__ wa, const float* __restrict__ ba, int A, const float* __restrict__ noise,
+    unsigned long long seed, unsigned long long counter, int deterministic, const int64_t* __restrict__ given,
+    float* __restrict__ value_out, int64_t* __restrict__ action_out, float* __restrict__ logp_out,
+    float* __restrict__ ent_out, int rows_per_wave) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  HeadW<HC, AMAX> w;
+  load_head_w(w, wc, wa, A, H, lane);
+  const float b0 = bc[0];
+  const long long r0 = ((long long)blockIdx.x * HW + wave) * rows_per_wave;
+  for (int rr = 0; rr < rows_per_wave; ++rr) {
+    const long long row = r0 + rr;
+    if (row >= N) break;
+    float f[HC];
+#pragma unroll
+    for (int c = 0; c < HC; ++c) f[c] = feat[row * H + lane + 64 * c];
+    float value, z[AMAX], nl[AMAX], p[AMAX];
+    head_dots(w, f, value, z, b0, ba, A);
+    categorical(z, A, nl, p);
+    int act;
+    if (given) {
+      act = (int)given[row];
+    } else {
+      act = 0;
+      float best = -INFINITY;
+#pragma unroll
+      for (int o = 0; o < AMAX; ++o) {
+        if (o < A) {
+          const float sc = deterministic ? p[o] : p[o] / (noise ? noise[row * A + o] : exp_noise(seed, counter, row, o, A));
+          if (sc > best) { best = sc; act = o; }
+        }
+      }
+    }
+    float lp = 0.f, ent = 0.f;
+#pragma unroll
+    for (int o = 0; o < AMAX; ++o) {
+      if (o == act) lp = nl[o];
+      if (o < A) ent -= nl[o] * p[o];
+    }
+    if (lane == 0) {
+      if (value_out) value_out[row] = value;
+      if (action_out) action_out[row] = act;
+      if (logp_out) logp_out[row] = lp;
+      if (ent_out) ent_out[row] = ent;
+    }
+  }
+}
+
+struct TrainArgs {
+  const float* feat;  // [B][H] post-ReLU fc output
+  int B, H, A;
+  const float *wc, *bc, *wa, *ba;
+  const int64_t* idx;      // storage row of each sample (nullable: row0 + b)
+  long long row0;
+  const int64_t* actions;  // storage planes, indexed by storage row
+  const float *old_logp, *adv, *vpred, *ret;
+  float clip, value_coef, entropy_coef, inv_b;
+  int use_clipped_value_loss;
+  float* dfeat;            // [B][H] dL/d(fc pre-activation)
+  float* part_w;           // [blocks][1+A][H]
+  float* part_b;           // [blocks][1+A]
+  float* part_loss;        // [blocks][3]: Σ max(l1,l2), Σ min(s1,s2), Σ H
+  int rows_per_wave;
+};
+
+template <int HC, int AMAX>
+__global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int H = a.H, A = a.A;
+  HeadW<HC, AMAX> w;
+  load_head_w(w, a.wc, a.wa, A, H, lane);
+  const float b0 = a.bc[0];
+  float gwc[HC], gwa[AMAX][HC], gbc = 0.f, gba[AMAX];
+#pragma unroll
+  for (int c = 0; c < HC; ++c) gwc[c] = 0.f;
+#pragma unroll
+  for (int o = 0; o < AMAX; ++o) {
+    gba[o] = 0.f;
+#pragma unroll
+    for (int c = 0; c < HC; ++c) gwa[o][c] = 0.f;
+  }
+  float s_vl = 0.f, s_al = 0.f, s_ent = 0.f;
+  const float clip = a.clip;
+  const long long r0 = ((long long)blockIdx.x * HW + wave) * a.rows_per_wave;
+  for (int rr = 0; rr < a.rows_per_wave; ++rr) {
+    const long long row = r0 + rr;
+    if (row >= a.B) break;
+    float f[HC];
+#pragma unroll
+    for (int c = 0; c < HC; ++c) f[c] = a.feat[row * H + lane + 64 * c];
+    float value, z[AMAX], nl[AMAX], p[AMAX];
+    head_dots(w, f, value, z, b0, a.ba, A);
+    categorical(z, A, nl, p);
+    const long long sr = a.idx ? (long long)a.idx[row] : a.row0 + row;
+    const int act = (int)a.actions[sr];
+    float lp = 0.f, ent = 0.f;
+#pragma unroll
+    for (int o = 0; o < AMAX; ++o) {
+      if (o == act) lp = nl[o];
+      if (o < A) ent -= nl[o] * p[o];
+    }
+    // action loss (ppo.py:61-66)
+    const float adv = a.adv[sr];
+    const float ratio = expf(lp - a.old_logp[sr]);
+    const float surr1 = ratio * adv;
+    const float rc = fminf(fmaxf(ratio, 1.0f - clip), 1.0f + clip);
+    const float surr2 = rc * adv;
+    const float w1 = surr1 < surr2 ? 1.f : (surr1 == surr2 ? 0.5f : 0.f);
+    const float inr = (ratio >= 1.0f - clip && ratio <= 1.0f + clip) ? 1.f : 0.f;
+    const float g_logp = -a.inv_b * (w1 * adv + (1.f - w1) * adv * inr) * ratio;
+    // value loss (ppo.py:68-77)
+    const float vo = a.vpred[sr], R = a.ret[sr];
+    float g_v, vl_row;
+    if (a.use_clipped_value_loss) {
+      const float dv = value - vo;
+      const float vpc = vo + fminf(fmaxf(dv, -clip), clip);
+      const float l1 = (value - R) * (value - R);
+      const float l2 = (vpc - R) * (vpc - R);
+      vl_row = fmaxf(l1, l2);
+      const float u1 = l1 > l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+      const float vin = (dv >= -clip && dv <= clip) ? 1.f : 0.f;
+      g_v = a.value_coef * 0.5f * a.inv_b * (u1 * 2.f * (value - R) + (1.f - u1) * 2.f * (vpc - R) * vin);
+    } else {
+      vl_row = (R - value) * (R - value);
+      g_v = a.value_coef * a.inv_b * (value - R);
+    }
+    s_vl += vl_row;
+    s_al += fminf(surr1, surr2);
+    s_ent += ent;
+    // dL/dlogits = g_logp (onehot - p) + (c_e/B) p (nl + H)
+    float gz[AMAX];
+    const float ce = a.entropy_coef * a.inv_b;
+#pragma unroll
+    for (int o = 0; o < AMAX; ++o)
+      gz[o] = o < A ? g_logp * ((o == act ? 1.f : 0.f) - p[o]) + ce * p[o] * (nl[o] + ent) : 0.f;
+    // dL/dh for this lane's columns, masked by the fc ReLU; head grads
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+      float d = g_v * w.wc[c];
+#pragma unroll
+      for (int o = 0; o < AMAX; ++o) d += gz[o] * w.wa[o][c];
+      a.dfeat[row * H + lane + 64 * c] = f[c] > 0.f ? d : 0.f;
+      gwc[c] += g_v * f[c];
+#pragma unroll
+      for (int o = 0; o < AMAX; ++o) gwa[o][c] += gz[o] * f[c];
+    }
+    gbc += g_v;
+#pragma unroll
+    for (int o = 0; o < AMAX; ++o) gba[o] += gz[o];
+  }
+  // block reduction of the head-gradient partials across the HW waves
+  __shared__ float red[HW][64 * HC];
+  __shared__ float redb[HW][AMAX + 4];
+  const int NO = 1 + A;
+  for (int o = 0; o < NO; ++o) {
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+      float v = gwc[c];
+#pragma unroll
+      for (int q = 0; q < AMAX; ++q)
+        if (o == q + 1) v = gwa[q][c];
+      red[wave][lane + 64 * c] = v;
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int c = 0; c < HC; ++c) {
+        const int j = lane + 64 * c;
+        float s = red[0][j];
+        for (int q = 1; q < HW; ++q) s += red[q][j];
+        a.part_w[((size_t)blockIdx.x * NO + o) * H + j] = s;
+      }
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {
+    redb[wave][0] = gbc;
+#pragma unroll
+    for (int o = 0; o < AMAX; ++o) redb[wave][1 + o] = gba[o];
+    redb[wave][AMAX + 1] = s_vl;
+    redb[wave][AMAX + 2] = s_al;
+    redb[wave][AMAX + 3] = s_ent;
+  }
+  __syncthreads();
+  if (threadIdx.x < NO) {
+    float s = 0.f;
+    for (int q = 0; q < HW; ++q) s += redb[q][threadIdx.x];
+    a.part_b[(size_t)blockIdx.x * NO + threadIdx.x] = s;
+  }
+  if (threadIdx.x < 3) {
+    float s = 0.f;
+    for (int q = 0; q < HW; ++q) s += redb[q][AMAX + 1 + threadIdx.x];
+    a.part_loss[(size_t)blockIdx.x * 3 + threadIdx.x] = s;
+  }
+}
+
+// Σ over blocks (fixed order) of the head partials -> gradient planes;
+// loss partials -> acc[0..2] += {0.5·Σvl/B, -Σal/B, Σent/B} (double).
+__global__ __launch_bounds__(256) void heads_reduce_kernel(const float* __restrict__ part_w,
+                                                           const float* __restrict__ part_b,
+                                                           const float* __restrict__ part_loss, int nblk, int H,
+                                                           int A, float* __restrict__ g_wc, float* __restrict__ g_bc,
+                                                           float* __restrict__ g_wa, float* __restrict__ g_ba,
+                                                           double* __restrict__ loss_acc, double inv_b, float scale,
+                                                           int use_clipped) {
+  const int NO = 1 + A;
+  const long long total = (long long)NO * H;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    float s = 0.f;
+    for (int b = 0; b < nblk; ++b) s += part_w[(size_t)b * total + i];
+    s *= scale;
+    const int o = (int)(i / H), j = (int)(i % H);
+    if (o == 0) g_wc[j] = s;
+    else g_wa[(size_t)(o - 1) * H + j] = s;
+  }
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < NO) {
+      float s = 0.f;
+      for (int b = 0; b < nblk; ++b) s += part_b[(size_t)b * NO + threadIdx.x];
+      s *= scale;
+      if (threadIdx.x == 0) g_bc[0] = s;
+      else g_ba[threadIdx.x - 1] = s;
+    }
+    if (threadIdx.x >= 64 && threadIdx.x < 67 && loss_acc) {
+      const int q = threadIdx.x - 64;
+      double s = 0.0;
+      for (int b = 0; b < nblk; ++b) s += (double)part_loss[(size_t)b * 3 + q];
+      const double c = q == 0 ? (use_clipped ? 0.5 : 0.5) : (q == 1 ? -1.0 : 1.0);
+      loss_acc[q] += c * s * inv_b;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void mean_kernel(const float* __restrict__ x, long long n, float* __restrict__ out) {
+  double s = 0.0;
+  for (long long i = threadIdx.x; i < n; i += 256) s += (double)x[i];
+  __shared__ double r[256];
+  r[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) r[threadIdx.x] += r[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)(r[0] / (double)n);
+}
+
+template <int HC, int AMAX>
+int launch_act(const float* feat, int N, int H, const float* wc, const float* bc, const float* wa, const float* ba,
+               int A, const float* noise, unsigned long long seed, unsigned long long counter, int det,
+               const int64_t* given, float* v, int64_t* act, float* lp, float* ent, hipStream_t st) {
+  const int rpw = 8;
+  const unsigned blocks = ceil_div(N, HW * rpw);
+  heads_act_kernel<HC, AMAX><<<blocks, 64 * HW, 0, st>>>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det,
+                                                        given, v, act, lp, ent, rpw);
+  PPO_LAUNCH_CHECK("heads_act_kernel");
+  return 0;
+}
+
+template <int AMAX>
+int dispatch_act(int HC, const float* feat, int N, int H, const float* wc, const float* bc, const float* wa,
+                 const float* ba, int A, const float* noise, unsigned long long seed, unsigned long long counter,
+                 int det, const int64_t* given, float* v, int64_t* act, float* lp, float* ent, hipStream_t st) {
+  switch (HC) {
+    case 1: return launch_act<1, AMAX>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
+    case 2: return launch_act<2, AMAX>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
+    case 4: return launch_act<4, AMAX>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
+    case 8: return launch_act<8, AMAX>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
+  }
+  ppo_set_error("heads: hidden size %d not supported (64, 128, 256, 512)", H);
+  return PPO_EARG;
+}
+
+template <int HC, int AMAX>
+int launch_train(const TrainArgs& a, int blocks, hipStream_t st) {
+  heads_train_kernel<HC, AMAX><<<blocks, 64 * HW, 0, st>>>(a);
+  PPO_LAUNCH_CHECK("heads_train_kernel");
+  return 0;
+}
+
+template <int AMAX>
+int dispatch_train(int HC, const TrainArgs& a, int blocks, hipStream_t st) {
+  switch (HC) {
+    case 1: return launch_train<1, AMAX>(a, blocks, st);
+    case 2: return launch_train<2, AMAX>(a, blocks, st);
+    case 4: return launch_train<4, AMAX>(a, blocks, st);
+    case 8: return launch_train<8, AMAX>(a, blocks, st);
+  }
+  ppo_set_error("heads: hidden size %d not supported (64, 128, 256, 512)", a.H);
+  return PPO_EARG;
+}
+
+}  // namespace
+
+// Policy.act / evaluate_actions heads (model.py:54-79):
+//   noise   != NULL: sample = argmax(probs / noise) (host-replay parity mode)
+//   noise   == NULL: Exp(1) noise from the counter RNG (seed, counter, row)
+//   given   != NULL: log_prob/entropy of the given actions (evaluate_actions)
+//   deterministic: mode = argmax(probs)
+PPO_API int ppo_heads_act(const float* feat, int N, int H, const float* wc, const float* bc, const float* wa,
+                          const float* ba, int A, const float* noise, unsigned long long seed,
+                          unsigned long long counter, int deterministic, const int64_t* given, float* value,
+                          int64_t* action, float* logp, float* entropy, void* stream) {
+  PPO_REQUIRE(N >= 0 && A >= 1 && A <= 16, "ppo_heads_act: N=%d A=%d (1..16 actions)", N, A);
+  PPO_REQUIRE(H % 64 == 0, "ppo_heads_act: hidden size %d must be a multiple of 64", H);
+  if (N == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  if (A <= 8)
+    return dispatch_act<8>(H / 64, feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
+                           action, logp, entropy, st);
+  return dispatch_act<16>(H / 64, feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
+                          action, logp, entropy, st);
+}
+
+PPO_API int ppo_heads_train_blocks(int B) {
+  const int rpw = 16;
+  return (int)ceil_div(B, HW * rpw);
+}
+
+PPO_API int ppo_heads_train(const float* feat, int B, int H, const float* wc, const float* bc, const float* wa,
+                            const float* ba, int A, const int64_t* idx, long long row0, const int64_t* actions,
+                            const float* old_logp, const float* adv, const float* vpred, const float* ret, float clip,
+                            float value_coef, float entropy_coef, float inv_b, int use_clipped_value_loss,
+                            float* dfeat, float* part_w, float* part_b, float* part_loss, void* stream) {
+  PPO_REQUIRE(B > 0 && A >= 1 && A <= 16, "ppo_heads_train: B=%d A=%d", B, A);
+  PPO_REQUIRE(H % 64 == 0, "ppo_heads_train: hidden size %d must be a multiple of 64", H);
+  TrainArgs a;
+  a.feat = feat; a.B = B; a.H = H; a.A = A; a.wc = wc; a.bc = bc; a.wa = wa; a.ba = ba;
+  a.idx = idx; a.row0 = row0; a.actions = actions; a.old_logp = old_logp; a.adv = adv; a.vpred = vpred; a.ret = ret;
+  a.clip = clip; a.value_coef = value_coef; a.entropy_coef = entropy_coef; a.inv_b = inv_b;
+  a.use_clipped_value_loss = use_clipped_value_loss;
+  a.dfeat = dfeat; a.part_w = part_w; a.part_b = part_b; a.part_loss = part_loss;
+  a.rows_per_wave = 16;
+  const int blocks = ppo_heads_train_blocks(B);
+  hipStream_t st = as_stream(stream);
+  if (A <= 8) return dispatch_train<8>(H / 64, a, blocks, st);
+  return dispatch_train<16>(H / 64, a, blocks, st);
+}
+
+PPO_API int ppo_heads_reduce(const float* part_w, const float* part_b, const float* part_loss, int nblk, int H, int A,
+                             float* g_wc, float* g_bc, float* g_wa, float* g_ba, double* loss_acc, double inv_b,
+                             float scale, int use_clipped_value_loss, void* stream) {
+  const long long total = (long long)(1 + A) * H;
+  long long nb = (total + 255) / 256;
+  heads_reduce_kernel<<<(unsigned)(nb < 1024 ? nb : 1024), 256, 0, as_stream(stream)>>>(
+      part_w, part_b, part_loss, nblk, H, A, g_wc, g_bc, g_wa, g_ba, loss_acc, inv_b, scale, use_clipped_value_loss);
+  PPO_LAUNCH_CHECK("heads_reduce_kernel");
+  return 0;
+}
+
+PPO_API int ppo_mean_f32(const float* x, long long n, float* out, void* stream) {
+  PPO_REQUIRE(n > 0, "ppo_mean_f32: n=%lld", n);
+  mean_kernel<<<1, 256, 0, as_stream(stream)>>>(x, n, out);
+  PPO_LAUNCH_CHECK("mean_kernel");
+  return 0;
+}

@@ -1,0 +1,67 @@
+"""The N>1 protocol (a2c_ppo_acktr/_dist.py) on CPU with gloo, world_size 2:
+sharded lanes see the single-process advantage statistics, and the averaged
+gradient drives an identical clip + Adam step on every rank."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG_DIR, ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import sys
+    for p in (ROOT, PKG_DIR):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from a2c_ppo_acktr import _dist
+    from oracle import ppo_oracle as O
+    rng = np.random.default_rng(0)
+    T, N = 16, 12                       # global lanes, split 6 + 6
+    ret = (3 * rng.standard_normal((T + 1, N)) + 1).astype(np.float32)
+    val = (3 * rng.standard_normal((T + 1, N))).astype(np.float32)
+    lanes = slice(rank * N // world, (rank + 1) * N // world)
+    adv = (ret[:-1, lanes] - val[:-1, lanes]).astype(np.float32)
+    stats = torch.tensor([adv.size, adv.astype(np.float64).sum(), (adv.astype(np.float64) ** 2).sum()],
+                         dtype=torch.float64)
+    _dist.allreduce_stats(stats)
+    mean, std = _dist.stats_mean_std(*stats.tolist())
+    norm = (adv - np.float32(mean)) / (np.float32(std) + np.float32(1e-5))
+    full = O.normalize_advantages(ret, val)[:, lanes]
+    # per-rank gradients -> all-reduce -> averaged clip + Adam
+    P = 50
+    g_local = torch.from_numpy(rng.standard_normal((world, P)).astype(np.float32)[rank] * 4)
+    params = torch.from_numpy(np.linspace(-1, 1, P).astype(np.float32))
+    _dist.broadcast_params(params)
+    g = g_local.clone()
+    scale = _dist.allreduce_grads(g)
+    gmean = (g.numpy() * scale).astype(np.float64)
+    p1, *_ = O.clip_adam(params.numpy().astype(np.float64), gmean, np.zeros(P), np.zeros(P), 1, 1e-3, 1e-5, 0.5)
+    losses = torch.tensor([1.0 + rank, 2.0, 3.0], dtype=torch.float64)
+    _dist.allreduce_losses(losses)
+    out[rank] = (np.abs(norm - full).max(), p1, losses.numpy())
+    dist.destroy_process_group()
+
+
+def test_two_rank_protocol():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    err0, p0, l0 = out[0]
+    err1, p1, l1 = out[1]
+    assert err0 < 2e-6 and err1 < 2e-6          # global advantage normalisation
+    assert np.array_equal(p0, p1)               # identical step on every rank
+    assert np.allclose(l0, [1.5, 2.0, 3.0]) and np.allclose(l1, l0)

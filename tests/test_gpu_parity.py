@@ -1,0 +1,456 @@
+"""GPU parity: every HIP kernel through the C ABI against the oracle (and the
+reference's golden vectors).  Tolerances are stated per test; integer/index work
+and GAE are bit-exact."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden
+from oracle import ppo_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _hip():
+    from a2c_ppo_acktr import _hip
+    return _hip
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+# ---------------------------------------------------------------- GAE (K3/K4)
+@pytest.mark.parametrize("gi", [0, 1])
+@pytest.mark.parametrize("use_gae", [True, False])
+@pytest.mark.parametrize("ptl", [True, False])
+def test_gae_golden_bit_exact(gpu, gi, use_gae, ptl):
+    H = _hip()
+    d = golden("gae.npz")
+    T, N = d["rewards"].shape[:2]
+    r, v, m, bm = (_dev(d[k][..., 0]) for k in ("rewards", "value_preds", "masks", "bad_masks"))
+    nv = _dev(d["next_value"][:, 0])
+    ret = torch.full((T + 1, N), -7.0, device=gpu)
+    H.call("ppo_compute_returns", r.data_ptr(), v.data_ptr(), m.data_ptr(), bm.data_ptr(), nv.data_ptr(),
+           ret.data_ptr(), None, None, T, N, float(d["gammas"][gi]), float(d["lambdas"][gi]), int(use_gae),
+           int(ptl), _s())
+    k = f"g{gi}_gae{int(use_gae)}_ptl{int(ptl)}"
+    assert np.array_equal(ret.cpu().numpy(), d[k + "_returns"][..., 0])
+    assert np.array_equal(v.cpu().numpy(), d[k + "_value_preds"][..., 0])
+
+
+@pytest.mark.parametrize("T,N", [(128, 4096), (5, 1), (1, 300), (77, 1031)])
+def test_gae_fused_adv_vs_oracle(gpu, T, N):
+    """bit-exact returns at the c3 shape and ragged shapes; fused advantage
+    statistics within 1e-6 (the reference reduces in float, we in double)."""
+    H = _hip()
+    rng = np.random.default_rng(T * 7 + N)
+    r = rng.random((T, N), np.float32)
+    v = (3 * rng.standard_normal((T + 1, N))).astype(np.float32)
+    m = (rng.random((T + 1, N)) > 0.01).astype(np.float32)
+    bm = np.ones((T + 1, N), np.float32)
+    nv = rng.standard_normal(N).astype(np.float32)
+    rd, vd, md, bmd, nvd = _dev(r), _dev(v), _dev(m), _dev(bm), _dev(nv)
+    ret = torch.zeros(T + 1, N, device=gpu)
+    adv = torch.zeros(T, N, device=gpu)
+    nparts = H.call("ppo_gae_partials_count", N)
+    parts = torch.zeros(2 * nparts, dtype=torch.float64, device=gpu)
+    stats = torch.zeros(3, dtype=torch.float64, device=gpu)
+    H.call("ppo_compute_returns", rd.data_ptr(), vd.data_ptr(), md.data_ptr(), bmd.data_ptr(), nvd.data_ptr(),
+           ret.data_ptr(), adv.data_ptr(), parts.data_ptr(), T, N, 0.99, 0.95, 1, 0, _s())
+    H.call("ppo_adv_finalize", parts.data_ptr(), nparts, float(T * N), stats.data_ptr(), _s())
+    H.call("ppo_adv_normalize", adv.data_ptr(), T * N, stats.data_ptr(), _s())
+    eret, ev = O.compute_returns(r, v, m, bm, nv, True, 0.99, 0.95, False)
+    assert np.array_equal(ret.cpu().numpy()[:T], eret[:T])
+    assert np.array_equal(vd.cpu().numpy(), ev)
+    if T * N > 1:
+        np.testing.assert_allclose(adv.cpu().numpy(), O.normalize_advantages(eret, ev), rtol=1e-6, atol=1e-6)
+
+
+def test_advnorm_golden(gpu):
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import Discrete
+    d = golden("advnorm.npz")
+    for c in range(3):
+        ret, val = d[f"c{c}_returns"], d[f"c{c}_value_preds"]
+        T, N = ret.shape[0] - 1, ret.shape[1]
+        st = RolloutStorage(T, N, (1,), [0], Discrete(2), 1, device=gpu)
+        st.returns.copy_(_dev(ret))
+        st.value_preds.copy_(_dev(val))
+        adv = st.normalized_advantages()
+        np.testing.assert_allclose(adv.cpu().numpy(), d[f"c{c}_advantages"][..., 0], rtol=1e-6, atol=1e-6)
+
+
+# ------------------------------------------------------------- storage (K1/K2/K5/K6)
+def test_sampler_golden_bit_exact(gpu):
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import Discrete
+    d = golden("sampler.npz")
+    for c in range(4):
+        seed, T, N, M = (int(x) for x in d[f"c{c}_meta"])
+        st = RolloutStorage(T, N, (1,), [0], Discrete(2), 1, device=gpu)
+        st.value_preds[:-1].copy_(torch.arange(T * N, dtype=torch.float32, device=gpu).view(T, N, 1))
+        adv = torch.zeros(T, N, 1, device=gpu)
+        torch.manual_seed(seed)
+        ff = np.stack([b[4].view(-1).long().cpu().numpy() for b in st.feed_forward_generator(adv, M)])
+        assert np.array_equal(ff, d[f"c{c}_ff"])
+        if f"c{c}_rec" in d:
+            torch.manual_seed(seed)
+            rec = np.stack([b[4].view(-1).long().cpu().numpy() for b in st.recurrent_generator(adv, M)])
+            assert np.array_equal(rec, d[f"c{c}_rec"])
+
+
+def test_generator_gathers_every_field(gpu):
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import Discrete
+    T, N, M = 6, 5, 3
+    st = RolloutStorage(T, N, (4, 84, 84), [3], Discrete(8), 2, obs_dtype=torch.uint8, device=gpu)
+    g = torch.Generator().manual_seed(0)
+    st.obs.copy_(torch.randint(0, 256, st.obs.shape, dtype=torch.uint8, generator=g).to(gpu))
+    for t in (st.vector_obs, st.recurrent_hidden_states, st.value_preds, st.returns, st.masks, st.action_log_probs):
+        t.copy_(torch.randn(t.shape, generator=g).to(gpu))
+    st.actions.copy_(torch.randint(0, 8, st.actions.shape, generator=g).to(gpu))
+    adv = torch.randn(T, N, 1, generator=g).to(gpu)
+    torch.manual_seed(3)
+    batches = list(st.feed_forward_generator(adv, M))
+    torch.manual_seed(3)
+    perm = torch.randperm(T * N)
+    mb = T * N // M
+    for i, b in enumerate(batches):
+        idx = perm[i * mb:(i + 1) * mb].to(gpu)
+        exp = [st.obs[:-1].reshape(T * N, 4, 84, 84)[idx], st.vector_obs[:-1].reshape(T * N, 3)[idx],
+               st.recurrent_hidden_states[:-1].reshape(T * N, 2)[idx], st.actions.reshape(T * N, 1)[idx],
+               st.value_preds[:-1].reshape(-1, 1)[idx], st.returns[:-1].reshape(-1, 1)[idx],
+               st.masks[:-1].reshape(-1, 1)[idx], st.action_log_probs.reshape(-1, 1)[idx], adv.reshape(-1, 1)[idx]]
+        for got, e in zip(b, exp):
+            assert torch.equal(got, e)
+    # recurrent generator: env columns, hxs from t=0
+    torch.manual_seed(4)
+    perm = torch.randperm(N)
+    st2 = RolloutStorage(T, 6, (4, 84, 84), [3], Discrete(8), 2, obs_dtype=torch.uint8, device=gpu)
+    st2.obs.copy_(torch.randint(0, 256, st2.obs.shape, dtype=torch.uint8, generator=g).to(gpu))
+    st2.recurrent_hidden_states.copy_(torch.randn(st2.recurrent_hidden_states.shape, generator=g).to(gpu))
+    adv2 = torch.randn(T, 6, 1, generator=g).to(gpu)
+    torch.manual_seed(4)
+    perm = torch.randperm(6)
+    for i, b in enumerate(st2.recurrent_generator(adv2, 3)):
+        envs = perm[i * 2:(i + 1) * 2].to(gpu)
+        assert torch.equal(b[0], st2.obs[:-1][:, envs].reshape(T * 2, 4, 84, 84))
+        assert torch.equal(b[2], st2.recurrent_hidden_states[0][envs])
+        assert torch.equal(b[8], adv2[:, envs].reshape(T * 2, 1))
+    with pytest.raises(IndexError):
+        next(iter(RolloutStorage(2, 7, (1,), [0], Discrete(2), 1, device=gpu).recurrent_generator(
+            torch.zeros(2, 7, 1, device=gpu), 3)))
+
+
+def test_insert_and_after_update(gpu):
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import Discrete
+    T, N = 3, 5
+    st = RolloutStorage(T, N, (4, 84, 84), [2], Discrete(8), 1, device=gpu)
+    ref = {k: getattr(st, k).clone() for k in ("obs", "vector_obs", "recurrent_hidden_states", "actions",
+                                               "action_log_probs", "value_preds", "rewards", "masks", "bad_masks")}
+    g = torch.Generator().manual_seed(1)
+    for step in range(T):
+        o = torch.rand(N, 4, 84, 84, generator=g)
+        vo = torch.rand(N, 2, generator=g)
+        h = torch.rand(N, 1, generator=g)
+        a = torch.randint(0, 8, (N, 1), generator=g)
+        lp, v, r = torch.rand(N, 1, generator=g), torch.rand(N, 1, generator=g), torch.rand(N, 1, generator=g)
+        mk = (torch.rand(N, 1, generator=g) > 0.5).float()
+        bmk = (torch.rand(N, 1, generator=g) > 0.5).float()
+        # host tensors on purpose (run.py passes CPU masks/rewards)
+        st.insert(o, vo.cuda(), h.cuda(), a.cuda(), lp.cuda(), v.cuda(), r, mk, bmk)
+        ref["obs"][step + 1] = o.cuda(); ref["vector_obs"][step + 1] = vo.cuda()
+        ref["recurrent_hidden_states"][step + 1] = h.cuda(); ref["actions"][step] = a.cuda()
+        ref["action_log_probs"][step] = lp.cuda(); ref["value_preds"][step] = v.cuda()
+        ref["rewards"][step] = r.cuda(); ref["masks"][step + 1] = mk.cuda(); ref["bad_masks"][step + 1] = bmk.cuda()
+    assert st.step == 0
+    for k, t in ref.items():
+        assert torch.equal(getattr(st, k), t), k
+    st.after_update()
+    for k in ("obs", "vector_obs", "recurrent_hidden_states", "masks", "bad_masks"):
+        assert torch.equal(getattr(st, k)[0], ref[k][-1]), k
+
+
+def _synth_ref(seed, step, N, nbytes, p_done):
+    """numpy restatement of synth_env_kernel (storage.hip)"""
+    M64 = (1 << 64) - 1
+
+    def mix(z):
+        z = (z + 0x9E3779B97F4A7C15) & M64
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+        return z ^ (z >> 31)
+
+    obs = np.zeros((N, nbytes), np.uint8)
+    rew = np.zeros(N, np.float32)
+    msk = np.zeros(N, np.float32)
+    for n in range(N):
+        key = seed ^ mix((step * 0x100000001B3 + n * 0x9E3779B1) & M64)
+        words = []
+        for c in range(nbytes // 8):
+            words.append(mix((key + c) & M64))
+        obs[n] = np.array(words, dtype=np.uint64).view(np.uint8)
+        k = mix(seed ^ mix((step * 0x100000001B3 + n * 0x9E3779B1 + 0x5EED) & M64))
+        u = (np.float32((k >> 40) & 0xFFFFFF) + np.float32(1)) * np.float32(1 / 16777216)
+        rew[n] = u - np.float32(1 / 16777216)
+        k2 = mix(k ^ 0xD0D0D0D0)
+        u2 = (np.float32((k2 >> 40) & 0xFFFFFF) + np.float32(1)) * np.float32(1 / 16777216)
+        msk[n] = 0.0 if u2 < np.float32(p_done) else 1.0
+    return obs, rew, msk
+
+
+def test_synthetic_env_reproducible(gpu):
+    from a2c_ppo_acktr.synthetic import SyntheticVecEnv
+    N = 3
+    env = SyntheticVecEnv(N, seed=99, p_done=0.5, device=gpu)
+    slot = torch.zeros(N, 4, 84, 84, dtype=torch.uint8, device=gpu)
+    env.counter = 5
+    r, m, bm = env.step_into(slot)
+    obs, rew, msk = _synth_ref(99, 5, N, 4 * 84 * 84, 0.5)
+    assert np.array_equal(slot.cpu().numpy().reshape(N, -1), obs)
+    assert np.array_equal(r.cpu().numpy()[:, 0], rew)
+    assert np.array_equal(m.cpu().numpy()[:, 0], msk)
+    assert torch.all(bm == 1)
+
+
+# ------------------------------------------------------------- trunk (K7-K10, K16)
+def _cnn_params(H, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    shapes = O.cnn_param_shapes(H)
+    flat = torch.cat([torch.randn(int(np.prod(s)), generator=g) * (scale / np.sqrt(np.prod(s[1:]) if len(s) > 1
+                                                                                    else 1.0))
+                      for _, s in shapes])
+    return flat.numpy().astype(np.float32), shapes
+
+
+@pytest.mark.parametrize("B,H", [(8, 64), (37, 512)])
+def test_trunk_forward_vs_torch_fp32(gpu, B, H):
+    """conv1..fc forward through the ABI vs torch fp32 (same op, plain PyTorch);
+    tolerance 2e-5 relative to the activation scale (fp32, different sum order)."""
+    Hh = _hip()
+    flat, shapes = _cnn_params(H, seed=B)
+    p = {n: torch.from_numpy(v.astype(np.float32)) for n, v in O.unflatten(flat, shapes, np.float32).items()}
+    g = torch.Generator().manual_seed(B)
+    obs_u8 = torch.randint(0, 256, (B + 3, 4, 84, 84), dtype=torch.uint8, generator=g)
+    idx = torch.randperm(B + 3, generator=g)[:B]
+    x = obs_u8[idx].float() / 255.0
+    a1 = F.relu(F.conv2d(x, p["base.main.0.weight"], p["base.main.0.bias"], stride=4))
+    a2 = F.relu(F.conv2d(a1, p["base.main.2.weight"], p["base.main.2.bias"], stride=2))
+    a3 = F.relu(F.conv2d(a2, p["base.main.4.weight"], p["base.main.4.bias"], stride=1))
+    hh = F.relu(a3.reshape(B, -1) @ p["base.main.7.weight"].t() + p["base.main.7.bias"])
+    d = {k: v.cuda() for k, v in p.items()}
+    packed = torch.empty(Hh.call("ppo_packed_weights_size", H), device=gpu)
+    offs = torch.zeros(6, dtype=torch.int64)
+    Hh.call("ppo_packed_offsets", H, offs.data_ptr())
+    pk = [packed.data_ptr() + 4 * int(o) for o in offs]
+    Hh.call("ppo_pack_weights", d["base.main.2.weight"].data_ptr(), d["base.main.4.weight"].data_ptr(),
+            d["base.main.7.weight"].data_ptr(), H, packed.data_ptr(), _s())
+    obs_d, idx_d = obs_u8.cuda(), idx.cuda()
+    o1 = torch.empty(B, 20, 20, 32, device=gpu)
+    o2 = torch.empty(B, 9, 9, 64, device=gpu)
+    o3 = torch.empty(B, 7, 7, 32, device=gpu)
+    o4 = torch.empty(B, H, device=gpu)
+    Hh.call("ppo_conv1_fwd", obs_d.data_ptr(), 1, idx_d.data_ptr(), 0, 4, B, d["base.main.0.weight"].data_ptr(),
+            d["base.main.0.bias"].data_ptr(), o1.data_ptr(), _s())
+    Hh.call("ppo_conv2_fwd", o1.data_ptr(), B, pk[0], d["base.main.2.bias"].data_ptr(), o2.data_ptr(), _s())
+    Hh.call("ppo_conv3_fwd", o2.data_ptr(), B, pk[1], d["base.main.4.bias"].data_ptr(), o3.data_ptr(), _s())
+    Hh.call("ppo_linear_relu_fwd", o3.data_ptr(), B, 1568, pk[2], d["base.main.7.bias"].data_ptr(), H,
+            o4.data_ptr(), _s())
+    for got, ref in ((o1, a1.permute(0, 2, 3, 1)), (o2, a2.permute(0, 2, 3, 1)), (o3, a3.permute(0, 2, 3, 1)),
+                     (o4, hh)):
+        ref = ref.contiguous()
+        err = (got.cpu() - ref).abs().max().item()
+        assert err <= 2e-5 * max(1.0, ref.abs().max().item()), err
+    # f32 observation path (reference convention: pre-normalised floats)
+    xf = (obs_u8.float() / 255.0).cuda()
+    o1f = torch.empty_like(o1)
+    Hh.call("ppo_conv1_fwd", xf.data_ptr(), 0, idx_d.data_ptr(), 0, 4, B, d["base.main.0.weight"].data_ptr(),
+            d["base.main.0.bias"].data_ptr(), o1f.data_ptr(), _s())
+    assert torch.equal(o1f, o1)   # u8 decode is bit-identical to u8.float()/255
+
+
+@pytest.mark.parametrize("B,H", [(6, 64), (33, 512)])
+def test_loss_and_backward_vs_oracle(gpu, B, H):
+    """Fused heads/loss + every dgrad/wgrad kernel (through the engine) vs the
+    oracle's float64 analytic backward: max |err| <= 1e-5 * max|grad| per tensor."""
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.algo.ppo import FlatAdam
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import Discrete
+    torch.manual_seed(B)
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase, base_kwargs={"recurrent": False, "hidden_size": H})
+    with torch.no_grad():   # widen the heads so every loss branch carries weight
+        pol.dist.linear.weight.mul_(50.0)
+        pol.base.critic_linear.weight.mul_(3.0)
+    init = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy().astype(np.float64)
+    pol.to(gpu)
+    eng = pol.hip_engine()
+    T, N = 3, B
+    st = RolloutStorage(T, N, (4, 84, 84), [0], Discrete(8), 1, obs_dtype=torch.uint8, device=gpu)
+    g = torch.Generator().manual_seed(B + 1)
+    st.obs.copy_(torch.randint(0, 256, st.obs.shape, dtype=torch.uint8, generator=g).to(gpu))
+    st.actions.copy_(torch.randint(0, 8, st.actions.shape, generator=g).to(gpu))
+    st.action_log_probs.copy_((torch.log(torch.rand(st.action_log_probs.shape, generator=g)) * 0.3 - 2.0).to(gpu))
+    st.value_preds.copy_(torch.randn(st.value_preds.shape, generator=g).to(gpu) * 0.1)
+    st.returns.copy_(torch.randn(st.returns.shape, generator=g).to(gpu))
+    adv = torch.randn(T, N, generator=g).to(gpu)
+    idx = torch.randperm(T * N, generator=g)[: (T * N) // 2].to(gpu)
+    hp = {"clip": 0.1, "value_coef": 0.5, "entropy_coef": 0.01, "use_clipped_value_loss": True}
+    loss = torch.zeros(3, dtype=torch.float64, device=gpu)
+    opt = FlatAdam(pol.parameters(), lr=0.0, eps=1e-5, max_grad_norm=None)  # lr 0: grads only
+    eng.train_minibatch(st, adv, idx, hp, loss, opt)
+    torch.cuda.synchronize()
+    shapes = O.cnn_param_shapes(H)
+    p = O.unflatten(init, shapes)
+    ii = idx.cpu().numpy()
+    obs = st.obs[:-1].reshape(T * N, 4, 84, 84).cpu().numpy()[ii]
+    value, logits, cache = O.cnn_forward(p, O.decode_obs(obs))
+    f = lambda t: t.reshape(-1).cpu().numpy()[ii]  # noqa: E731
+    lg = O.loss_head_grads(value, logits, f(st.actions), f(st.action_log_probs), f(adv),
+                           st.value_preds[:-1].reshape(-1).cpu().numpy()[ii],
+                           st.returns[:-1].reshape(-1).cpu().numpy()[ii], 0.1, 0.5, 0.01)
+    grads = O.cnn_backward(p, cache, lg["g_value"], lg["g_logits"])
+    got = O.unflatten(eng.grad.cpu().numpy(), shapes)
+    for name, _ in shapes:
+        ref = grads[name]
+        err = np.abs(got[name] - ref).max()
+        assert err <= 1e-5 * max(np.abs(ref).max(), 1e-3), (name, err, np.abs(ref).max())
+    np.testing.assert_allclose(loss.cpu().numpy(), [lg["value_loss"], lg["action_loss"], lg["entropy"]],
+                               rtol=2e-5, atol=1e-6)
+
+
+# ------------------------------------------------------------------ heads (K13/K14)
+def test_categorical_golden(gpu):
+    Hh = _hip()
+    d = golden("categorical.npz")
+    feats = d["features"]
+    N, Hd = feats.shape
+    A = d["weight"].shape[0]
+    Hp = 64   # kernel needs H % 64 == 0: zero-pad the feature dimension
+    f = np.zeros((N, Hp), np.float32); f[:, :Hd] = feats
+    wa = np.zeros((A, Hp), np.float32); wa[:, :Hd] = d["weight"]
+    fd, wad, bad = _dev(f), _dev(wa), _dev(d["bias"])
+    wc, bc = torch.zeros(Hp, device=gpu), torch.zeros(1, device=gpu)
+    noise = _dev(d["exp_noise"])
+    val = torch.empty(N, device=gpu); act = torch.empty(N, dtype=torch.int64, device=gpu)
+    lp = torch.empty(N, device=gpu); ent = torch.empty(N, device=gpu)
+    Hh.call("ppo_heads_act", fd.data_ptr(), N, Hp, wc.data_ptr(), bc.data_ptr(), wad.data_ptr(), bad.data_ptr(), A,
+            noise.data_ptr(), 0, 0, 0, None, val.data_ptr(), act.data_ptr(), lp.data_ptr(), ent.data_ptr(), _s())
+    assert np.array_equal(act.cpu().numpy(), d["action"][:, 0])                  # bit-exact sampling
+    np.testing.assert_allclose(lp.cpu().numpy(), d["log_probs"][:, 0], atol=2e-6)
+    np.testing.assert_allclose(ent.cpu().numpy(), d["entropy"], atol=2e-6)
+    Hh.call("ppo_heads_act", fd.data_ptr(), N, Hp, wc.data_ptr(), bc.data_ptr(), wad.data_ptr(), bad.data_ptr(), A,
+            None, 0, 0, 1, None, val.data_ptr(), act.data_ptr(), lp.data_ptr(), ent.data_ptr(), _s())
+    assert np.array_equal(act.cpu().numpy(), d["mode"][:, 0])
+
+
+def test_device_sampling_distribution(gpu):
+    """device RNG mode: empirical action frequencies match probs (chi-square-ish)."""
+    Hh = _hip()
+    N, Hp, A = 200000, 64, 8
+    f = torch.zeros(N, Hp, device=gpu); f[:, 0] = 1.0
+    wa = torch.zeros(A, Hp, device=gpu); wa[:, 0] = torch.linspace(-1, 1.5, A, device=gpu)
+    ba = torch.zeros(A, device=gpu)
+    wc, bc = torch.zeros(Hp, device=gpu), torch.zeros(1, device=gpu)
+    act = torch.empty(N, dtype=torch.int64, device=gpu)
+    Hh.call("ppo_heads_act", f.data_ptr(), N, Hp, wc.data_ptr(), bc.data_ptr(), wa.data_ptr(), ba.data_ptr(), A,
+            None, 1234, 1, 0, None, None, act.data_ptr(), None, None, _s())
+    freq = np.bincount(act.cpu().numpy(), minlength=A) / N
+    p = torch.softmax(torch.linspace(-1, 1.5, A), 0).numpy()
+    assert np.abs(freq - p).max() < 0.005
+
+
+# --------------------------------------------------------------- optimizer (K17/K18)
+def test_clip_adam_golden(gpu):
+    Hh = _hip()
+    d = golden("adam_clip.npz")
+    n = d["init"].size
+    p = _dev(d["init"])
+    m = torch.zeros(n, device=gpu); v = torch.zeros(n, device=gpu)
+    parts = torch.zeros(Hh.call("ppo_grad_partials_count", n), dtype=torch.float64, device=gpu)
+    nrm = torch.zeros(1, dtype=torch.float64, device=gpu)
+    for k in range(d["grads"].shape[0]):
+        g = _dev(d["grads"][k])
+        Hh.call("ppo_grad_sumsq", g.data_ptr(), n, 1.0, parts.data_ptr(), _s())
+        Hh.call("ppo_clip_adam", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, parts.data_ptr(), 1.0,
+                float(d["max_norm"][0]), float(d["lr"][0]), 0.9, 0.999, float(d["eps"][0]), k + 1, nrm.data_ptr(),
+                _s())
+        np.testing.assert_allclose(nrm.item(), d["total_norms"][k], rtol=1e-6)
+        np.testing.assert_allclose(g.cpu().numpy(), d["clipped"][k], rtol=1e-5, atol=1e-9)
+        np.testing.assert_allclose(p.cpu().numpy(), d["after"][k], rtol=0, atol=1e-6)
+
+
+# ------------------------------------------------------------------ whole iteration
+def test_full_iteration_replays_reference(gpu):
+    """The reference iteration recorded in cnn_update.npz, replayed through the
+    drop-in API: same init (same seed + construction), same host sampling draws,
+    same randperms -> bit-exact actions, returns within 1e-5, losses within 1e-4
+    relative, final parameters within 2e-5 absolute (lr 1e-3 steps)."""
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.algo import PPO
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import Discrete
+    d = golden("cnn_update.npz")
+    hidden, N, T, E, Mb = (int(x) for x in d["meta"])
+    torch.set_num_threads(1)   # as T/run.py:55 (orthogonal_ init is thread-count sensitive)
+    torch.manual_seed(1)
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase,
+                   base_kwargs={"recurrent": False, "hidden_size": hidden}, vector_obs_len=0)
+    init = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy()
+    assert np.array_equal(init, d["init_params"])          # identical construction + init
+    pol.to(gpu)
+    agent = PPO(pol, 0.1, E, Mb, 0.5, 0.001, lr=float(d["lr"][0]), eps=1e-5, max_grad_norm=0.5)
+    st = RolloutStorage(T, N, (4, 84, 84), [0], Discrete(8), pol.recurrent_hidden_state_size,
+                        obs_dtype=torch.uint8, device=gpu)
+    st.obs.copy_(_dev(d["obs_u8"]))
+    M.set_sampling_mode("host")
+    try:
+        for step in range(T):
+            v, a, lp, h = pol.act(st.obs[step], st.vector_obs[step], st.recurrent_hidden_states[step],
+                                  st.masks[step])
+            st.insert(st.obs[step + 1], st.vector_obs[step + 1], h, a, lp, v, _dev(d["rewards"][step]),
+                      _dev(d["masks"][step]), torch.ones(N, 1, device=gpu))
+        nv = pol.get_value(st.obs[-1], st.vector_obs[-1], st.recurrent_hidden_states[-1], st.masks[-1])
+        st.compute_returns(nv, True, 0.99, 0.95, False)
+        losses = agent.update(st)
+    finally:
+        M.set_sampling_mode("device")
+    assert np.array_equal(st.actions.cpu().numpy(), d["actions"])
+    np.testing.assert_allclose(st.action_log_probs.cpu().numpy(), d["action_log_probs"], atol=1e-5)
+    np.testing.assert_allclose(st.returns.cpu().numpy(), d["returns"], atol=1e-5)
+    np.testing.assert_allclose(losses, d["losses"], rtol=1e-4, atol=1e-6)
+    final = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).cpu().numpy()
+    np.testing.assert_allclose(final, d["final_params"], rtol=0, atol=2e-5)
+    st.after_update()
+    assert torch.equal(st.obs[0], st.obs[-1])
+
+
+def test_full_size_forward_vs_oracle(gpu):
+    """c3 network (H=512) on 4096 lanes: value/log-prob through Policy.act
+    (deterministic) vs the float64 oracle — max abs err 1e-4."""
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.synthetic import Discrete
+    torch.manual_seed(5)
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase, base_kwargs={"recurrent": False})
+    init = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy()
+    pol.to(gpu)
+    N = 4096
+    g = torch.Generator().manual_seed(6)
+    obs = torch.randint(0, 256, (N, 4, 84, 84), dtype=torch.uint8, generator=g)
+    v, a, lp, _ = pol.act(obs.cuda(), None, None, None, deterministic=True)
+    sub = np.arange(0, N, 64)
+    p = O.unflatten(init, O.cnn_param_shapes(512))
+    value, logits, _ = O.cnn_forward(p, O.decode_obs(obs.numpy()[sub]))
+    c = O.categorical(logits, deterministic=True)
+    np.testing.assert_allclose(v.cpu().numpy()[sub, 0], value, atol=1e-4)
+    np.testing.assert_allclose(lp.cpu().numpy()[sub, 0], c["log_prob"], atol=1e-4)

@@ -1,0 +1,29 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprof.  Every GPU step has
+# its own time limit; a fault/abort/timeout (rc not 0/1) ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STEPS="${STEPS:-pytest smoke bench}"
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "!! stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+export PYTHONDONTWRITEBYTECODE=1
+for s in $STEPS; do
+  case $s in
+    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    pytestall) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 900 python bench.py ;;
+    benchq) run bench 900 python bench.py --no-cpu-baseline --steps 2 --warmup 1 ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          run rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-gae-roofline --steps 2 --warmup 1 ;;
+  esac
+done
+echo "== all done"
