@@ -173,6 +173,8 @@ class CNNEngine:
     def train_minibatch(self, storage, adv, idx, hp, loss_acc, optimizer):
         """Forward + backward + (all-reduce) + clip + Adam for one minibatch of
         storage rows idx (int64 [B], device)."""
+        self.ensure_bound()
+        self.pack()
         dev, H, A = self.device, self.H, self.A
         B = idx.numel()
         ws = self.ws["train"]

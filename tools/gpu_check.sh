@@ -23,7 +23,7 @@ for s in $STEPS; do
     bench) run bench 900 python bench.py ;;
     benchq) run bench 900 python bench.py --no-cpu-baseline --steps 2 --warmup 1 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-          run rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-gae-roofline --steps 2 --warmup 1 ;;
+          run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-gae-roofline --steps 2 --warmup 1 ;;
   esac
 done
 echo "== all done"
