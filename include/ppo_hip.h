@@ -82,7 +82,8 @@ int ppo_packed_offsets(int H, long long* off6);
 /* once per optimizer step: torch-layout conv2/conv3/fc weights -> loader orders */
 int ppo_pack_weights(const float* w2, const float* w3, const float* w4, int H, float* packed, void* stream);
 /* model.py:177 Conv2d(C,32,8,s4)+ReLU over obs rows (idx: storage-row gather,
- * storage.py:143; NULL: rows row0..row0+B-1); u8 decoded as u8/255 */
+ * storage.py:143; NULL: rows row0..row0+B-1); u8 staged as integers, 1/255 applied
+ * to the accumulator (Σ w·u/255) */
 int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B, const float* w1,
                   const float* b1, float* out, void* stream);
 /* model.py:178 Conv2d(32,64,4,s2)+ReLU */
@@ -105,8 +106,15 @@ int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, float* slab
 int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, float* slab, float* slab_bias, void* stream);
 int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int K, int Z, float* slab, float* slab_bias,
                      void* stream);
+/* scale multiplies the weight sums only (conv1 with u8 observations stages the
+ * bytes as integers: pass 1/255); bias sums are unscaled */
 int ppo_wgrad_reduce(const float* slab, const float* slab_bias, int Z, int M, int NW, int kind, int a, int b,
                      float* gw, float* gb, float scale, int accumulate, void* stream);
+/* deterministic column sums out[c] = scale·Σ_r src[r*ld + c] (split-partial reduces) */
+int ppo_colsum(const float* src, long long ld, int rows, long long cols, float* out, float scale, int accumulate,
+               void* stream);
+/* tile-configuration variant of a GEMM family (development A/B knob; 0 = default) */
+int ppo_tune_set(const char* key, int value);
 
 /* ---------------- heads, distribution, loss -------------------------------- */
 /* model.py:54-79 act / get_value / evaluate_actions heads + distributions.py:17-27

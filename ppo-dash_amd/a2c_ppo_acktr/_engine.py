@@ -240,5 +240,6 @@ class CNNEngine:
         else:
             call("ppo_linear_wgrad", dz.data_ptr(), x.data_ptr(), B, self.H, FEAT, Z, slab.data_ptr(),
                  slab_b.data_ptr(), s)
+        scale = 1.0 / 255.0 if layer == "conv1" and x.dtype == torch.uint8 else 1.0   # u8 staged as integers
         call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, M, NW, kind, ka, kb, self.gv(wi), self.gv(bi),
-             1.0, 0, s)
+             scale, 0, s)

@@ -52,6 +52,8 @@ SIGNATURES = {
     "ppo_conv3_wgrad": [c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     "ppo_linear_wgrad": [c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
     "ppo_wgrad_reduce": [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_f, c_int, c_p],
+    "ppo_colsum": [c_p, c_ll, c_int, c_ll, c_p, c_f, c_int, c_p],
+    "ppo_tune_set": [ctypes.c_char_p, c_int],
     # heads.hip
     "ppo_heads_act": [c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_ull, c_ull, c_int, c_p, c_p, c_p, c_p,
                       c_p, c_p],

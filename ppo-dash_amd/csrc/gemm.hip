@@ -22,23 +22,38 @@
 // one ds_read_b128 of 4 k values per lane) or row-contiguous ([BK][rows], read
 // as 4 ds_read_b32); the 4 k values of a lane feed 4 successive MFMAs, so the
 // physical k order inside a BK=16 step is a fixed permutation common to A and B.
+#include <string.h>
+
 #include "common.h"
 
 namespace {
 
-constexpr int BK = 16;
-constexpr int KC_LD = BK + 4;  // k-contiguous row stride: conflict-free ds_read_b128
+constexpr int BK16 = 16;  // default k-tile depth (wgrad chunks are multiples of it)
 
-template <int ROWS, bool KC>
+// k-contiguous tiles: rows of BK floats (CPR = BK/4 16-B chunks), chunk q of
+// row r stored at chunk q ^ f(r), f(r) = (r / (16/CPR)) mod CPR.  A wave's
+// fragment read (32 rows, one chunk each) then hits 16 distinct 16-B slots in
+// every ds_read_b128 lane group, and the staging ds_write_b128 of whole rows is
+// contiguous — both conflict-free (PMC: SQ_LDS_BANK_CONFLICT, the +4 padding
+// this replaces cost 37 % of LDS cycles in the staging writes).
+template <int ROWS, bool KC, int BK>
 struct Tile {
-  static constexpr int SIZE = KC ? ROWS * KC_LD : BK * ROWS;
+  static constexpr int LD = BK;
+  static constexpr int SIZE = KC ? ROWS * LD : BK * ROWS;
   static constexpr int NV4 = ROWS * BK / 4;
 };
 
-template <int ROWS, bool KC>
+template <int BK>
+__device__ __forceinline__ int kc_off(int row, int k) {  // k multiple of 4
+  constexpr int CPR = BK / 4;
+  const int q = (k >> 2) ^ ((row / (16 / CPR)) & (CPR - 1));
+  return row * BK + 4 * q;
+}
+
+template <int ROWS, bool KC, int BK>
 __device__ __forceinline__ f32x4 frag(const float* S, int row, int kb) {
   if constexpr (KC) {
-    return *reinterpret_cast<const f32x4*>(S + row * KC_LD + kb);
+    return *reinterpret_cast<const f32x4*>(S + kc_off<BK>(row, kb));
   } else {
     f32x4 r;
     r[0] = S[(kb + 0) * ROWS + row];
@@ -65,11 +80,12 @@ __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 // ---------------------------------------------------------------------------
 template <class P>
 __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
-  constexpr int BM = P::BM, BN = P::BN, NT = P::NT, WM = P::WM, WN = P::WN;
+  constexpr int BM = P::BM, BN = P::BN, NT = P::NT, WM = P::WM, WN = P::WN, BK = P::BK;
   constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN);
   static_assert(TM * 32 * WM == BM && TN * 32 * WN == BN && WM * WN * 64 == NT, "tile config");
-  using TA = Tile<BM, P::A_KC>;
-  using TB = Tile<BN, P::B_KC>;
+  static_assert(BK == 16 || BK == 32, "k-tile");
+  using TA = Tile<BM, P::A_KC, BK>;
+  using TB = Tile<BN, P::B_KC, BK>;
   constexpr int NVA = (TA::NV4 + NT - 1) / NT, NVB = (TB::NV4 + NT - 1) / NT;
   constexpr int STAGE = TA::SIZE + TB::SIZE;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
@@ -95,7 +111,7 @@ __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
       const int row = f / (BK / 4), kq = f % (BK / 4);
       actx[i] = p.a_ctx(m0 + row, z);
       ak[i] = 4 * kq;
-      aoff[i] = row * KC_LD + 4 * kq;
+      aoff[i] = kc_off<BK>(row, 4 * kq);
     } else {
       const int k = f / (BM / 4), rq = f % (BM / 4);
       actx[i] = p.a_ctx(m0 + 4 * rq, z);
@@ -111,7 +127,7 @@ __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
       const int row = f / (BK / 4), kq = f % (BK / 4);
       bctx[i] = p.b_ctx(n0 + row, z);
       bk[i] = 4 * kq;
-      boff[i] = row * KC_LD + 4 * kq;
+      boff[i] = kc_off<BK>(row, 4 * kq);
     } else {
       const int k = f / (BN / 4), rq = f % (BN / 4);
       bctx[i] = p.b_ctx(n0 + 4 * rq, z);
@@ -169,9 +185,9 @@ __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
     for (int kk = 0; kk < BK; kk += 8) {
       f32x4 af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag<BM, P::A_KC>(As, (wm * TM + i) * 32 + frow, kk + fk);
+      for (int i = 0; i < TM; ++i) af[i] = frag<BM, P::A_KC, BK>(As, (wm * TM + i) * 32 + frow, kk + fk);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = frag<BN, P::B_KC>(Bs, (wn * TN + j) * 32 + frow, kk + fk);
+      for (int j = 0; j < TN; ++j) bf[j] = frag<BN, P::B_KC, BK>(Bs, (wn * TN + j) * 32 + frow, kk + fk);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -200,16 +216,20 @@ __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
   }
 }
 
-template <int BM_, int BN_, int WM_, int WN_, bool AKC, bool BKC, bool BIASA = false>
+template <int BM_, int BN_, int WM_, int WN_, bool AKC, bool BKC, bool BIASA = false, int BK_ = BK16>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NT = 64 * WM_ * WN_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NT = 64 * WM_ * WN_, BK = BK_;
   static constexpr bool A_KC = AKC, B_KC = BKC, BIAS_FROM_A = BIASA;
   struct ACtx { const float* p; int a; int b; bool ok; };
   struct BCtx { const float* p; int a; bool ok; };
 };
 
-__device__ __forceinline__ f32x4 decode4(uint32_t u) {
-  return f32x4{decode_u8(u & 255u), decode_u8((u >> 8) & 255u), decode_u8((u >> 16) & 255u), decode_u8(u >> 24)};
+// u8 operand as exact integers 0..255; the 1/255 of the decode is folded into
+// the epilogue (forward) or the slab reduce (wgrad): Σ w·u/255 instead of
+// Σ w·fl(u/255), a ≤ 1-ulp-per-term difference (within the fp32 tolerance of
+// the GEMM's own summation order) for 16 fewer VALU ops per 4 bytes.
+__device__ __forceinline__ f32x4 u8x4(uint32_t u) {
+  return f32x4{(float)(u & 255u), (float)((u >> 8) & 255u), (float)((u >> 16) & 255u), (float)(u >> 24)};
 }
 
 // obs row of minibatch sample b: storage row idx[b] (gather) or row0 + b
@@ -223,8 +243,9 @@ __device__ __forceinline__ long long obs_row(const int64_t* idx, long long row0,
 constexpr int IMG = 84, IMG2 = 84 * 84;
 
 // conv1: 8x8 stride 4 over the u8/f32 NCHW observation, k = (c, ky, kx) (torch order)
-template <typename InT>
-struct Conv1Fwd : Cfg<256, 32, 4, 1, true, true> {
+template <typename InT, class C_>
+struct Conv1Fwd : C_ {
+  using BCtx = typename C_::BCtx;
   const InT* obs; const int64_t* idx; long long row0; int C, M;
   const float* w; const float* bias; float* out;
   struct ACtx { const InT* base; bool ok; };
@@ -237,7 +258,7 @@ struct Conv1Fwd : Cfg<256, 32, 4, 1, true, true> {
     if (!c.ok) return zero4();
     const int ch = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
     const InT* q = c.base + ch * IMG2 + ky * IMG + kx;
-    if constexpr (sizeof(InT) == 1) return decode4(*reinterpret_cast<const uint32_t*>(q));
+    if constexpr (sizeof(InT) == 1) return u8x4(*reinterpret_cast<const uint32_t*>(q));
     else return *reinterpret_cast<const f32x4*>(q);
   }
   __device__ BCtx b_ctx(int n, int) const { return {w + n * (C * 64), 0, n < 32}; }
@@ -246,6 +267,7 @@ struct Conv1Fwd : Cfg<256, 32, 4, 1, true, true> {
   }
   __device__ void k_range(int, int& b, int& e) const { b = 0; e = C * 64; }
   __device__ void store(int m, int n, int, float v) const {
+    if constexpr (sizeof(InT) == 1) v *= (1.0f / 255.0f);
     if (m < M) out[(size_t)m * 32 + n] = fmaxf(v + bias[n], 0.f);
   }
 };
@@ -360,7 +382,9 @@ struct ConvDgradS1 : C_ {
 // (y&1, x&1) = blockIdx.z so each phase is a dense 2x2-tap problem:
 // m = (b, yy, xx) with y = 2yy+py; k = (ty, tx, co): ky = py+2ty,
 // oy = yy - ty.  wd packed [4 phases][CIN][4*COUT].
-struct Conv2Dgrad : Cfg<256, 32, 4, 1, true, true> {
+template <class C_>
+struct Conv2Dgrad : C_ {
+  using BCtx = typename C_::BCtx;
   static constexpr int HIN = 20, CIN = 32, HOUT = 9, COUT = 64, K = 4 * COUT, PPH = 100;
   const float* dy; const float* wd; const float* act; float* dx; int M;  // M = B*100 per phase
   struct ACtx { const float* p; int yy; int xx; bool ok; };
@@ -399,7 +423,7 @@ struct Conv2Dgrad : Cfg<256, 32, 4, 1, true, true> {
 // ---------------------------------------------------------------------------
 template <class C_>
 struct WgradBase : C_ {
-  const float* dz; int COUT; long long R; int chunk;  // chunk: multiple of BK
+  const float* dz; int COUT; long long R; int chunk;  // chunk: multiple of 16 (and of BK)
   float* slab; float* slab_bias; int NW;             // slab [Z][COUT][NW]
   using ACtx = typename C_::ACtx;
   __device__ ACtx a_ctx(int co, int) const { return {dz + co, 0, 0, co < COUT}; }
@@ -433,7 +457,7 @@ struct Conv1Wgrad : WgradBase<C_> {
     if (!c.ok || r >= this->R) return zero4();
     const int b = r / 400, pp = r - b * 400, oy = pp / 20, ox = pp - oy * 20;
     const InT* q = obs + obs_row(idx, row0, b) * (long long)(C * IMG2) + (oy * 4) * IMG + ox * 4 + c.off;
-    if constexpr (sizeof(InT) == 1) return decode4(*reinterpret_cast<const uint32_t*>(q));
+    if constexpr (sizeof(InT) == 1) return u8x4(*reinterpret_cast<const uint32_t*>(q));
     else return *reinterpret_cast<const f32x4*>(q);
   }
 };
@@ -466,39 +490,54 @@ struct DenseWgrad : WgradBase<C_> {
   }
 };
 
-// Deterministic slab sum -> gradient in torch parameter order.
-//   kind 0: w[m][n]                      (conv1 (c,ky,kx), identity)
-//   kind 1: n=(ky,kx,ci) -> w[m][ci][ky][kx]   (conv2/conv3)
-//   kind 2: n=(p,c)      -> w[m][c*P + p]      (fc over the NHWC flatten)
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab,
-                                                           const float* __restrict__ slab_bias, int Z, int M, int NW,
-                                                           int kind, int a, int b, float* __restrict__ gw,
-                                                           float* __restrict__ gb, float scale, int accumulate) {
-  const long long total = (long long)M * NW;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    float s = 0.f;
-    for (int zz = 0; zz < Z; ++zz) s += slab[(size_t)zz * total + i];
-    const int m = (int)(i / NW), n = (int)(i - (long long)m * NW);
-    size_t o;
-    if (kind == 0) {
-      o = i;
-    } else if (kind == 1) {  // a = KS, b = CIN
+// Deterministic column sums: out[c] = scale * Σ_z src[z*ld + c], c < cols.
+// A block covers 32 consecutive columns with 8 z-groups (each summing
+// z ≡ g mod 8 in a fixed order, 4 loads in flight), then combines the groups
+// in a fixed order — bitwise reproducible, and ≥ cols/32 blocks of parallelism.
+//   map kind 0: w[c]                                  (conv1 (c,ky,kx), biases)
+//   map kind 1: c=(m, n=(ky,kx,ci)) -> w[m][ci][ky][kx]  (conv2/conv3; a=KS, b=CIN, nw)
+//   map kind 2: c=(m, n=(p,ch))     -> w[m][ch*P + p]    (fc; a=C, b=P, nw)
+struct ColMap {
+  int kind, a, b, nw;
+  __device__ __forceinline__ size_t operator()(long long c) const {
+    if (kind == 0) return (size_t)c;
+    const int m = (int)(c / nw), n = (int)(c - (long long)m * nw);
+    if (kind == 1) {
       const int ky = n / (a * b), rem = n - ky * (a * b), kx = rem / b, ci = rem - kx * b;
-      o = (size_t)m * NW + (size_t)ci * a * a + ky * a + kx;
-    } else {  // a = C, b = P
-      const int pp = n / a, c = n - pp * a;
-      o = (size_t)m * NW + (size_t)c * b + pp;
+      return (size_t)m * nw + (size_t)ci * a * a + ky * a + kx;
     }
-    s *= scale;
-    gw[o] = accumulate ? gw[o] + s : s;
+    const int pp = n / a, ch = n - pp * a;
+    return (size_t)m * nw + (size_t)ch * b + pp;
   }
-  if (blockIdx.x == 0) {
-    for (int m = threadIdx.x; m < M; m += 256) {
-      float s = 0.f;
-      for (int zz = 0; zz < Z; ++zz) s += slab_bias[(size_t)zz * M + m];
-      s *= scale;
-      gb[m] = accumulate ? gb[m] + s : s;
+};
+
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ src, long long ld, int Z,
+                                                     long long cols, ColMap map, float* __restrict__ out, float scale,
+                                                     int accumulate) {
+  const int cl = threadIdx.x & 31, zg = threadIdx.x >> 5;
+  const long long c = (long long)blockIdx.x * 32 + cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < cols) {
+    const float* p = src + c;
+    int z = zg;
+    for (; z + 24 < Z; z += 32) {
+      s0 += p[(size_t)z * ld];
+      s1 += p[(size_t)(z + 8) * ld];
+      s2 += p[(size_t)(z + 16) * ld];
+      s3 += p[(size_t)(z + 24) * ld];
     }
+    for (; z < Z; z += 8) s0 += p[(size_t)z * ld];
+  }
+  __shared__ float red[8][33];
+  red[zg][cl] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (zg == 0 && c < cols) {
+    float t = red[0][cl];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) t += red[g][cl];
+    t *= scale;
+    const size_t o = map(c);
+    out[o] = accumulate ? out[o] + t : t;
   }
 }
 
@@ -593,31 +632,83 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Tile-configuration variants (A/B knobs for tools/kbench.py; defaults are the
+// measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
+// ---------------------------------------------------------------------------
+enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_N };
+static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad"};
+static int g_tune[TK_N] = {1, 1, 1, 1, 1};  // measured best (kbench sweep, profiles/)
+
+PPO_API int ppo_tune_set(const char* key, int value) {
+  for (int i = 0; i < TK_N; ++i)
+    if (strcmp(key, g_tune_names[i]) == 0) {
+      g_tune[i] = value;
+      return 0;
+    }
+  ppo_set_error("ppo_tune_set: unknown key %s", key);
+  return PPO_EARG;
+}
+
+// N = 32 output-channel problems (conv1/conv3 fwd, conv2 dgrad)
+using V32_0 = Cfg<256, 32, 4, 1, true, true>;           // 4 waves x 64 rows, 46 KB LDS
+using V32_1 = Cfg<128, 32, 4, 1, true, true>;           // 4 waves x 32 rows, 26 KB
+using V32_2 = Cfg<128, 32, 2, 1, true, true>;           // 2 waves x 64 rows, 26 KB
+using V32_3 = Cfg<128, 32, 4, 1, true, true, false, 32>;  // BK 32, 46 KB
+using V32_4 = Cfg<64, 32, 2, 1, true, true, false, 32>;   // 2 waves x 32 rows, BK 32, 28 KB
+// N = 64 problems (conv2 fwd, conv3 dgrad)
+using V64_0 = Cfg<128, 64, 2, 2, true, true>;
+using V64_1 = Cfg<64, 64, 2, 2, true, true>;
+using V64_2 = Cfg<128, 64, 4, 1, true, true>;
+
+#define PPO_VARIANTS32(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                        \
+  switch (g_tune[tk]) {                                                                           \
+    case 1: { TEMPL(V32_1) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+    case 2: { TEMPL(V32_2) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+    case 3: { TEMPL(V32_3) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+    case 4: { TEMPL(V32_4) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+    default: { TEMPL(V32_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+  }
+
+#define PPO_VARIANTS64(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                        \
+  switch (g_tune[tk]) {                                                                           \
+    case 1: { TEMPL(V64_1) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+    case 2: { TEMPL(V64_2) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+    default: { TEMPL(V64_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+  }
+
 // conv1 forward: out [B][20][20][32] = relu(conv(obs rows, W1 torch layout) + b1)
 PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
                           const float* w1, const float* b1, float* out, void* stream) {
   PPO_REQUIRE(B >= 0 && C > 0, "ppo_conv1_fwd: B=%d C=%d", B, C);
   const long long M = (long long)B * 400;
+  const int tk = TK_CONV1_FWD;
+  const double fl = 2.0 * M * 32 * C * 64;
+#define SETUP1(T_)                                                                                 \
+  p.obs = (const T_*)obs; p.idx = idx; p.row0 = row0; p.C = C; p.M = (int)M; p.w = w1; p.bias = b1; p.out = out
   if (obs_is_u8) {
-    Conv1Fwd<uint8_t> p;
-    p.obs = (const uint8_t*)obs; p.idx = idx; p.row0 = row0; p.C = C; p.M = (int)M; p.w = w1; p.bias = b1; p.out = out;
-    return launch(p, M, 32, 1, as_stream(stream), "conv1_fwd_u8", 2.0 * M * 32 * C * 64);
+#define T1(C_) Conv1Fwd<uint8_t, C_>
+    PPO_VARIANTS32(T1, SETUP1(uint8_t), M, 32, 1, "conv1_fwd_u8", fl)
+#undef T1
   }
-  Conv1Fwd<float> p;
-  p.obs = (const float*)obs; p.idx = idx; p.row0 = row0; p.C = C; p.M = (int)M; p.w = w1; p.bias = b1; p.out = out;
-  return launch(p, M, 32, 1, as_stream(stream), "conv1_fwd_f32", 2.0 * M * 32 * C * 64);
+#define T1(C_) Conv1Fwd<float, C_>
+  PPO_VARIANTS32(T1, SETUP1(float), M, 32, 1, "conv1_fwd_f32", fl)
+#undef T1
+#undef SETUP1
 }
 
 PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream) {
-  ConvFwd<20, 32, 4, 2, 9, 64, CfgN64> p;
+  ConvFwd<20, 32, 4, 2, 9, 64, V64_0> p;
   p.in = a1; p.w = w2p; p.bias = b2; p.out = out; p.M = B * 81;
   return launch(p, (long long)B * 81, 64, 1, as_stream(stream), "conv2_fwd", 2.0 * B * 81 * 64 * 512);
 }
 
 PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream) {
-  ConvFwd<9, 64, 3, 1, 7, 32, CfgN32> p;
-  p.in = a2; p.w = w3p; p.bias = b3; p.out = out; p.M = B * 49;
-  return launch(p, (long long)B * 49, 32, 1, as_stream(stream), "conv3_fwd", 2.0 * B * 49 * 32 * 576);
+  const int tk = TK_CONV3_FWD;
+#define T3(C_) ConvFwd<9, 64, 3, 1, 7, 32, C_>
+  PPO_VARIANTS32(T3, (p.in = a2, p.w = w3p, p.bias = b3, p.out = out, p.M = B * 49), (long long)B * 49, 32, 1,
+                 "conv3_fwd", 2.0 * B * 49 * 32 * 576)
+#undef T3
 }
 
 // Linear + ReLU: out [M][N] = relu(x [M][K] · w [N][K]^T + b)
@@ -644,20 +735,24 @@ PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt
 }
 
 PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream) {
-  ConvDgradS1<9, 64, 3, 7, 32, CfgN64> p;
-  p.dy = dz3; p.wd = w3d; p.act = a2; p.dx = dz2; p.M = B * 81;
-  return launch(p, (long long)B * 81, 64, 1, as_stream(stream), "conv3_dgrad", 2.0 * B * 49 * 32 * 576);
+  const int tk = TK_CONV3_DGRAD;
+#define TD3(C_) ConvDgradS1<9, 64, 3, 7, 32, C_>
+  PPO_VARIANTS64(TD3, (p.dy = dz3, p.wd = w3d, p.act = a2, p.dx = dz2, p.M = B * 81), (long long)B * 81, 64, 1,
+                 "conv3_dgrad", 2.0 * B * 49 * 32 * 576)
+#undef TD3
 }
 
 PPO_API int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const float* a1, float* dz1, void* stream) {
-  Conv2Dgrad p;
-  p.dy = dz2; p.wd = w2d; p.act = a1; p.dx = dz1; p.M = B * 100;
-  return launch(p, (long long)B * 100, 32, 4, as_stream(stream), "conv2_dgrad", 2.0 * B * 81 * 64 * 512);
+  const int tk = TK_CONV2_DGRAD;
+#define TD2(C_) Conv2Dgrad<C_>
+  PPO_VARIANTS32(TD2, (p.dy = dz2, p.wd = w2d, p.act = a1, p.dx = dz1, p.M = B * 100), (long long)B * 100, 32, 4,
+                 "conv2_dgrad", 2.0 * B * 81 * 64 * 512)
+#undef TD2
 }
 
 // split count and chunk for a wgrad reduction of R rows (BK-aligned chunks)
 PPO_API int ppo_wgrad_splits(long long R, int tiles, int target_blocks, int min_ktiles) {
-  long long kt = (R + BK - 1) / BK;
+  long long kt = (R + BK16 - 1) / BK16;
   long long z = target_blocks / (tiles > 0 ? tiles : 1);
   if (z < 1) z = 1;
   if (kt / z < min_ktiles) z = kt / min_ktiles;
@@ -667,8 +762,8 @@ PPO_API int ppo_wgrad_splits(long long R, int tiles, int target_blocks, int min_
 }
 
 static inline int wgrad_chunk(long long R, int Z) {
-  long long kt = (R + BK - 1) / BK;
-  return (int)(((kt + Z - 1) / Z) * BK);
+  long long kt = (R + BK16 - 1) / BK16;
+  return (int)(((kt + Z - 1) / Z) * BK16);
 }
 
 template <class P>
@@ -677,6 +772,7 @@ static void set_wgrad(P& p, const float* dz, int COUT, long long R, int Z, float
 }
 
 using CfgW32 = Cfg<32, 256, 1, 4, false, false, true>;
+using CfgW32n = Cfg<32, 128, 1, 4, false, false, true>;
 using CfgW64 = Cfg<64, 128, 2, 2, false, false, true>;
 using CfgW32b = Cfg<32, 128, 1, 4, false, false, true>;
 using CfgWfc = Cfg<128, 128, 2, 2, false, false, true>;
@@ -686,16 +782,23 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
                             int C, int B, int Z, float* slab, float* slab_bias, void* stream) {
   const long long R = (long long)B * 400;
   PPO_REQUIRE(R < 0x7fffffffLL, "ppo_conv1_wgrad: B too large");
+  const double fl = 2.0 * R * 32 * C * 64;
   if (obs_is_u8) {
+    if (g_tune[TK_CONV1_WGRAD] == 1) {
+      Conv1Wgrad<uint8_t, CfgW32n> p;
+      set_wgrad(p, dz1, 32, R, Z, slab, slab_bias, C * 64);
+      p.obs = (const uint8_t*)obs; p.idx = idx; p.row0 = row0; p.C = C;
+      return launch(p, 32, C * 64, Z, as_stream(stream), "conv1_wgrad_u8", fl);
+    }
     Conv1Wgrad<uint8_t, CfgW32> p;
     set_wgrad(p, dz1, 32, R, Z, slab, slab_bias, C * 64);
     p.obs = (const uint8_t*)obs; p.idx = idx; p.row0 = row0; p.C = C;
-    return launch(p, 32, C * 64, Z, as_stream(stream), "conv1_wgrad_u8", 2.0 * R * 32 * C * 64);
+    return launch(p, 32, C * 64, Z, as_stream(stream), "conv1_wgrad_u8", fl);
   }
   Conv1Wgrad<float, CfgW32> p;
   set_wgrad(p, dz1, 32, R, Z, slab, slab_bias, C * 64);
   p.obs = (const float*)obs; p.idx = idx; p.row0 = row0; p.C = C;
-  return launch(p, 32, C * 64, Z, as_stream(stream), "conv1_wgrad_f32", 2.0 * R * 32 * C * 64);
+  return launch(p, 32, C * 64, Z, as_stream(stream), "conv1_wgrad_f32", fl);
 }
 
 PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, float* slab, float* slab_bias,
@@ -724,13 +827,27 @@ PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int 
   return launch(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K);
 }
 
+static int colsum(const float* src, long long ld, int Z, long long cols, ColMap map, float* out, float scale,
+                  int accumulate, hipStream_t st) {
+  if (cols <= 0) return 0;
+  colsum_kernel<<<ceil_div(cols, 32), 256, 0, st>>>(src, ld, Z, cols, map, out, scale, accumulate);
+  PPO_LAUNCH_CHECK("colsum_kernel");
+  return 0;
+}
+
+// Σ over the Z split partials (fixed order) -> gw (torch order, see ColMap) and gb
 PPO_API int ppo_wgrad_reduce(const float* slab, const float* slab_bias, int Z, int M, int NW, int kind, int a, int b,
                              float* gw, float* gb, float scale, int accumulate, void* stream) {
   PPO_REQUIRE(kind >= 0 && kind <= 2, "ppo_wgrad_reduce: kind=%d", kind);
-  const long long total = (long long)M * NW;
-  long long nb = (total + 255) / 256;
-  wgrad_reduce_kernel<<<(unsigned)(nb < 2048 ? nb : 2048), 256, 0, as_stream(stream)>>>(
-      slab, slab_bias, Z, M, NW, kind, a, b, gw, gb, scale, accumulate);
-  PPO_LAUNCH_CHECK("wgrad_reduce_kernel");
-  return 0;
+  hipStream_t st = as_stream(stream);
+  const long long cols = (long long)M * NW;
+  int rc = colsum(slab, cols, Z, cols, ColMap{kind, a, b, NW}, gw, scale, accumulate, st);
+  if (rc) return rc;
+  return colsum(slab_bias, M, Z, M, ColMap{0, 0, 0, 1}, gb, 1.0f, accumulate, st);
+}
+
+// generic deterministic column sum (used for the heads' partials)
+PPO_API int ppo_colsum(const float* src, long long ld, int rows, long long cols, float* out, float scale,
+                       int accumulate, void* stream) {
+  return colsum(src, ld, rows, cols, ColMap{0, 0, 0, 1}, out, scale, accumulate, as_stream(stream));
 }

@@ -295,40 +295,29 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
   }
 }
 
-// Σ over blocks (fixed order) of the head partials -> gradient planes;
-// loss partials -> acc[0..2] += {0.5·Σvl/B, -Σal/B, Σent/B} (double).
-__global__ __launch_bounds__(256) void heads_reduce_kernel(const float* __restrict__ part_w,
-                                                           const float* __restrict__ part_b,
-                                                           const float* __restrict__ part_loss, int nblk, int H,
-                                                           int A, float* __restrict__ g_wc, float* __restrict__ g_bc,
-                                                           float* __restrict__ g_wa, float* __restrict__ g_ba,
-                                                           double* __restrict__ loss_acc, double inv_b, float scale,
-                                                           int use_clipped) {
-  const int NO = 1 + A;
-  const long long total = (long long)NO * H;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    float s = 0.f;
-    for (int b = 0; b < nblk; ++b) s += part_w[(size_t)b * total + i];
-    s *= scale;
-    const int o = (int)(i / H), j = (int)(i % H);
-    if (o == 0) g_wc[j] = s;
-    else g_wa[(size_t)(o - 1) * H + j] = s;
+// loss partials -> acc[0..2] += {0.5·Σvl/B, -Σal/B, Σent/B} (double, fixed order)
+__global__ __launch_bounds__(256) void loss_reduce_kernel(const float* __restrict__ part_loss, int nblk,
+                                                          double* __restrict__ loss_acc, double inv_b) {
+  __shared__ double r[3][256];
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += 256) {
+    a0 += (double)part_loss[(size_t)b * 3];
+    a1 += (double)part_loss[(size_t)b * 3 + 1];
+    a2 += (double)part_loss[(size_t)b * 3 + 2];
   }
-  if (blockIdx.x == 0) {
-    if (threadIdx.x < NO) {
-      float s = 0.f;
-      for (int b = 0; b < nblk; ++b) s += part_b[(size_t)b * NO + threadIdx.x];
-      s *= scale;
-      if (threadIdx.x == 0) g_bc[0] = s;
-      else g_ba[threadIdx.x - 1] = s;
-    }
-    if (threadIdx.x >= 64 && threadIdx.x < 67 && loss_acc) {
-      const int q = threadIdx.x - 64;
-      double s = 0.0;
-      for (int b = 0; b < nblk; ++b) s += (double)part_loss[(size_t)b * 3 + q];
-      const double c = q == 0 ? (use_clipped ? 0.5 : 0.5) : (q == 1 ? -1.0 : 1.0);
-      loss_acc[q] += c * s * inv_b;
-    }
+  r[0][threadIdx.x] = a0;
+  r[1][threadIdx.x] = a1;
+  r[2][threadIdx.x] = a2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      for (int q = 0; q < 3; ++q) r[q][threadIdx.x] += r[q][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    loss_acc[0] += 0.5 * r[0][0] * inv_b;
+    loss_acc[1] += -r[1][0] * inv_b;
+    loss_acc[2] += r[2][0] * inv_b;
   }
 }
 
@@ -413,7 +402,7 @@ PPO_API int ppo_heads_act(const float* feat, int N, int H, const float* wc, cons
 }
 
 PPO_API int ppo_heads_train_blocks(int B) {
-  const int rpw = 16;
+  const int rpw = 32;
   return (int)ceil_div(B, HW * rpw);
 }
 
@@ -430,21 +419,28 @@ PPO_API int ppo_heads_train(const float* feat, int B, int H, const float* wc, co
   a.clip = clip; a.value_coef = value_coef; a.entropy_coef = entropy_coef; a.inv_b = inv_b;
   a.use_clipped_value_loss = use_clipped_value_loss;
   a.dfeat = dfeat; a.part_w = part_w; a.part_b = part_b; a.part_loss = part_loss;
-  a.rows_per_wave = 16;
+  a.rows_per_wave = 32;
   const int blocks = ppo_heads_train_blocks(B);
   hipStream_t st = as_stream(stream);
   if (A <= 8) return dispatch_train<8>(H / 64, a, blocks, st);
   return dispatch_train<16>(H / 64, a, blocks, st);
 }
 
+// Σ over the heads_train blocks (fixed order) -> head gradients; losses -> loss_acc
 PPO_API int ppo_heads_reduce(const float* part_w, const float* part_b, const float* part_loss, int nblk, int H, int A,
                              float* g_wc, float* g_bc, float* g_wa, float* g_ba, double* loss_acc, double inv_b,
                              float scale, int use_clipped_value_loss, void* stream) {
-  const long long total = (long long)(1 + A) * H;
-  long long nb = (total + 255) / 256;
-  heads_reduce_kernel<<<(unsigned)(nb < 1024 ? nb : 1024), 256, 0, as_stream(stream)>>>(
-      part_w, part_b, part_loss, nblk, H, A, g_wc, g_bc, g_wa, g_ba, loss_acc, inv_b, scale, use_clipped_value_loss);
-  PPO_LAUNCH_CHECK("heads_reduce_kernel");
+  (void)use_clipped_value_loss;  // both value losses are 0.5·mean(·)
+  const long long NO = 1 + A;
+  int rc;
+  if ((rc = ppo_colsum(part_w, NO * H, nblk, H, g_wc, scale, 0, stream))) return rc;
+  if ((rc = ppo_colsum(part_w + H, NO * H, nblk, (long long)A * H, g_wa, scale, 0, stream))) return rc;
+  if ((rc = ppo_colsum(part_b, NO, nblk, 1, g_bc, scale, 0, stream))) return rc;
+  if ((rc = ppo_colsum(part_b + 1, NO, nblk, A, g_ba, scale, 0, stream))) return rc;
+  if (loss_acc) {
+    loss_reduce_kernel<<<1, 256, 0, as_stream(stream)>>>(part_loss, nblk, loss_acc, inv_b);
+    PPO_LAUNCH_CHECK("loss_reduce_kernel");
+  }
   return 0;
 }
 

@@ -276,7 +276,8 @@ def test_trunk_forward_vs_torch_fp32(gpu, B, H):
     o1f = torch.empty_like(o1)
     Hh.call("ppo_conv1_fwd", xf.data_ptr(), 0, idx_d.data_ptr(), 0, 4, B, d["base.main.0.weight"].data_ptr(),
             d["base.main.0.bias"].data_ptr(), o1f.data_ptr(), _s())
-    assert torch.equal(o1f, o1)   # u8 decode is bit-identical to u8.float()/255
+    # u8 path folds the 1/255 into the accumulator: within fp32 rounding of the f32 path
+    assert (o1f - o1).abs().max().item() <= 2e-6 * max(1.0, o1.abs().max().item())
 
 
 @pytest.mark.parametrize("B,H", [(6, 64), (33, 512)])

@@ -47,7 +47,7 @@ def test_host_only_queries():
     assert _hip.call("ppo_packed_weights_size", 512) == 64 * 512 + 32 * 576 + 2 * 512 * 1568 + 64 * 288 + 4 * 32 * 256
     z = _hip.call("ppo_wgrad_splits", 65536 * 400, 1, 2048, 16)
     assert 1 <= z <= 4096
-    assert _hip.call("ppo_heads_train_blocks", 65536) == 65536 // 64
+    assert _hip.call("ppo_heads_train_blocks", 65536) == 65536 // 128
 
 
 def test_u8_decode_exact_for_all_codes():

@@ -1,0 +1,121 @@
+#!/usr/bin/env python3
+"""Per-kernel micro-benchmark of the trunk GEMMs at the PPO minibatch size
+(B = 4096*128/8 = 65536 samples) through the C ABI.  Prints ms and TFLOP/s per
+kernel; used with rocprofv3 --pmc for counter passes.
+
+  python tools/kbench.py [--B 65536] [--reps 5] [--only conv1_fwd,conv2_dgrad]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ppo-dash_amd")]
+
+import torch  # noqa: E402
+
+from a2c_ppo_acktr._hip import call  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=65536)
+    ap.add_argument("--H", type=int, default=512)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--tune", default="", help="key=v[,key=v...] tile variants (ppo_tune_set)")
+    a = ap.parse_args()
+    for kv in [x for x in a.tune.split(",") if x]:
+        k, v = kv.split("=")
+        call("ppo_tune_set", k.encode(), int(v))
+    B, H = a.B, a.H
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    rows = B + 4096
+    obs = torch.randint(0, 256, (rows, 4, 84, 84), dtype=torch.uint8, device=dev, generator=g)
+    idx = torch.randperm(rows, device=dev)[:B].contiguous()
+
+    def rn(*s, sc=0.05):
+        return torch.randn(*s, device=dev, generator=g) * sc
+
+    w1, b1 = rn(32, 256), rn(32)
+    w2, b2 = rn(64, 512), rn(64)
+    w3, b3 = rn(32, 576), rn(32)
+    w4, b4 = rn(H, 1568), rn(H)
+    packed = torch.empty(call("ppo_packed_weights_size", H), device=dev)
+    offs = torch.zeros(6, dtype=torch.int64)
+    call("ppo_packed_offsets", H, offs.data_ptr())
+    pk = [packed.data_ptr() + 4 * int(o) for o in offs]
+    s = torch.cuda.current_stream().cuda_stream
+    call("ppo_pack_weights", w2.data_ptr(), w3.data_ptr(), w4.data_ptr(), H, packed.data_ptr(), s)
+    a1 = torch.empty(B * 400 * 32, device=dev)
+    a2 = torch.empty(B * 81 * 64, device=dev)
+    a3 = torch.empty(B * 1568, device=dev)
+    h = torch.empty(B * H, device=dev)
+    dh = rn(B * H, sc=1e-3)
+    dz3 = torch.empty(B * 1568, device=dev)
+    dz2 = torch.empty(B * 81 * 64, device=dev)
+    dz1 = torch.empty(B * 400 * 32, device=dev)
+    gw = torch.empty(H * 1568 + 1024, device=dev)
+    gb = torch.empty(1024, device=dev)
+    Zmax = 4096
+    slab = torch.empty(Zmax * 32 * 576 + Zmax * 64 * 512, device=dev)
+    slab_b = torch.empty(Zmax * 512, device=dev)
+
+    def zs(R, tiles):
+        return call("ppo_wgrad_splits", R, tiles, 2048, 16)
+
+    z1, z2, z3, z4 = zs(B * 400, 1), zs(B * 81, 4), zs(B * 49, 5), zs(B, ((H + 127) // 128) * 13)
+    K = {
+        "conv1_fwd": (lambda: call("ppo_conv1_fwd", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, w1.data_ptr(),
+                                   b1.data_ptr(), a1.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
+        "conv2_fwd": (lambda: call("ppo_conv2_fwd", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2.data_ptr(), s),
+                      2.0 * B * 81 * 64 * 512),
+        "conv3_fwd": (lambda: call("ppo_conv3_fwd", a2.data_ptr(), B, pk[1], b3.data_ptr(), a3.data_ptr(), s),
+                      2.0 * B * 49 * 32 * 576),
+        "fc_fwd": (lambda: call("ppo_linear_relu_fwd", a3.data_ptr(), B, 1568, pk[2], b4.data_ptr(), H, h.data_ptr(),
+                                s), 2.0 * B * 1568 * H),
+        "fc_dgrad": (lambda: call("ppo_linear_dgrad_mask", dh.data_ptr(), B, H, pk[3], 1568, a3.data_ptr(),
+                                  dz3.data_ptr(), s), 2.0 * B * 1568 * H),
+        "fc_wgrad": (lambda: call("ppo_linear_wgrad", dh.data_ptr(), a3.data_ptr(), B, H, 1568, z4, slab.data_ptr(),
+                                  slab_b.data_ptr(), s), 2.0 * B * 1568 * H),
+        "fc_wreduce": (lambda: call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), z4, H, 1568, 2, 32, 49,
+                                    gw.data_ptr(), gb.data_ptr(), 1.0, 0, s), 0.0),
+        "conv3_dgrad": (lambda: call("ppo_conv3_dgrad", dz3.data_ptr(), B, pk[4], a2.data_ptr(), dz2.data_ptr(), s),
+                        2.0 * B * 49 * 32 * 576),
+        "conv3_wgrad": (lambda: call("ppo_conv3_wgrad", dz3.data_ptr(), a2.data_ptr(), B, z3, slab.data_ptr(),
+                                     slab_b.data_ptr(), s), 2.0 * B * 49 * 32 * 576),
+        "conv2_dgrad": (lambda: call("ppo_conv2_dgrad", dz2.data_ptr(), B, pk[5], a1.data_ptr(), dz1.data_ptr(), s),
+                        2.0 * B * 81 * 64 * 512),
+        "conv2_wgrad": (lambda: call("ppo_conv2_wgrad", dz2.data_ptr(), a1.data_ptr(), B, z2, slab.data_ptr(),
+                                     slab_b.data_ptr(), s), 2.0 * B * 81 * 64 * 512),
+        "conv1_wgrad": (lambda: call("ppo_conv1_wgrad", dz1.data_ptr(), obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, z1,
+                                     slab.data_ptr(), slab_b.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
+        "conv1_wreduce": (lambda: call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), z1, 32, 256, 0, 0, 0,
+                                       gw.data_ptr(), gb.data_ptr(), 1.0 / 255, 0, s), 0.0),
+    }
+    # realistic activations for the backward kernels
+    K["conv1_fwd"][0](); K["conv2_fwd"][0](); K["conv3_fwd"][0](); K["fc_fwd"][0]()
+    K["fc_dgrad"][0](); K["conv3_dgrad"][0](); K["conv2_dgrad"][0]()
+    torch.cuda.synchronize()
+    only = [x for x in a.only.split(",") if x]
+    total = 0.0
+    for name, (fn, fl) in K.items():
+        if only and name not in only:
+            continue
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / a.reps
+        total += ms
+        tf = fl / (ms * 1e-3) / 1e12 if fl else 0.0
+        print(f"{name:14s} {ms:8.3f} ms  {tf:7.1f} TFLOP/s", flush=True)
+    print(f"{'total':14s} {total:8.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
