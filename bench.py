@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--hidden", type=int, default=512)
     p.add_argument("--profile-kernel", default="conv1_fwd_u8")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-envs", type=int, default=16)
+    p.add_argument("--cpu-envs", type=int, default=32)
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-gae-roofline", action="store_true")
     p.add_argument("--gae-lanes", type=int, default=1 << 20)
@@ -89,6 +89,19 @@ def gae_roofline(device, lanes, T=128, reps=10):
             "frac": round(gbps / PEAK_HBM_GBPS, 4), "traffic": None,
             "config": f"T={T} x {lanes} lanes (fp32 planes, {nbytes / 1e9:.2f} GB algorithmic per launch)",
             "ms_per_launch": round(ms, 4)}
+
+
+def pmc_traffic(kernel):
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/roofline_traffic.json, written by tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "roofline_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    if d.get("kernel") != kernel:
+        return None, None
+    return d.get("traffic_bytes_per_launch"), f"profiles/{d.get('tag', '?')}_traffic.json"
 
 
 def cpu_baseline(envs, T, E, M, hidden, threads):
@@ -191,8 +204,11 @@ def main():
     roof = None
     if launches > 0 and ms_total > 0:
         tflops = flops / (ms_total * 1e-3) / 1e12
+        traffic, tsrc = pmc_traffic(args.profile_kernel)
         roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(tflops / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                "frac": round(tflops / PEAK_FP32_MFMA_TFLOPS, 4),
+                "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch (HBM, PMC)",
+                "traffic_source": tsrc,
                 "kernel": args.profile_kernel, "launches": int(launches),
                 "avg_launch_ms": round(ms_total / launches, 4),
                 "flop_per_launch": round(flops / launches)}
