@@ -93,6 +93,12 @@ int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, flo
 /* model.py:180 Linear(1568,H)+ReLU (generic Linear+ReLU) */
 int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, const float* b, int N, float* out,
                         void* stream);
+/* Linear with row strides and optional ReLU / bias (GRU input projection, fc into a
+ * padded [x | vector_obs] row) */
+int ppo_linear_fwd_ex(const float* x, int M, int K, int lda, const float* w, const float* b, int N, float* out,
+                      int ldo, int relu, void* stream);
+int ppo_linear_dgrad_ex(const float* dy, int M, int K, const float* wt, int N, const float* act, int ldact, float* dx,
+                        void* stream);
 /* algo/ppo.py:80-81 loss.backward() through the trunk: dgrad with the ReLU mask
  * of the layer below fused, wgrad as split-K partial slabs + deterministic reduce */
 int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
@@ -116,6 +122,28 @@ int ppo_colsum(const float* src, long long ld, int rows, long long cols, float* 
 /* tile-configuration variant of a GEMM family (development A/B knob; 0 = default) */
 int ppo_tune_set(const char* key, int value);
 
+/* ---------------- GRU (model.py:89-95, 111-166) ---------------------------- */
+/* one step h' = GRU(gi, h_prev·mask) with the cell fused into the W_hh GEMM;
+ * save_* (all or none) keep r, z, n, W_hn·h+b_hn, h_in for the backward */
+int ppo_gru_step_fwd(const float* hprev, const float* masks, const int64_t* mask_idx, const float* whh,
+                     const float* bhh, const float* gi, int M, int H, float* hout, float* save_r, float* save_z,
+                     float* save_n, float* save_ghn, float* save_hin, void* stream);
+/* backward of one step: gate gradients (dgi, dgh rows [M][3H]) and dh'·z */
+int ppo_gru_cell_bwd(const float* dout, const float* carry, const float* r, const float* z, const float* n,
+                     const float* ghn, const float* hin, float* dgi, float* dgh, float* dhz, int M, int H,
+                     int has_carry, void* stream);
+/* carry(t-1) = (dgh·W_hh + dh'·z)·mask(t) */
+int ppo_gru_step_bwd(const float* dgh, const float* whhT, const float* dhz, const float* masks,
+                     const int64_t* mask_idx, float* carry, int M, int H, void* stream);
+/* W_ih -> zero-padded [3H][Ip], W_ih[:, :H]ᵀ [H][3H], W_hhᵀ [H][3H] */
+int ppo_gru_pack(const float* wih, const float* whh, int H, int I, int Ip, float* wih_pad, float* wihT, float* whhT,
+                 void* stream);
+/* model.py:195 torch.cat((x, vector_inputs)): dst[r][col0 + c] = src[idx(r)][c], zero pad */
+int ppo_concat_cols(const float* src, const int64_t* idx, long long rows, int ncols, float* dst, int ld, int col0,
+                    int zero_to, void* stream);
+/* storage.py:195-220 recurrent minibatch sample order: idx[t*n + j] = t*N + envs[j] */
+int ppo_rec_indices(const int64_t* envs, int n, int T, int N, int64_t* idx, void* stream);
+
 /* ---------------- heads, distribution, loss -------------------------------- */
 /* model.py:54-79 act / get_value / evaluate_actions heads + distributions.py:17-27
  * FixedCategorical: value, logits, logsumexp, sample = argmax(probs/E) (noise =
@@ -130,8 +158,8 @@ int ppo_heads_train_blocks(int B);
 int ppo_heads_train(const float* feat, int B, int H, const float* wc, const float* bc, const float* wa,
                     const float* ba, int A, const int64_t* idx, long long row0, const int64_t* actions,
                     const float* old_logp, const float* adv, const float* vpred, const float* ret, float clip,
-                    float value_coef, float entropy_coef, float inv_b, int use_clipped_value_loss, float* dfeat,
-                    float* part_w, float* part_b, float* part_loss, void* stream);
+                    float value_coef, float entropy_coef, float inv_b, int use_clipped_value_loss, int feat_relu,
+                    float* dfeat, float* part_w, float* part_b, float* part_loss, void* stream);
 int ppo_heads_reduce(const float* part_w, const float* part_b, const float* part_loss, int nblk, int H, int A,
                      float* g_wc, float* g_bc, float* g_wa, float* g_ba, double* loss_acc, double inv_b, float scale,
                      int use_clipped_value_loss, void* stream);

@@ -307,6 +307,96 @@ def gru_sequence(p, x, h0, masks):
     return np.concatenate(outs, 0), h
 
 
+def gru_sequence_cache(p, x, h0, masks):
+    """gru_sequence with everything the backward needs; x [T*n, I], masks [T, n]."""
+    T, n = masks.shape[:2]
+    xs = x.reshape(T, n, -1)
+    H = h0.shape[1]
+    Wih, Whh = p["base.gru.weight_ih_l0"], p["base.gru.weight_hh_l0"]
+    bih, bhh = p["base.gru.bias_ih_l0"], p["base.gru.bias_hh_l0"]
+    h = np.asarray(h0, np.float64)
+    cache = []
+    outs = []
+    for t in range(T):
+        hin = h * masks[t].reshape(n, 1)
+        gi = xs[t] @ Wih.T + bih
+        gh = hin @ Whh.T + bhh
+        r = sigmoid(gi[:, :H] + gh[:, :H])
+        z = sigmoid(gi[:, H:2 * H] + gh[:, H:2 * H])
+        nn_ = np.tanh(gi[:, 2 * H:] + r * gh[:, 2 * H:])
+        h = (1 - z) * nn_ + z * hin
+        cache.append((hin, r, z, nn_, gh[:, 2 * H:]))
+        outs.append(h)
+    return np.concatenate(outs, 0), cache
+
+
+def gru_backward(p, x, masks, cache, dout):
+    """BPTT of gru_sequence_cache: dout [T*n, H] = dL/d(outputs) -> (grads, dx [T*n, I])."""
+    T, n = masks.shape[:2]
+    H = cache[0][0].shape[1]
+    Wih, Whh = p["base.gru.weight_ih_l0"], p["base.gru.weight_hh_l0"]
+    xs = x.reshape(T, n, -1)
+    do = dout.reshape(T, n, H)
+    g = {k: np.zeros_like(p[k]) for k in ("base.gru.weight_ih_l0", "base.gru.weight_hh_l0",
+                                          "base.gru.bias_ih_l0", "base.gru.bias_hh_l0")}
+    dx = np.zeros_like(xs)
+    carry = np.zeros((n, H))
+    for t in range(T - 1, -1, -1):
+        hin, r, z, nn_, ghn = cache[t]
+        dh = do[t] + carry
+        dn = dh * (1 - z)
+        dz = dh * (hin - nn_)
+        dan = dn * (1 - nn_ ** 2)
+        dar = dan * ghn * r * (1 - r)
+        daz = dz * z * (1 - z)
+        dgi = np.concatenate([dar, daz, dan], 1)
+        dgh = np.concatenate([dar, daz, dan * r], 1)
+        g["base.gru.weight_ih_l0"] += dgi.T @ xs[t]
+        g["base.gru.bias_ih_l0"] += dgi.sum(0)
+        g["base.gru.weight_hh_l0"] += dgh.T @ hin
+        g["base.gru.bias_hh_l0"] += dgh.sum(0)
+        dx[t] = dgi @ Wih
+        carry = (dh * z + dgh @ Whh) * masks[t].reshape(n, 1)
+    return g, dx.reshape(T * n, -1)
+
+
+def recurrent_forward(p, obs_f32, vec, h0, masks):
+    """CNNBase(recurrent) forward over a [T*n] sequence batch (rows t*n + j)."""
+    feat, cache = cnn_trunk(p, obs_f32)
+    x = np.concatenate([feat, np.asarray(vec, np.float64).reshape(feat.shape[0], -1)], 1)
+    out, gcache = gru_sequence_cache(p, x, h0, masks)
+    value, logits = heads(p, out)
+    cache.update(x=x, gcache=gcache, out=out, masks=masks)
+    return value, logits, cache
+
+
+def recurrent_backward(p, cache, g_value, g_logits):
+    H = p["base.main.7.weight"].shape[0]
+    out = cache["out"]
+    g = {}
+    g["base.critic_linear.weight"] = g_value[None, :] @ out
+    g["base.critic_linear.bias"] = np.array([g_value.sum()])
+    g["dist.linear.weight"] = g_logits.T @ out
+    g["dist.linear.bias"] = g_logits.sum(0)
+    dout = g_value[:, None] * p["base.critic_linear.weight"] + g_logits @ p["dist.linear.weight"]
+    gg, dx = gru_backward(p, cache["x"], cache["masks"], cache["gcache"], dout)
+    g.update(gg)
+    dz4 = dx[:, :H] * (cache["h"] > 0)
+    g["base.main.7.weight"] = dz4.T @ cache["f"]
+    g["base.main.7.bias"] = dz4.sum(0)
+    da3 = (dz4 @ p["base.main.7.weight"]).reshape(cache["a3"].shape)
+    dz3 = da3 * (cache["a3"] > 0)
+    dw, db, da2 = _conv_bwd(dz3, cache["c3"], p["base.main.4.weight"], cache["a2"].shape, 1)
+    g["base.main.4.weight"], g["base.main.4.bias"] = dw, db
+    dz2 = da2 * (cache["a2"] > 0)
+    dw, db, da1 = _conv_bwd(dz2, cache["c2"], p["base.main.2.weight"], cache["a1"].shape, 2)
+    g["base.main.2.weight"], g["base.main.2.bias"] = dw, db
+    dz1 = da1 * (cache["a1"] > 0)
+    dw, db, _ = _conv_bwd(dz1, cache["c1"], p["base.main.0.weight"], cache["x_shape"], 4, need_dx=False)
+    g["base.main.0.weight"], g["base.main.0.bias"] = dw, db
+    return g
+
+
 # ---------------------------------------------------------------------------
 # PPO loss and its gradients (algo/ppo.py:61-81) with torch's autograd
 # conventions: min/max split the gradient 1/2-1/2 at ties; clamp passes it

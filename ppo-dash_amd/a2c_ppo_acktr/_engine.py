@@ -1,13 +1,18 @@
-"""HIP execution engine behind Policy / PPO (CNNBase, feed-forward).
+"""HIP execution engines behind Policy / PPO.
 
-Owns the flat parameter / gradient buffers (every nn.Parameter of the Policy is
-re-pointed to a view of one contiguous fp32 buffer, so clip + Adam is one pass),
-the per-step packed weight copies, and grow-only activation workspaces.
+CNNEngine        CNNBase, feed-forward (model.py:169-199)
+RecurrentEngine  CNNBase + [vector obs] + GRU (model.py:89-166, 192-199)
 
-Call sequence per PPO minibatch (every box is a libppo_hip.so kernel):
-  conv1(obs rows gathered by index, u8 decode) -> conv2 -> conv3 -> fc        (MFMA fwd)
-  heads_train (value/logits/Categorical/PPO loss + dL/dlogits, dL/dfeat)    (fused)
-  fc dgrad | fc wgrad | conv3 dgrad | conv3 wgrad | conv2 dgrad | conv2 wgrad | conv1 wgrad  (MFMA bwd)
+Each owns the flat parameter / gradient buffers (every nn.Parameter of the
+Policy is re-pointed to a view of one contiguous fp32 buffer, so clip + Adam is
+one pass), the per-step packed weight copies, and grow-only workspaces.
+
+Per PPO minibatch (every box is a libppo_hip.so kernel):
+  conv1(obs rows gathered by index, u8) -> conv2 -> conv3 -> fc       (MFMA fwd)
+  [recurrent: concat vector obs -> gi = x·W_ihᵀ -> T x fused GRU step]
+  heads_train (value/logits/Categorical/PPO loss + dL/dlogits, dL/dfeature)
+  [recurrent: T x (gate grads, dh·W_hh), dW_hh, dW_ih, dx]
+  fc dgrad | fc wgrad | conv3 dgrad | conv3 wgrad | conv2 dgrad | conv2 wgrad | conv1 wgrad
   wgrad slab reduces -> flat grad  [RCCL all-reduce when world_size > 1]
   grad Σg² -> clip + Adam -> pack weights
 """
@@ -31,7 +36,11 @@ class _Workspace:
 
 
 class CNNEngine:
-    """Binds to a Policy whose base is CNNBase (non-recurrent)."""
+    """Binds to a Policy whose base is a non-recurrent CNNBase."""
+
+    # parameter indices in policy.parameters() order (named_parameters order)
+    W1, B1, W2, B2, W3, B3, W4, B4, WC, BC, WA, BA = range(12)
+    recurrent = False
 
     def __init__(self, policy, device):
         self.policy = policy
@@ -40,9 +49,9 @@ class CNNEngine:
         self.C = base.main[0].weight.shape[1]
         self.H = base.main[7].weight.shape[0]
         self.A = policy.dist.linear.weight.shape[0]
-        if self.H % 64 != 0:
-            raise NotImplementedError(f"hidden_size {self.H}: the HIP heads need a multiple of 64 (64..512)")
-        if base.critic_linear.weight.shape[1] != self.H:
+        if self.H > 512 or self.H % 4 != 0:
+            raise NotImplementedError(f"hidden_size {self.H}: the HIP engine supports multiples of 4 up to 512")
+        if not self.recurrent and base.critic_linear.weight.shape[1] != self.H:
             raise NotImplementedError("vector observations with a non-recurrent CNNBase are not supported "
                                       "(the reference crashes there too: Categorical expects hidden_size inputs)")
         self.params = list(policy.parameters())
@@ -73,8 +82,6 @@ class CNNEngine:
         self.epoch += 1
 
     def is_bound(self):
-        if self.flat is None:
-            return False
         base = self.flat.data_ptr()
         for p, off in zip(self.params, self.offsets):
             if p.data.data_ptr() != base + 4 * off or not p.is_cuda:
@@ -92,50 +99,55 @@ class CNNEngine:
     def gv(self, i):
         return self.grad.data_ptr() + 4 * self.offsets[i]
 
-    # parameter indices (CNNBase non-recurrent, named_parameters order)
-    W1, B1, W2, B2, W3, B3, W4, B4, WC, BC, WA, BA = range(12)
-
     def pack(self, force=False):
         key = (sum(p._version for p in self.params), self.epoch)
         if not force and self.packed is not None and key == self._pack_key:
             return
         if self.packed is None:
             self.packed = torch.empty(call("ppo_packed_weights_size", self.H), device=self.device)
-            offs = (torch.zeros(6, dtype=torch.int64))
+            offs = torch.zeros(6, dtype=torch.int64)
             call("ppo_packed_offsets", self.H, offs.data_ptr())
             self.poff = [int(x) for x in offs]
         call("ppo_pack_weights", self.pv(self.W2), self.pv(self.W3), self.pv(self.W4), self.H,
              self.packed.data_ptr(), stream())
+        self._pack_extra()
         self._pack_key = key
+
+    def _pack_extra(self):
+        pass
 
     def pk(self, seg):
         """pointer to packed segment: 0 W2p 1 W3p 2 W4p 3 W4T 4 W3d 5 W2d"""
         return self.packed.data_ptr() + 4 * self.poff[seg]
 
     # ---------------------------------------------------------------- forward
-    def _obs_args(self, obs):
+    @staticmethod
+    def _obs_args(obs):
         if obs.dtype == torch.uint8:
             return 1
         if obs.dtype == torch.float32:
             return 0
         raise TypeError(f"observations must be uint8 or float32, got {obs.dtype}")
 
-    def trunk(self, obs, idx, B, ws):
+    def trunk(self, obs, idx, B, ws, out=None, ldo=None):
         """conv1..fc on B samples: obs is either a [B,C,84,84] batch (idx None) or the
-        storage plane whose rows idx[b] are gathered inside conv1.  Returns feat [B,H]."""
+        storage plane whose rows idx[b] are gathered inside conv1.  Writes the fc
+        output (post-ReLU) to `out` (row stride ldo) or a workspace [B,H]."""
         dev = self.device
         is_u8 = self._obs_args(obs)
         a1 = ws.get("a1", B * 400 * 32, device=dev)
         a2 = ws.get("a2", B * 81 * 64, device=dev)
         a3 = ws.get("a3", B * FEAT, device=dev)
-        h = ws.get("h", B * self.H, device=dev)
+        if out is None:
+            out, ldo = ws.get("h", B * self.H, device=dev), self.H
         s = stream()
         call("ppo_conv1_fwd", obs.data_ptr(), is_u8, ptr(idx, torch.int64, "idx"), 0, self.C, B, self.pv(self.W1),
              self.pv(self.B1), a1.data_ptr(), s)
         call("ppo_conv2_fwd", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), s)
         call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
-        call("ppo_linear_relu_fwd", a3.data_ptr(), B, FEAT, self.pk(2), self.pv(self.B4), self.H, h.data_ptr(), s)
-        return h
+        call("ppo_linear_fwd_ex", a3.data_ptr(), B, FEAT, FEAT, self.pk(2), self.pv(self.B4), self.H, out.data_ptr(),
+             ldo, 1, s)
+        return out
 
     def _check_obs(self, obs):
         obs = obs if obs.is_cuda else obs.to(self.device)
@@ -143,13 +155,7 @@ class CNNEngine:
             raise RuntimeError(f"CNNBase expects [N,{self.C},84,84] observations, got {tuple(obs.shape)}")
         return obs.contiguous()
 
-    def act(self, obs, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False):
-        self.ensure_bound()
-        self.pack()
-        obs = self._check_obs(obs)
-        B = obs.shape[0]
-        ws = self.ws["act"]
-        h = self.trunk(obs, None, B, ws)
+    def _heads(self, h, B, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False):
         value = torch.empty(B, 1, device=self.device)
         if value_only:
             action = logp = ent = None
@@ -169,52 +175,64 @@ class CNNEngine:
              ptr(logp), ptr(ent), stream())
         return value, action, logp, ent
 
+    def act(self, obs, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False):
+        self.ensure_bound()
+        self.pack()
+        obs = self._check_obs(obs)
+        B = obs.shape[0]
+        h = self.trunk(obs, None, B, self.ws["act"])
+        return self._heads(h, B, deterministic, noise, given, want_entropy, value_only)
+
     # --------------------------------------------------------------- training
+    def _heads_train(self, storage, adv, idx, feat, B, hp, loss_acc, dfeat, feat_relu):
+        ws, dev, H, A, s = self.ws["train"], self.device, self.H, self.A, stream()
+        nblk = call("ppo_heads_train_blocks", B)
+        part_w = ws.get("part_w", nblk * (1 + A) * H, device=dev)
+        part_b = ws.get("part_b", nblk * (1 + A), device=dev)
+        part_l = ws.get("part_l", nblk * 3, device=dev)
+        inv_b = 1.0 / B
+        call("ppo_heads_train", feat.data_ptr(), B, H, self.pv(self.WC), self.pv(self.BC), self.pv(self.WA),
+             self.pv(self.BA), A, idx.data_ptr(), 0, storage.actions.data_ptr(), storage.action_log_probs.data_ptr(),
+             adv.data_ptr(), storage.value_preds.data_ptr(), storage.returns.data_ptr(), hp["clip"], hp["value_coef"],
+             hp["entropy_coef"], inv_b, int(hp["use_clipped_value_loss"]), int(feat_relu), dfeat.data_ptr(),
+             part_w.data_ptr(), part_b.data_ptr(), part_l.data_ptr(), s)
+        call("ppo_heads_reduce", part_w.data_ptr(), part_b.data_ptr(), part_l.data_ptr(), nblk, H, A,
+             self.gv(self.WC), self.gv(self.BC), self.gv(self.WA), self.gv(self.BA), loss_acc.data_ptr(), inv_b, 1.0,
+             int(hp["use_clipped_value_loss"]), s)
+
+    def _trunk_backward(self, B, dh, obs, idx):
+        """dh: dL/d(fc pre-activation) [B,H] (ReLU mask applied) -> trunk gradients."""
+        ws, dev, s = self.ws["train"], self.device, stream()
+        a1, a2, a3 = ws.bufs["a1"], ws.bufs["a2"], ws.bufs["a3"]
+        dz3 = ws.get("dz3", B * FEAT, device=dev)
+        dz2 = ws.get("dz2", B * 81 * 64, device=dev)
+        dz1 = ws.get("dz1", B * 400 * 32, device=dev)
+        call("ppo_linear_dgrad_mask", dh.data_ptr(), B, self.H, self.pk(3), FEAT, a3.data_ptr(), dz3.data_ptr(), s)
+        self._wgrad("fc", B, dh, a3, None, s)
+        call("ppo_conv3_dgrad", dz3.data_ptr(), B, self.pk(4), a2.data_ptr(), dz2.data_ptr(), s)
+        self._wgrad("conv3", B, dz3, a2, None, s)
+        call("ppo_conv2_dgrad", dz2.data_ptr(), B, self.pk(5), a1.data_ptr(), dz1.data_ptr(), s)
+        self._wgrad("conv2", B, dz2, a1, None, s)
+        self._wgrad("conv1", B, dz1, obs, idx, s)
+
+    def _finish_step(self, optimizer):
+        optimizer._step_flat(self)
+        self.epoch += 1
+        self.pack(force=True)
+
     def train_minibatch(self, storage, adv, idx, hp, loss_acc, optimizer):
         """Forward + backward + (all-reduce) + clip + Adam for one minibatch of
         storage rows idx (int64 [B], device)."""
         self.ensure_bound()
         self.pack()
-        dev, H, A = self.device, self.H, self.A
         B = idx.numel()
         ws = self.ws["train"]
-        s = stream()
-        obs = storage.obs
-        h = self.trunk(obs, idx, B, ws)
-        a1, a2, a3 = ws.bufs["a1"], ws.bufs["a2"], ws.bufs["a3"]
-        nblk = call("ppo_heads_train_blocks", B)
-        dh = ws.get("dh", B * H, device=dev)
-        part_w = ws.get("part_w", nblk * (1 + A) * H, device=dev)
-        part_b = ws.get("part_b", nblk * (1 + A), device=dev)
-        part_l = ws.get("part_l", nblk * 3, device=dev)
-        inv_b = 1.0 / B
-        call("ppo_heads_train", h.data_ptr(), B, H, self.pv(self.WC), self.pv(self.BC), self.pv(self.WA),
-             self.pv(self.BA), A, idx.data_ptr(), 0, storage.actions.data_ptr(), storage.action_log_probs.data_ptr(),
-             adv.data_ptr(), storage.value_preds.data_ptr(), storage.returns.data_ptr(), hp["clip"], hp["value_coef"],
-             hp["entropy_coef"], inv_b, int(hp["use_clipped_value_loss"]), dh.data_ptr(), part_w.data_ptr(),
-             part_b.data_ptr(), part_l.data_ptr(), s)
-        call("ppo_heads_reduce", part_w.data_ptr(), part_b.data_ptr(), part_l.data_ptr(), nblk, H, A,
-             self.gv(self.WC), self.gv(self.BC), self.gv(self.WA), self.gv(self.BA), loss_acc.data_ptr(), inv_b, 1.0,
-             int(hp["use_clipped_value_loss"]), s)
-        dz3 = ws.get("dz3", B * FEAT, device=dev)
-        dz2 = ws.get("dz2", B * 81 * 64, device=dev)
-        dz1 = ws.get("dz1", B * 400 * 32, device=dev)
-        # fc
-        call("ppo_linear_dgrad_mask", dh.data_ptr(), B, H, self.pk(3), FEAT, a3.data_ptr(), dz3.data_ptr(), s)
-        self._wgrad("fc", B, dh, a3, None, s)
-        # conv3
-        call("ppo_conv3_dgrad", dz3.data_ptr(), B, self.pk(4), a2.data_ptr(), dz2.data_ptr(), s)
-        self._wgrad("conv3", B, dz3, a2, None, s)
-        # conv2
-        call("ppo_conv2_dgrad", dz2.data_ptr(), B, self.pk(5), a1.data_ptr(), dz1.data_ptr(), s)
-        self._wgrad("conv2", B, dz2, a1, None, s)
-        # conv1 (weights only)
-        self._wgrad("conv1", B, dz1, obs, idx, s)
-        optimizer._step_flat(self)
-        self.epoch += 1
-        self.pack(force=True)
+        h = self.trunk(storage.obs, idx, B, ws)
+        dh = ws.get("dh", B * self.H, device=self.device)
+        self._heads_train(storage, adv, idx, h, B, hp, loss_acc, dh, feat_relu=True)
+        self._trunk_backward(B, dh, storage.obs, idx)
+        self._finish_step(optimizer)
 
-    # wgrad layer table: (M rows, NW cols, reduce kind, a, b, w index, b index, tiles)
     def _wgrad(self, layer, B, dz, x, idx, s):
         dev = self.device
         ws = self.ws["train"]
@@ -243,3 +261,149 @@ class CNNEngine:
         scale = 1.0 / 255.0 if layer == "conv1" and x.dtype == torch.uint8 else 1.0   # u8 staged as integers
         call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, M, NW, kind, ka, kb, self.gv(wi), self.gv(bi),
              scale, 0, s)
+
+    def _dense_wgrad(self, dy, x, R, N, K, kind, a, wi, bi):
+        """dW[n][k] = Σ_r dy[r][n] x[r][k] (+ bias) -> grad planes wi, bi"""
+        ws, dev, s = self.ws["train"], self.device, stream()
+        tiles = ((N + 127) // 128) * ((K + 127) // 128)
+        Z = call("ppo_wgrad_splits", R, tiles, 2048, 16)
+        slab = ws.get("slab", Z * N * K, device=dev)
+        slab_b = ws.get("slab_b", Z * N, device=dev)
+        call("ppo_linear_wgrad", dy.data_ptr(), x.data_ptr(), R, N, K, Z, slab.data_ptr(), slab_b.data_ptr(), s)
+        call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, N, K, kind, a, 0, self.gv(wi), self.gv(bi),
+             1.0, 0, s)
+
+
+class RecurrentEngine(CNNEngine):
+    """CNNBase(recurrent=True) + vector obs: x = cat(fc(obs), vec) -> GRU -> heads.
+    Parameter order: gru.{weight_ih, weight_hh, bias_ih, bias_hh}, main.*, critic, dist."""
+
+    GIH, GHH, GBI, GBH = range(4)
+    W1, B1, W2, B2, W3, B3, W4, B4, WC, BC, WA, BA = range(4, 16)
+    recurrent = True
+
+    def __init__(self, policy, device):
+        gru = policy.base.gru
+        self.V = policy.base.vector_obs_len
+        H = policy.base.main[7].weight.shape[0]
+        self.I = H + self.V
+        self.Ip = (self.I + 3) // 4 * 4   # GEMM rows padded to 16-B multiples
+        if gru.weight_ih_l0.shape != (3 * H, self.I) or H % 32 != 0:
+            raise NotImplementedError("GRU engine needs hidden_size a multiple of 32 (<= 512)")
+        self.gru_packed = None
+        super().__init__(policy, device)
+
+    def _pack_extra(self):
+        H, Ip = self.H, self.Ip
+        if self.gru_packed is None:
+            self.gru_packed = torch.empty(3 * H * Ip + 6 * H * H, device=self.device)
+        gp = self.gru_packed.data_ptr()
+        self.wih_pad, self.wihT, self.whhT = gp, gp + 4 * 3 * H * Ip, gp + 4 * (3 * H * Ip + 3 * H * H)
+        call("ppo_gru_pack", self.pv(self.GIH), self.pv(self.GHH), H, self.I, Ip, self.wih_pad, self.wihT, self.whhT,
+             stream())
+
+    def _input(self, obs, vec, idx, B, ws, rows_vec=None):
+        """x_pad [B][Ip] = (fc(obs) | vector obs | 0-pad) and gi = x·W_ihᵀ + b_ih [B][3H]."""
+        dev, s, H, Ip = self.device, stream(), self.H, self.Ip
+        x = ws.get("xpad", B * Ip, device=dev)
+        self.trunk(obs, idx, B, ws, out=x, ldo=Ip)
+        if Ip > H:
+            src = vec if vec is not None else x   # V == 0: only the zero pad is written
+            call("ppo_concat_cols", src.data_ptr(), ptr(rows_vec), B, self.V if vec is not None else 0,
+                 x.data_ptr(), Ip, H, Ip - H, s)
+        gi = ws.get("gi", B * 3 * H, device=dev)
+        call("ppo_linear_fwd_ex", x.data_ptr(), B, Ip, Ip, self.wih_pad, self.pv(self.GBI), 3 * H, gi.data_ptr(),
+             3 * H, 0, s)
+        return x, gi
+
+    def _vec(self, vec, B):
+        if self.V == 0:
+            return None
+        return vec.to(self.device, torch.float32).reshape(B, self.V).contiguous()
+
+    def act(self, obs, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False,
+            vec=None, hxs=None, masks=None):
+        """Single step (model.py:112-115): returns (value, action, logp, entropy, hxs')."""
+        self.ensure_bound()
+        self.pack()
+        obs = self._check_obs(obs)
+        B = obs.shape[0]
+        ws = self.ws["act"]
+        _, gi = self._input(obs, self._vec(vec, B), None, B, ws)
+        hxs = hxs.to(self.device, torch.float32).reshape(B, self.H).contiguous()
+        m = masks.to(self.device, torch.float32).reshape(B).contiguous() if masks is not None else None
+        hout = torch.empty(B, self.H, device=self.device)
+        call("ppo_gru_step_fwd", hxs.data_ptr(), ptr(m), None, self.pv(self.GHH), self.pv(self.GBH), gi.data_ptr(),
+             B, self.H, hout.data_ptr(), None, None, None, None, None, stream())
+        value, action, logp, ent = self._heads(hout, B, deterministic, noise, given, want_entropy, value_only)
+        return value, action, logp, ent, hout
+
+    def evaluate_sequence(self, obs, vec, hxs, masks, action):
+        """Multi-step branch (model.py:116-165): rows are t*N + n."""
+        self.ensure_bound()
+        self.pack()
+        obs = self._check_obs(obs)
+        R = obs.shape[0]
+        N = hxs.shape[0]
+        T = R // N
+        ws = self.ws["act"]
+        _, gi = self._input(obs, self._vec(vec, R), None, R, ws)
+        hxs = hxs.to(self.device, torch.float32).reshape(N, self.H).contiguous()
+        m = masks.to(self.device, torch.float32).reshape(R).contiguous()
+        hout = torch.empty(R, self.H, device=self.device)
+        H, s = self.H, stream()
+        for t in range(T):
+            hprev = hxs.data_ptr() if t == 0 else hout.data_ptr() + 4 * (t - 1) * N * H
+            call("ppo_gru_step_fwd", hprev, m.data_ptr() + 4 * t * N, None, self.pv(self.GHH), self.pv(self.GBH),
+                 gi.data_ptr() + 4 * t * N * 3 * H, N, H, hout.data_ptr() + 4 * t * N * H, None, None, None, None,
+                 None, s)
+        value, _, logp, ent = self._heads(hout, R, given=action.to(self.device, torch.int64), want_entropy=True)
+        return value, logp, ent, hout[(T - 1) * N:]
+
+    def train_minibatch_rec(self, storage, adv, envs, hp, loss_acc, optimizer):
+        """recurrent_generator minibatch (storage.py:162-223): whole T-sequences of
+        the n envs `envs` (int64 device), BPTT over the full T, then one Adam step."""
+        self.ensure_bound()
+        self.pack()
+        dev, H, s = self.device, self.H, stream()
+        T, N, n = storage.num_steps, storage.rewards.shape[1], envs.numel()
+        R = T * n
+        ws = self.ws["train"]
+        idx = ws.get("ridx", R, torch.int64, dev)[:R]
+        call("ppo_rec_indices", envs.data_ptr(), n, T, N, idx.data_ptr(), s)
+        h0 = ws.get("h0", n * H, device=dev)
+        call("ppo_gather_rows", storage.recurrent_hidden_states.data_ptr(), envs.data_ptr(), h0.data_ptr(), n,
+             4 * H, s)
+        vec = storage.vector_obs if self.V else None
+        x, gi = self._input(storage.obs, vec, idx, R, ws, rows_vec=idx if self.V else None)
+        hout = ws.get("hout", R * H, device=dev)
+        sv = {k: ws.get("s_" + k, R * H, device=dev) for k in ("r", "z", "n", "ghn", "hin")}
+        masks = storage.masks
+        for t in range(T):
+            o = 4 * t * n * H
+            hprev = h0.data_ptr() if t == 0 else hout.data_ptr() + o - 4 * n * H
+            call("ppo_gru_step_fwd", hprev, masks.data_ptr(), idx.data_ptr() + 8 * t * n, self.pv(self.GHH),
+                 self.pv(self.GBH), gi.data_ptr() + 3 * o, n, H, hout.data_ptr() + o, sv["r"].data_ptr() + o,
+                 sv["z"].data_ptr() + o, sv["n"].data_ptr() + o, sv["ghn"].data_ptr() + o, sv["hin"].data_ptr() + o,
+                 s)
+        dout = ws.get("dout", R * H, device=dev)
+        self._heads_train(storage, adv, idx, hout, R, hp, loss_acc, dout, feat_relu=False)
+        # backward through time
+        dgi = ws.get("dgi", R * 3 * H, device=dev)
+        dgh = ws.get("dgh", R * 3 * H, device=dev)
+        dhz = ws.get("dhz", n * H, device=dev)
+        carry = ws.get("carry", n * H, device=dev)
+        for t in range(T - 1, -1, -1):
+            o = 4 * t * n * H
+            call("ppo_gru_cell_bwd", dout.data_ptr() + o, carry.data_ptr(), sv["r"].data_ptr() + o,
+                 sv["z"].data_ptr() + o, sv["n"].data_ptr() + o, sv["ghn"].data_ptr() + o, sv["hin"].data_ptr() + o,
+                 dgi.data_ptr() + 3 * o, dgh.data_ptr() + 3 * o, dhz.data_ptr(), n, H, int(t < T - 1), s)
+            if t > 0:
+                call("ppo_gru_step_bwd", dgh.data_ptr() + 3 * o, self.whhT, dhz.data_ptr(), masks.data_ptr(),
+                     idx.data_ptr() + 8 * t * n, carry.data_ptr(), n, H, s)
+        self._dense_wgrad(dgh, sv["hin"], R, 3 * H, H, 0, 0, self.GHH, self.GBH)
+        self._dense_wgrad(dgi, x, R, 3 * H, self.Ip, 3, self.I, self.GIH, self.GBI)
+        dh = ws.get("dh", R * H, device=dev)
+        call("ppo_linear_dgrad_ex", dgi.data_ptr(), R, 3 * H, self.wihT, H, x.data_ptr(), self.Ip, dh.data_ptr(), s)
+        self._trunk_backward(R, dh, storage.obs, idx)
+        self._finish_step(optimizer)

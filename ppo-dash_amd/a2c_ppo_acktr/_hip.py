@@ -59,7 +59,15 @@ SIGNATURES = {
                       c_p, c_p],
     "ppo_heads_train_blocks": [c_int],
     "ppo_heads_train": [c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_ll, c_p, c_p, c_p, c_p, c_p, c_f, c_f,
-                        c_f, c_f, c_int, c_p, c_p, c_p, c_p, c_p],
+                        c_f, c_f, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
+    "ppo_linear_fwd_ex": [c_p, c_int, c_int, c_int, c_p, c_p, c_int, c_p, c_int, c_int, c_p],
+    "ppo_linear_dgrad_ex": [c_p, c_int, c_int, c_p, c_int, c_p, c_int, c_p, c_p],
+    "ppo_gru_step_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    "ppo_gru_cell_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p],
+    "ppo_gru_step_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p],
+    "ppo_gru_pack": [c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p],
+    "ppo_concat_cols": [c_p, c_p, c_ll, c_int, c_p, c_int, c_int, c_int, c_p],
+    "ppo_rec_indices": [c_p, c_int, c_int, c_int, c_p, c_p],
     "ppo_heads_reduce": [c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_d, c_f, c_int, c_p],
     "ppo_mean_f32": [c_p, c_ll, c_p, c_p],
     # optim.hip

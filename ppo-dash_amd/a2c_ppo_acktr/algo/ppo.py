@@ -103,8 +103,6 @@ class PPO():
 
     def update(self, rollouts):
         eng = self.actor_critic.hip_engine()
-        if self.actor_critic.is_recurrent:
-            raise NotImplementedError("recurrent PPO update is not on the HIP path yet")
         advantages = rollouts.normalized_advantages()            # ppo.py:35-37
         if self._loss_acc is None or self._loss_acc.device != eng.device:
             self._loss_acc = torch.zeros(3, dtype=torch.float64, device=eng.device)
@@ -113,6 +111,9 @@ class PPO():
         hp = {"clip": float(self.clip_param), "value_coef": float(self.value_loss_coef),
               "entropy_coef": float(self.entropy_coef), "use_clipped_value_loss": bool(self.use_clipped_value_loss)}
         num_steps, num_processes = rollouts.rewards.size()[0:2]
+        if self.actor_critic.is_recurrent:
+            self._update_recurrent(eng, rollouts, advantages, hp, num_processes)
+            return self._losses()
         batch_size = num_processes * num_steps
         assert batch_size >= self.num_mini_batch, (
             "PPO requires the number of processes ({}) "
@@ -126,6 +127,27 @@ class PPO():
             for start in range(0, batch_size - mini_batch_size + 1, mini_batch_size):
                 idx = perm[start:start + mini_batch_size]
                 eng.train_minibatch(rollouts, advantages, idx, hp, self._loss_acc, self.optimizer)
+        return self._losses()
+
+    def _update_recurrent(self, eng, rollouts, advantages, hp, num_processes):
+        """recurrent_generator semantics (storage.py:162-223): env order from
+        torch.randperm(N) on the default CPU generator, N//M whole sequences per
+        minibatch, BPTT over the full rollout."""
+        assert num_processes >= self.num_mini_batch, (
+            "PPO requires the number of processes ({}) "
+            "to be greater than or equal to the number of "
+            "PPO mini batches ({}).".format(num_processes, self.num_mini_batch))
+        per = num_processes // self.num_mini_batch
+        for e in range(self.ppo_epoch):
+            perm = torch.randperm(num_processes)
+            for start in range(0, num_processes, per):
+                if start + per > num_processes:
+                    raise IndexError("index {} is out of bounds for dimension 0 with size {}".format(
+                        num_processes, num_processes))
+                envs = perm[start:start + per].to(eng.device, non_blocking=True)
+                eng.train_minibatch_rec(rollouts, advantages, envs, hp, self._loss_acc, self.optimizer)
+
+    def _losses(self):
         _dist.allreduce_losses(self._loss_acc)
         num_updates = self.ppo_epoch * self.num_mini_batch        # ppo.py:90 (not the drop_last count)
         losses = (self._loss_acc / num_updates).tolist()           # one D2H per update

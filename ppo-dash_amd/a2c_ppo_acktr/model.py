@@ -13,7 +13,7 @@ Differences from the reference, all documented in DESIGN.md:
     Policy can build it (the reference mis-calls it, model.py:28 vs :203).
   * evaluate_actions returns values without an autograd graph; PPO.update runs
     its own fused HIP backward.
-  * Recurrent (GRU) and MLP forward passes are not on the HIP path yet.
+  * MLPBase's forward pass is not on the HIP path yet.
 """
 import numpy as np
 import torch
@@ -88,19 +88,19 @@ class Policy(nn.Module):
 
     def hip_engine(self, device=None):
         require_device()
-        if not isinstance(self.base, CNNBase) or self.base.is_recurrent:
-            raise NotImplementedError("the MI355X engine currently runs the feed-forward CNNBase policy; "
-                                      "recurrent (GRU) and MLPBase policies are on the roadmap (DESIGN.md)")
+        if not isinstance(self.base, CNNBase):
+            raise NotImplementedError("the MI355X engine runs CNNBase policies (feed-forward or GRU); "
+                                      "MLPBase is on the roadmap (DESIGN.md)")
         if not isinstance(self.dist, Categorical):
             raise NotImplementedError("only Discrete action spaces run on the MI355X engine")
         if device is None:
             p = next(self.parameters())
             device = p.device if p.is_cuda else torch.device("cuda", torch.cuda.current_device())
         if self._engine is None or self._engine.device != device:
-            from ._engine import CNNEngine
+            from ._engine import CNNEngine, RecurrentEngine
             if not next(self.parameters()).is_cuda:
                 self.to(device)
-            self._engine = CNNEngine(self, device)
+            self._engine = (RecurrentEngine if self.base.is_recurrent else CNNEngine)(self, device)
         self._engine.ensure_bound()
         return self._engine
 
@@ -115,18 +115,33 @@ class Policy(nn.Module):
         eng = self.hip_engine()
         n = visual_inputs.shape[0]
         noise = None if deterministic else self._noise(n)
+        if self.is_recurrent:
+            value, action, logp, _, rnn_hxs = eng.act(visual_inputs, deterministic=deterministic, noise=noise,
+                                                      vec=vector_inputs, hxs=rnn_hxs, masks=masks)
+            return value, action, logp, rnn_hxs
         value, action, logp, _ = eng.act(visual_inputs, deterministic=deterministic, noise=noise)
         return value, action, logp, rnn_hxs
 
     def get_value(self, visual_inputs, vector_inputs, rnn_hxs, masks):
         """model.py:68-70."""
-        value, _, _, _ = self.hip_engine().act(visual_inputs, value_only=True)
+        eng = self.hip_engine()
+        if self.is_recurrent:
+            return eng.act(visual_inputs, value_only=True, vec=vector_inputs, hxs=rnn_hxs, masks=masks)[0]
+        value, _, _, _ = eng.act(visual_inputs, value_only=True)
         return value
 
     def evaluate_actions(self, visual_inputs, vector_inputs, rnn_hxs, masks, action):
         """model.py:72-79 -> (value [B,1], action_log_probs [B,1], dist_entropy (0-d), rnn_hxs)."""
         eng = self.hip_engine()
         action = action.to(eng.device, torch.int64)
+        if self.is_recurrent:
+            if visual_inputs.shape[0] == rnn_hxs.shape[0]:   # model.py:112 single-step branch
+                value, _, logp, ent, rnn_hxs = eng.act(visual_inputs, given=action, want_entropy=True,
+                                                       vec=vector_inputs, hxs=rnn_hxs, masks=masks)
+            else:                                             # model.py:116-165 sequence branch
+                value, logp, ent, rnn_hxs = eng.evaluate_sequence(visual_inputs, vector_inputs, rnn_hxs, masks,
+                                                                  action)
+            return value, logp, ent.mean(), rnn_hxs
         value, _, logp, ent = eng.act(visual_inputs, given=action, want_entropy=True)
         return value, logp, ent.mean(), rnn_hxs
 

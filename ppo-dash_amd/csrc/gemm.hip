@@ -22,221 +22,9 @@
 // one ds_read_b128 of 4 k values per lane) or row-contiguous ([BK][rows], read
 // as 4 ds_read_b32); the 4 k values of a lane feed 4 successive MFMAs, so the
 // physical k order inside a BK=16 step is a fixed permutation common to A and B.
-#include <string.h>
-
-#include "common.h"
+#include "igemm.h"
 
 namespace {
-
-constexpr int BK16 = 16;  // default k-tile depth (wgrad chunks are multiples of it)
-
-// k-contiguous tiles: rows of BK floats (CPR = BK/4 16-B chunks), chunk q of
-// row r stored at chunk q ^ f(r), f(r) = (r / (16/CPR)) mod CPR.  A wave's
-// fragment read (32 rows, one chunk each) then hits 16 distinct 16-B slots in
-// every ds_read_b128 lane group, and the staging ds_write_b128 of whole rows is
-// contiguous — both conflict-free (PMC: SQ_LDS_BANK_CONFLICT, the +4 padding
-// this replaces cost 37 % of LDS cycles in the staging writes).
-template <int ROWS, bool KC, int BK>
-struct Tile {
-  static constexpr int LD = BK;
-  static constexpr int SIZE = KC ? ROWS * LD : BK * ROWS;
-  static constexpr int NV4 = ROWS * BK / 4;
-};
-
-template <int BK>
-__device__ __forceinline__ int kc_off(int row, int k) {  // k multiple of 4
-  constexpr int CPR = BK / 4;
-  const int q = (k >> 2) ^ ((row / (16 / CPR)) & (CPR - 1));
-  return row * BK + 4 * q;
-}
-
-template <int ROWS, bool KC, int BK>
-__device__ __forceinline__ f32x4 frag(const float* S, int row, int kb) {
-  if constexpr (KC) {
-    return *reinterpret_cast<const f32x4*>(S + kc_off<BK>(row, kb));
-  } else {
-    f32x4 r;
-    r[0] = S[(kb + 0) * ROWS + row];
-    r[1] = S[(kb + 1) * ROWS + row];
-    r[2] = S[(kb + 2) * ROWS + row];
-    r[3] = S[(kb + 3) * ROWS + row];
-    return r;
-  }
-}
-
-// Bijective XCD-aware remap (guide §5.5 T1): blocks that share an XCD
-// (b ≡ b' mod 8) get consecutive tiles, so neighbouring im2col windows and
-// weight tiles are served from that XCD's L2.
-__device__ __forceinline__ int xcd_remap(int bid, int nb) {
-  const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
-  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  return base + (bid >> 3);
-}
-
-__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
-
-// ---------------------------------------------------------------------------
-// Core: C[m][n] = Σ_k A[m][k] B[n][k]; problem P supplies loaders + epilogue.
-// ---------------------------------------------------------------------------
-template <class P>
-__global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
-  constexpr int BM = P::BM, BN = P::BN, NT = P::NT, WM = P::WM, WN = P::WN, BK = P::BK;
-  constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN);
-  static_assert(TM * 32 * WM == BM && TN * 32 * WN == BN && WM * WN * 64 == NT, "tile config");
-  static_assert(BK == 16 || BK == 32, "k-tile");
-  using TA = Tile<BM, P::A_KC, BK>;
-  using TB = Tile<BN, P::B_KC, BK>;
-  constexpr int NVA = (TA::NV4 + NT - 1) / NT, NVB = (TB::NV4 + NT - 1) / NT;
-  constexpr int STAGE = TA::SIZE + TB::SIZE;
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
-  const int n0 = blockIdx.y * BN;
-  const int z = blockIdx.z;
-  int kbeg, kend;
-  p.k_range(z, kbeg, kend);
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-
-  typename P::ACtx actx[NVA];
-  typename P::BCtx bctx[NVB];
-  int ak[NVA], aoff[NVA], bk[NVB], boff[NVB];
-  bool aon[NVA], bon[NVB];
-#pragma unroll
-  for (int i = 0; i < NVA; ++i) {
-    const int f = tid + i * NT;
-    aon[i] = f < TA::NV4;
-    if constexpr (P::A_KC) {
-      const int row = f / (BK / 4), kq = f % (BK / 4);
-      actx[i] = p.a_ctx(m0 + row, z);
-      ak[i] = 4 * kq;
-      aoff[i] = kc_off<BK>(row, 4 * kq);
-    } else {
-      const int k = f / (BM / 4), rq = f % (BM / 4);
-      actx[i] = p.a_ctx(m0 + 4 * rq, z);
-      ak[i] = k;
-      aoff[i] = k * BM + 4 * rq;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NVB; ++i) {
-    const int f = tid + i * NT;
-    bon[i] = f < TB::NV4;
-    if constexpr (P::B_KC) {
-      const int row = f / (BK / 4), kq = f % (BK / 4);
-      bctx[i] = p.b_ctx(n0 + row, z);
-      bk[i] = 4 * kq;
-      boff[i] = kc_off<BK>(row, 4 * kq);
-    } else {
-      const int k = f / (BN / 4), rq = f % (BN / 4);
-      bctx[i] = p.b_ctx(n0 + 4 * rq, z);
-      bk[i] = k;
-      boff[i] = k * BN + 4 * rq;
-    }
-  }
-
-  f32x4 ra[NVA], rb[NVB];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < NVA; ++i) ra[i] = aon[i] ? p.a_load(actx[i], k0 + ak[i]) : zero4();
-#pragma unroll
-    for (int i = 0; i < NVB; ++i) rb[i] = bon[i] ? p.b_load(bctx[i], k0 + bk[i]) : zero4();
-  };
-  auto sstore = [&](int buf) {
-    float* As = smem + buf * STAGE;
-    float* Bs = As + TA::SIZE;
-#pragma unroll
-    for (int i = 0; i < NVA; ++i)
-      if (aon[i]) *reinterpret_cast<f32x4*>(As + aoff[i]) = ra[i];
-#pragma unroll
-    for (int i = 0; i < NVB; ++i)
-      if (bon[i]) *reinterpret_cast<f32x4*>(Bs + boff[i]) = rb[i];
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  float bias_acc = 0.f;
-
-  if (nk > 0) {
-    gload(kbeg);
-    sstore(0);
-  }
-  __syncthreads();
-  const int frow = lane & 31, fk = 4 * (lane >> 5);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload(kbeg + (kt + 1) * BK);
-    const float* As = smem + buf * STAGE;
-    const float* Bs = As + TA::SIZE;
-    if constexpr (P::BIAS_FROM_A) {
-      static_assert(!P::A_KC, "bias partials read the row-contiguous A tile");
-      if (blockIdx.y == 0 && tid < BM) {
-#pragma unroll
-        for (int k = 0; k < BK; ++k) bias_acc += As[k * BM + tid];
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 8) {
-      f32x4 af[TM], bf[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag<BM, P::A_KC, BK>(As, (wm * TM + i) * 32 + frow, kk + fk);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = frag<BN, P::B_KC, BK>(Bs, (wn * TN + j) * 32 + frow, kk + fk);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) sstore(buf ^ 1);
-    __syncthreads();
-  }
-
-  const int hi = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-        const int col = (wn * TN + j) * 32 + frow;
-        p.store(m0 + row, n0 + col, z, acc[i][j][r]);
-      }
-  if constexpr (P::BIAS_FROM_A) {
-    if (blockIdx.y == 0 && tid < BM) p.store_bias(m0 + tid, z, bias_acc);
-  }
-}
-
-template <int BM_, int BN_, int WM_, int WN_, bool AKC, bool BKC, bool BIASA = false, int BK_ = BK16>
-struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NT = 64 * WM_ * WN_, BK = BK_;
-  static constexpr bool A_KC = AKC, B_KC = BKC, BIAS_FROM_A = BIASA;
-  struct ACtx { const float* p; int a; int b; bool ok; };
-  struct BCtx { const float* p; int a; bool ok; };
-};
-
-// u8 operand as exact integers 0..255; the 1/255 of the decode is folded into
-// the epilogue (forward) or the slab reduce (wgrad): Σ w·u/255 instead of
-// Σ w·fl(u/255), a ≤ 1-ulp-per-term difference (within the fp32 tolerance of
-// the GEMM's own summation order) for 16 fewer VALU ops per 4 bytes.
-__device__ __forceinline__ f32x4 u8x4(uint32_t u) {
-  return f32x4{(float)(u & 255u), (float)((u >> 8) & 255u), (float)((u >> 16) & 255u), (float)(u >> 24)};
-}
-
-// obs row of minibatch sample b: storage row idx[b] (gather) or row0 + b
-__device__ __forceinline__ long long obs_row(const int64_t* idx, long long row0, int b) {
-  return idx ? (long long)idx[b] : row0 + b;
-}
-
 // ---------------------------------------------------------------------------
 // Forward problems
 // ---------------------------------------------------------------------------
@@ -299,53 +87,10 @@ struct ConvFwd : C_ {
   }
 };
 
-// Linear + ReLU: out[m][n] = relu(Σ_k x[m][k] w[n][k] + bias[n])
-template <class C_>
-struct DenseReluFwd : C_ {
-  const float* x; const float* w; const float* bias; float* out; int M, N, K;
-  using ACtx = typename C_::ACtx;
-  using BCtx = typename C_::BCtx;
-  __device__ ACtx a_ctx(int m, int) const { return {x + (size_t)m * K, 0, 0, m < M}; }
-  __device__ f32x4 a_load(const ACtx& c, int k) const {
-    return (c.ok && k < K) ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
-  }
-  __device__ BCtx b_ctx(int n, int) const { return {w + (size_t)n * K, 0, n < N}; }
-  __device__ f32x4 b_load(const BCtx& c, int k) const {
-    return (c.ok && k < K) ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
-  }
-  __device__ void k_range(int, int& b, int& e) const { b = 0; e = K; }
-  __device__ void store(int m, int n, int, float v) const {
-    if (m < M && n < N) out[(size_t)m * N + n] = fmaxf(v + bias[n], 0.f);
-  }
-};
-
 // ---------------------------------------------------------------------------
 // Input-gradient (dgrad) problems; epilogue applies the ReLU mask of the
 // layer below (threshold_backward: pass where the saved output is > 0).
 // ---------------------------------------------------------------------------
-// dx[m][n] = (act[m][n] > 0) * Σ_k dy[m][k] wt[n][k]
-template <class C_>
-struct DenseDgradMask : C_ {
-  const float* dy; const float* wt; const float* act; float* dx; int M, N, K;
-  using ACtx = typename C_::ACtx;
-  using BCtx = typename C_::BCtx;
-  __device__ ACtx a_ctx(int m, int) const { return {dy + (size_t)m * K, 0, 0, m < M}; }
-  __device__ f32x4 a_load(const ACtx& c, int k) const {
-    return (c.ok && k < K) ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
-  }
-  __device__ BCtx b_ctx(int n, int) const { return {wt + (size_t)n * K, 0, n < N}; }
-  __device__ f32x4 b_load(const BCtx& c, int k) const {
-    return (c.ok && k < K) ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
-  }
-  __device__ void k_range(int, int& b, int& e) const { b = 0; e = K; }
-  __device__ void store(int m, int n, int, float v) const {
-    if (m < M && n < N) {
-      const size_t i = (size_t)m * N + n;
-      dx[i] = act[i] > 0.f ? v : 0.f;
-    }
-  }
-};
-
 // stride-1 conv dgrad (conv3): m = (b, y, x) input pixel, n = ci,
 // k = (ky, kx, co): dy[b][y-ky][x-kx][co] (0 outside), wd packed [CIN][K]
 template <int HIN, int CIN, int KS, int HOUT, int COUT, class C_>
@@ -421,29 +166,6 @@ struct Conv2Dgrad : C_ {
 // row-contiguous tiles; blocks of tile column 0 also sum the dz tile into the
 // bias partial (db[co] = Σ_r dz[r][co]).
 // ---------------------------------------------------------------------------
-template <class C_>
-struct WgradBase : C_ {
-  const float* dz; int COUT; long long R; int chunk;  // chunk: multiple of 16 (and of BK)
-  float* slab; float* slab_bias; int NW;             // slab [Z][COUT][NW]
-  using ACtx = typename C_::ACtx;
-  __device__ ACtx a_ctx(int co, int) const { return {dz + co, 0, 0, co < COUT}; }
-  __device__ f32x4 a_load(const ACtx& c, int r) const {
-    return (c.ok && r < R) ? *reinterpret_cast<const f32x4*>(c.p + (size_t)r * COUT) : zero4();
-  }
-  __device__ void k_range(int z, int& b, int& e) const {
-    const long long bb = (long long)z * chunk;
-    b = (int)(bb < R ? bb : R);
-    const long long ee = bb + chunk;
-    e = (int)(ee < R ? ee : R);
-  }
-  __device__ void store(int m, int n, int z, float v) const {
-    if (m < COUT && n < NW) slab[((size_t)z * COUT + m) * NW + n] = v;
-  }
-  __device__ void store_bias(int m, int z, float v) const {
-    if (m < COUT) slab_bias[(size_t)z * COUT + m] = v;
-  }
-};
-
 // conv1 wgrad: X(r, kk) = decoded obs[idx[b]][c][4oy+ky][4ox+kx], kk = (c,ky,kx)
 template <typename InT, class C_>
 struct Conv1Wgrad : WgradBase<C_> {
@@ -478,68 +200,6 @@ struct ConvWgrad : WgradBase<C_> {
     return *reinterpret_cast<const f32x4*>(in + ((size_t)(b * HIN + ST * oy) * HIN + ST * ox) * CIN + c.off);
   }
 };
-
-// Linear wgrad: X(r, kk) = x[r][kk]
-template <class C_>
-struct DenseWgrad : WgradBase<C_> {
-  const float* x; int K;
-  struct BCtx { const float* p; bool ok; };
-  __device__ BCtx b_ctx(int n, int) const { return {x + n, n < K}; }
-  __device__ f32x4 b_load(const BCtx& c, int r) const {
-    return (c.ok && r < this->R) ? *reinterpret_cast<const f32x4*>(c.p + (size_t)r * K) : zero4();
-  }
-};
-
-// Deterministic column sums: out[c] = scale * Σ_z src[z*ld + c], c < cols.
-// A block covers 32 consecutive columns with 8 z-groups (each summing
-// z ≡ g mod 8 in a fixed order, 4 loads in flight), then combines the groups
-// in a fixed order — bitwise reproducible, and ≥ cols/32 blocks of parallelism.
-//   map kind 0: w[c]                                  (conv1 (c,ky,kx), biases)
-//   map kind 1: c=(m, n=(ky,kx,ci)) -> w[m][ci][ky][kx]  (conv2/conv3; a=KS, b=CIN, nw)
-//   map kind 2: c=(m, n=(p,ch))     -> w[m][ch*P + p]    (fc; a=C, b=P, nw)
-struct ColMap {
-  int kind, a, b, nw;
-  __device__ __forceinline__ size_t operator()(long long c) const {
-    if (kind == 0) return (size_t)c;
-    const int m = (int)(c / nw), n = (int)(c - (long long)m * nw);
-    if (kind == 1) {
-      const int ky = n / (a * b), rem = n - ky * (a * b), kx = rem / b, ci = rem - kx * b;
-      return (size_t)m * nw + (size_t)ci * a * a + ky * a + kx;
-    }
-    const int pp = n / a, ch = n - pp * a;
-    return (size_t)m * nw + (size_t)ch * b + pp;
-  }
-};
-
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ src, long long ld, int Z,
-                                                     long long cols, ColMap map, float* __restrict__ out, float scale,
-                                                     int accumulate) {
-  const int cl = threadIdx.x & 31, zg = threadIdx.x >> 5;
-  const long long c = (long long)blockIdx.x * 32 + cl;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (c < cols) {
-    const float* p = src + c;
-    int z = zg;
-    for (; z + 24 < Z; z += 32) {
-      s0 += p[(size_t)z * ld];
-      s1 += p[(size_t)(z + 8) * ld];
-      s2 += p[(size_t)(z + 16) * ld];
-      s3 += p[(size_t)(z + 24) * ld];
-    }
-    for (; z < Z; z += 8) s0 += p[(size_t)z * ld];
-  }
-  __shared__ float red[8][33];
-  red[zg][cl] = (s0 + s1) + (s2 + s3);
-  __syncthreads();
-  if (zg == 0 && c < cols) {
-    float t = red[0][cl];
-#pragma unroll
-    for (int g = 1; g < 8; ++g) t += red[g][cl];
-    t *= scale;
-    const size_t o = map(c);
-    out[o] = accumulate ? out[o] + t : t;
-  }
-}
 
 // Pack torch-layout weights into the loaders' k orders (once per optimizer step).
 //   W2p [64][512]  (ky,kx,ci)       W3p [32][576] (ky,kx,ci)
@@ -578,24 +238,6 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
     }
     out[i] = v;
   }
-}
-
-// flops: algorithmic FLOPs of this launch (2·M·N·K of the GEMM it computes)
-template <class P>
-int launch(const P& p, long long M, int N, int Z, hipStream_t st, const char* name, double flops) {
-  if (M <= 0 || N <= 0 || Z <= 0) return 0;
-  const long long gx = (M + P::BM - 1) / P::BM;
-  if (gx > 0x7fffffffLL) {
-    ppo_set_error("%s: grid too large (M=%lld)", name, M);
-    return PPO_ESHAPE;
-  }
-  dim3 grid((unsigned)gx, (unsigned)((N + P::BN - 1) / P::BN), (unsigned)Z);
-  int slot;
-  const bool prof = ppo_prof_begin(name, st, &slot);
-  igemm_kernel<P><<<grid, P::NT, 0, st>>>(p);
-  if (prof) ppo_prof_end(slot, st, flops);
-  PPO_LAUNCH_CHECK(name);
-  return 0;
 }
 
 using CfgN32 = Cfg<256, 32, 4, 1, true, true>;
@@ -725,6 +367,29 @@ PPO_API int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, co
   return launch(p, M, N, 1, as_stream(stream), "linear_relu_fwd", 2.0 * M * N * K);
 }
 
+// Linear with row strides: out[m*ldo + n] = act(x[m*lda + k] · w[n][k] + b[n]); b may be NULL
+PPO_API int ppo_linear_fwd_ex(const float* x, int M, int K, int lda, const float* w, const float* b, int N, float* out,
+                              int ldo, int relu, void* stream) {
+  PPO_REQUIRE(K % 4 == 0 && lda % 4 == 0, "ppo_linear_fwd_ex: K=%d lda=%d must be multiples of 4", K, lda);
+  if (N % 128 == 0) {
+    DenseReluFwd<CfgN128> p;
+    p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = relu;
+    return launch(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);
+  }
+  DenseReluFwd<CfgN64> p;
+  p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = relu;
+  return launch(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);
+}
+
+// dx [M][N] = (act > 0) * (dy [M][K] · wt [N][K]^T); act row stride ldact (act NULL: no mask)
+PPO_API int ppo_linear_dgrad_ex(const float* dy, int M, int K, const float* wt, int N, const float* act, int ldact,
+                                float* dx, void* stream) {
+  PPO_REQUIRE(K % 4 == 0, "ppo_linear_dgrad_ex: K=%d must be a multiple of 4", K);
+  DenseDgradMask<CfgN128> p;
+  p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K; p.ldact = ldact;
+  return launch(p, M, N, 1, as_stream(stream), "linear_dgrad_ex", 2.0 * M * N * K);
+}
+
 // dx [M][N] = (act > 0) * (dy [M][K] · wt [N][K]^T)
 PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
                                   void* stream) {
@@ -827,18 +492,10 @@ PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int 
   return launch(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K);
 }
 
-static int colsum(const float* src, long long ld, int Z, long long cols, ColMap map, float* out, float scale,
-                  int accumulate, hipStream_t st) {
-  if (cols <= 0) return 0;
-  colsum_kernel<<<ceil_div(cols, 32), 256, 0, st>>>(src, ld, Z, cols, map, out, scale, accumulate);
-  PPO_LAUNCH_CHECK("colsum_kernel");
-  return 0;
-}
-
 // Σ over the Z split partials (fixed order) -> gw (torch order, see ColMap) and gb
 PPO_API int ppo_wgrad_reduce(const float* slab, const float* slab_bias, int Z, int M, int NW, int kind, int a, int b,
                              float* gw, float* gb, float scale, int accumulate, void* stream) {
-  PPO_REQUIRE(kind >= 0 && kind <= 2, "ppo_wgrad_reduce: kind=%d", kind);
+  PPO_REQUIRE(kind >= 0 && kind <= 3, "ppo_wgrad_reduce: kind=%d", kind);
   hipStream_t st = as_stream(stream);
   const long long cols = (long long)M * NW;
   int rc = colsum(slab, cols, Z, cols, ColMap{kind, a, b, NW}, gw, scale, accumulate, st);

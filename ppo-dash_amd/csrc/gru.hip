@@ -1,0 +1,250 @@
+// Recurrent policy core (K12): the GRU of NNBase, forward and backward
+// through time, on the fp32 MFMA implicit-GEMM core.
+//
+// Reference: NNBase.__init__ / _forward_gru, ppo-dash-training/
+// pytorch-a2c-ppo-acktr-gail/a2c_ppo_acktr/model.py:89-95, 111-166 (torch.nn.GRU,
+// gates (r, z, n): r = σ(W_ir x + b_ir + W_hr h + b_hr), z likewise,
+// n = tanh(W_in x + b_in + r ⊙ (W_hn h + b_hn)), h' = (1 - z) ⊙ n + z ⊙ h).
+// The reference splits the sequence at steps where any env's mask is 0 and
+// feeds h·m[start] to each segment; that is exactly h_in(t) = h(t-1)·m(t) at
+// every step (the extra ×1 are exact), which is what runs here.
+//
+// Work split:
+//   gi = x · W_ihᵀ + b_ih         one big GEMM over all T·n_env rows (gemm.hip)
+//   per step t: gh = h_in · W_hhᵀ and the gate cell fused in the epilogue
+//     (tile epilogue: a wave's three 32-column tiles are the r, z, n columns of
+//     the same 32 hidden units, so each lane holds all three pre-activations)
+//   backward per step (reverse): gate gradients (elementwise) then
+//     dh_in = dgh · W_hh with the carry (dh_in + dh'·z)·m(t) in the epilogue
+//   after the loop: dW_hh, dW_ih as split-K wgrads over all T·n_env rows,
+//     dx = dgi · W_ih[:, :H] masked by the fc ReLU.
+// Saved per step for the backward: r, z, n, W_hn h + b_hn, h_in ([T][n][H] each).
+#include "igemm.h"
+
+namespace {
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// gh tile with the fused GRU cell.  B rows n = jt*96 + g*32 + jj <-> W_hh row g*H + jt*32 + jj.
+template <class C_>
+struct GruStep : C_ {
+  static constexpr bool TILE_EPI = true;
+  const float* hprev;            // [M][H] h(t-1)
+  const float* masks;            // mask plane (NULL: 1)
+  const int64_t* mask_idx;       // masks[mask_idx[m]] (NULL: masks[m])
+  const float* whh; const float* bhh;
+  const float* gi;               // [M][3H] x·W_ihᵀ + b_ih of this step
+  float* hout;                   // [M][H]
+  float *sr, *sz, *sn, *sghn, *shin;  // saved for backward (NULL: inference)
+  int M, H;
+  struct ACtx { const float* p; float m; bool ok; };
+  using BCtx = typename C_::BCtx;
+  __device__ float mask_of(int m) const {
+    if (!masks) return 1.0f;
+    return masks[mask_idx ? mask_idx[m] : m];
+  }
+  __device__ ACtx a_ctx(int m, int) const {
+    if (m >= M) return {hprev, 0.f, false};
+    return {hprev + (size_t)m * H, mask_of(m), true};
+  }
+  __device__ f32x4 a_load(const ACtx& c, int k) const {
+    if (!c.ok) return zero4();
+    return *reinterpret_cast<const f32x4*>(c.p + k) * c.m;
+  }
+  __device__ BCtx b_ctx(int n, int) const {
+    const int jt = n / 96, rem = n - jt * 96, g = rem >> 5, jj = rem & 31;
+    const int j = jt * 32 + jj;
+    return {whh + ((size_t)g * H + j) * H, 0, j < H};
+  }
+  __device__ f32x4 b_load(const BCtx& c, int k) const {
+    return c.ok ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
+  }
+  __device__ void k_range(int, int& b, int& e) const { b = 0; e = H; }
+  __device__ void store(int, int, int, float) const {}
+  __device__ void store_tile(int m, int j, int, const float (&v)[3]) const {
+    if (m >= M || j >= H) return;
+    const float* g = gi + (size_t)m * 3 * H;
+    const float ghr = v[0] + bhh[j], ghz = v[1] + bhh[H + j], ghn = v[2] + bhh[2 * H + j];
+    const float r = sigm(g[j] + ghr);
+    const float z = sigm(g[H + j] + ghz);
+    const float n = tanhf(g[2 * H + j] + r * ghn);
+    const float hin = hprev[(size_t)m * H + j] * mask_of(m);
+    const size_t o = (size_t)m * H + j;
+    hout[o] = (1.0f - z) * n + z * hin;
+    if (sr) {
+      sr[o] = r;
+      sz[o] = z;
+      sn[o] = n;
+      sghn[o] = ghn;
+      shin[o] = hin;
+    }
+  }
+};
+
+// dh_in = dgh · W_hh (B = W_hhᵀ packed [H][3H]); carry = (dh_in + dh'·z) · m(t)
+template <class C_>
+struct GruBwdStep : C_ {
+  const float* dgh; const float* whhT; const float* dhz;
+  const float* masks; const int64_t* mask_idx;
+  float* carry; int M, H;
+  using ACtx = typename C_::ACtx;
+  using BCtx = typename C_::BCtx;
+  __device__ ACtx a_ctx(int m, int) const { return {dgh + (size_t)m * 3 * H, 0, 0, m < M}; }
+  __device__ f32x4 a_load(const ACtx& c, int k) const {
+    return c.ok ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
+  }
+  __device__ BCtx b_ctx(int n, int) const { return {whhT + (size_t)n * 3 * H, 0, n < H}; }
+  __device__ f32x4 b_load(const BCtx& c, int k) const {
+    return c.ok ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
+  }
+  __device__ void k_range(int, int& b, int& e) const { b = 0; e = 3 * H; }
+  __device__ void store(int m, int n, int, float v) const {
+    if (m >= M || n >= H) return;
+    const float mk = masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
+    const size_t o = (size_t)m * H + n;
+    carry[o] = (v + dhz[o]) * mk;
+  }
+};
+
+// gate gradients of one step: dh' = dout + carry;
+//   dn = dh'(1-z), dz = dh'(h_in - n), da_n = dn(1-n²), dr = da_n·ghn,
+//   da_r = dr·r(1-r), da_z = dz·z(1-z);  dgi = [da_r, da_z, da_n],
+//   dgh = [da_r, da_z, da_n·r];  dhz = dh'·z
+__global__ __launch_bounds__(256) void gru_cell_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ carry,
+                                                           const float* __restrict__ r, const float* __restrict__ z,
+                                                           const float* __restrict__ n, const float* __restrict__ ghn,
+                                                           const float* __restrict__ hin, float* __restrict__ dgi,
+                                                           float* __restrict__ dgh, float* __restrict__ dhz, int M,
+                                                           int H, int has_carry) {
+  const long long total = (long long)M * H;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int m = (int)(i / H), j = (int)(i - (long long)m * H);
+    const float dh = dout[i] + (has_carry ? carry[i] : 0.f);
+    const float zz = z[i], nn = n[i], rr = r[i];
+    const float dn = dh * (1.0f - zz);
+    const float dz = dh * (hin[i] - nn);
+    const float dan = dn * (1.0f - nn * nn);
+    const float dr = dan * ghn[i];
+    const float dar = dr * rr * (1.0f - rr);
+    const float daz = dz * zz * (1.0f - zz);
+    const size_t g = (size_t)m * 3 * H + j;
+    dgi[g] = dar;
+    dgi[g + H] = daz;
+    dgi[g + 2 * H] = dan;
+    dgh[g] = dar;
+    dgh[g + H] = daz;
+    dgh[g + 2 * H] = dan * rr;
+    dhz[i] = dh * zz;
+  }
+}
+
+// W_ih [3H][I] -> W_ih padded [3H][Ip] (zeros), W_ihᵀ[:H] [H][3H], W_hhᵀ [H][3H]
+__global__ __launch_bounds__(256) void gru_pack_kernel(const float* __restrict__ wih, const float* __restrict__ whh,
+                                                       int H, int I, int Ip, float* __restrict__ wih_pad,
+                                                       float* __restrict__ wihT, float* __restrict__ whhT) {
+  const long long n0 = 3LL * H * Ip, n1 = (long long)H * 3 * H, n2 = n1;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n0 + n1 + n2; i += (long long)gridDim.x * 256) {
+    long long q = i;
+    if (q < n0) {
+      const int g = (int)(q / Ip), k = (int)(q % Ip);
+      wih_pad[q] = k < I ? wih[(size_t)g * I + k] : 0.f;
+    } else if ((q -= n0) < n1) {
+      const int j = (int)(q / (3 * H)), g = (int)(q % (3 * H));
+      wihT[q] = wih[(size_t)g * I + j];
+    } else {
+      q -= n1;
+      const int j = (int)(q / (3 * H)), g = (int)(q % (3 * H));
+      whhT[q] = whh[(size_t)g * H + j];
+    }
+  }
+}
+
+// dst[r*ld + col0 + c] = src[row(r)*ncols + c] (c < ncols), zeros for ncols <= c < zero_to
+__global__ __launch_bounds__(256) void concat_cols_kernel(const float* __restrict__ src, const int64_t* __restrict__ idx,
+                                                          long long rows, int ncols, float* __restrict__ dst, int ld,
+                                                          int col0, int zero_to) {
+  const long long total = rows * zero_to;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long r = i / zero_to;
+    const int c = (int)(i - r * zero_to);
+    const long long sr = idx ? idx[r] : r;
+    dst[r * ld + col0 + c] = c < ncols ? src[sr * ncols + c] : 0.f;
+  }
+}
+
+// idx[t*n + j] = t*N + envs[j]  (recurrent_generator sample order, storage.py:195-220)
+__global__ __launch_bounds__(256) void rec_indices_kernel(const int64_t* __restrict__ envs, int n, int T, int N,
+                                                          int64_t* __restrict__ idx) {
+  const long long total = (long long)T * n;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int t = (int)(i / n), j = (int)(i - (long long)t * n);
+    idx[i] = (int64_t)t * N + envs[j];
+  }
+}
+
+using CfgGru = Cfg<32, 96, 1, 1, true, true>;     // one wave: 32 rows x (r,z,n) x 32 units
+using CfgGruB = Cfg<64, 64, 2, 2, true, true>;
+
+static unsigned grid_for(long long total) {
+  long long b = (total + 255) / 256;
+  return (unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+}  // namespace
+
+// one GRU step, fused cell (model.py:112-115 single step, or one step of :116-165)
+PPO_API int ppo_gru_step_fwd(const float* hprev, const float* masks, const int64_t* mask_idx, const float* whh,
+                             const float* bhh, const float* gi, int M, int H, float* hout, float* save_r, float* save_z,
+                             float* save_n, float* save_ghn, float* save_hin, void* stream) {
+  PPO_REQUIRE(M >= 0 && H > 0 && H % 32 == 0, "ppo_gru_step_fwd: M=%d H=%d (H multiple of 32)", M, H);
+  GruStep<CfgGru> p;
+  p.hprev = hprev; p.masks = masks; p.mask_idx = mask_idx; p.whh = whh; p.bhh = bhh; p.gi = gi; p.hout = hout;
+  p.sr = save_r; p.sz = save_z; p.sn = save_n; p.sghn = save_ghn; p.shin = save_hin; p.M = M; p.H = H;
+  return launch(p, M, 3 * H, 1, as_stream(stream), "gru_step_fwd", 2.0 * M * 3 * H * H);
+}
+
+PPO_API int ppo_gru_cell_bwd(const float* dout, const float* carry, const float* r, const float* z, const float* n,
+                             const float* ghn, const float* hin, float* dgi, float* dgh, float* dhz, int M, int H,
+                             int has_carry, void* stream) {
+  PPO_REQUIRE(M >= 0 && H > 0, "ppo_gru_cell_bwd: M=%d H=%d", M, H);
+  if (M == 0) return 0;
+  gru_cell_bwd_kernel<<<grid_for((long long)M * H), 256, 0, as_stream(stream)>>>(dout, carry, r, z, n, ghn, hin, dgi,
+                                                                                 dgh, dhz, M, H, has_carry);
+  PPO_LAUNCH_CHECK("gru_cell_bwd_kernel");
+  return 0;
+}
+
+PPO_API int ppo_gru_step_bwd(const float* dgh, const float* whhT, const float* dhz, const float* masks,
+                             const int64_t* mask_idx, float* carry, int M, int H, void* stream) {
+  PPO_REQUIRE(M >= 0 && H > 0 && H % 4 == 0, "ppo_gru_step_bwd: M=%d H=%d", M, H);
+  GruBwdStep<CfgGruB> p;
+  p.dgh = dgh; p.whhT = whhT; p.dhz = dhz; p.masks = masks; p.mask_idx = mask_idx; p.carry = carry; p.M = M; p.H = H;
+  return launch(p, M, H, 1, as_stream(stream), "gru_step_bwd", 2.0 * M * 3 * H * H);
+}
+
+PPO_API int ppo_gru_pack(const float* wih, const float* whh, int H, int I, int Ip, float* wih_pad, float* wihT,
+                         float* whhT, void* stream) {
+  PPO_REQUIRE(H > 0 && I > 0 && Ip >= I && Ip % 4 == 0, "ppo_gru_pack: H=%d I=%d Ip=%d", H, I, Ip);
+  gru_pack_kernel<<<grid_for(3LL * H * Ip + 6LL * H * H), 256, 0, as_stream(stream)>>>(wih, whh, H, I, Ip, wih_pad,
+                                                                                      wihT, whhT);
+  PPO_LAUNCH_CHECK("gru_pack_kernel");
+  return 0;
+}
+
+PPO_API int ppo_concat_cols(const float* src, const int64_t* idx, long long rows, int ncols, float* dst, int ld,
+                            int col0, int zero_to, void* stream) {
+  PPO_REQUIRE(rows >= 0 && ncols >= 0 && zero_to >= ncols && col0 + zero_to <= ld, "ppo_concat_cols: bad shape");
+  if (rows == 0 || zero_to == 0) return 0;
+  concat_cols_kernel<<<grid_for(rows * zero_to), 256, 0, as_stream(stream)>>>(src, idx, rows, ncols, dst, ld, col0,
+                                                                              zero_to);
+  PPO_LAUNCH_CHECK("concat_cols_kernel");
+  return 0;
+}
+
+PPO_API int ppo_rec_indices(const int64_t* envs, int n, int T, int N, int64_t* idx, void* stream) {
+  PPO_REQUIRE(n >= 0 && T > 0 && N > 0, "ppo_rec_indices: bad shape");
+  if (n == 0) return 0;
+  rec_indices_kernel<<<grid_for((long long)T * n), 256, 0, as_stream(stream)>>>(envs, n, T, N, idx);
+  PPO_LAUNCH_CHECK("rec_indices_kernel");
+  return 0;
+}

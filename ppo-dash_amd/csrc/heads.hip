@@ -35,11 +35,11 @@ template <int HC, int AMAX>
 __device__ __forceinline__ void load_head_w(HeadW<HC, AMAX>& w, const float* __restrict__ wc,
                                             const float* __restrict__ wa, int A, int H, int lane) {
 #pragma unroll
-  for (int c = 0; c < HC; ++c) w.wc[c] = wc[lane + 64 * c];
+  for (int c = 0; c < HC; ++c) w.wc[c] = lane + 64 * c < H ? wc[lane + 64 * c] : 0.f;
 #pragma unroll
   for (int o = 0; o < AMAX; ++o)
 #pragma unroll
-    for (int c = 0; c < HC; ++c) w.wa[o][c] = o < A ? wa[o * H + lane + 64 * c] : 0.f;
+    for (int c = 0; c < HC; ++c) w.wa[o][c] = (o < A && lane + 64 * c < H) ? wa[o * H + lane + 64 * c] : 0.f;
 }
 
 // value and logits of one row (all lanes end up with the totals)
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(64 * HW) void heads_act_kernel(
     if (row >= N) break;
     float f[HC];
 #pragma unroll
-    for (int c = 0; c < HC; ++c) f[c] = feat[row * H + lane + 64 * c];
+    for (int c = 0; c < HC; ++c) f[c] = lane + 64 * c < H ? feat[row * H + lane + 64 * c] : 0.f;
     float value, z[AMAX], nl[AMAX], p[AMAX];
     head_dots(w, f, value, z, b0, ba, A);
     categorical(z, A, nl, p);
@@ -157,7 +157,8 @@ struct TrainArgs {
   const float *old_logp, *adv, *vpred, *ret;
   float clip, value_coef, entropy_coef, inv_b;
   int use_clipped_value_loss;
-  float* dfeat;            // [B][H] dL/d(fc pre-activation)
+  int feat_relu;           // features are a ReLU output (CNNBase fc): mask dfeat by f > 0
+  float* dfeat;            // [B][H] dL/d(feature pre-activation)
   float* part_w;           // [blocks][1+A][H]
   float* part_b;           // [blocks][1+A]
   float* part_loss;        // [blocks][3]: Σ max(l1,l2), Σ min(s1,s2), Σ H
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
     if (row >= a.B) break;
     float f[HC];
 #pragma unroll
-    for (int c = 0; c < HC; ++c) f[c] = a.feat[row * H + lane + 64 * c];
+    for (int c = 0; c < HC; ++c) f[c] = lane + 64 * c < H ? a.feat[row * H + lane + 64 * c] : 0.f;
     float value, z[AMAX], nl[AMAX], p[AMAX];
     head_dots(w, f, value, z, b0, a.ba, A);
     categorical(z, A, nl, p);
@@ -240,7 +241,7 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
       float d = g_v * w.wc[c];
 #pragma unroll
       for (int o = 0; o < AMAX; ++o) d += gz[o] * w.wa[o][c];
-      a.dfeat[row * H + lane + 64 * c] = f[c] > 0.f ? d : 0.f;
+      if (lane + 64 * c < H) a.dfeat[row * H + lane + 64 * c] = (!a.feat_relu || f[c] > 0.f) ? d : 0.f;
       gwc[c] += g_v * f[c];
 #pragma unroll
       for (int o = 0; o < AMAX; ++o) gwa[o][c] += gz[o] * f[c];
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
         const int j = lane + 64 * c;
         float s = red[0][j];
         for (int q = 1; q < HW; ++q) s += red[q][j];
-        a.part_w[((size_t)blockIdx.x * NO + o) * H + j] = s;
+        if (j < H) a.part_w[((size_t)blockIdx.x * NO + o) * H + j] = s;
       }
     }
     __syncthreads();
@@ -334,6 +335,12 @@ __global__ __launch_bounds__(256) void mean_kernel(const float* __restrict__ x, 
   if (threadIdx.x == 0) out[0] = (float)(r[0] / (double)n);
 }
 
+// 64-column chunks per lane, rounded up to an instantiated count (1, 2, 4, 8)
+static inline int hc_of(int H) {
+  const int c = (H + 63) / 64;
+  return c <= 1 ? 1 : c <= 2 ? 2 : c <= 4 ? 4 : 8;
+}
+
 template <int HC, int AMAX>
 int launch_act(const float* feat, int N, int H, const float* wc, const float* bc, const float* wa, const float* ba,
                int A, const float* noise, unsigned long long seed, unsigned long long counter, int det,
@@ -356,7 +363,7 @@ int dispatch_act(int HC, const float* feat, int N, int H, const float* wc, const
     case 4: return launch_act<4, AMAX>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
     case 8: return launch_act<8, AMAX>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
   }
-  ppo_set_error("heads: hidden size %d not supported (64, 128, 256, 512)", H);
+  ppo_set_error("heads: hidden size %d not supported (<= 512)", H);
   return PPO_EARG;
 }
 
@@ -375,7 +382,7 @@ int dispatch_train(int HC, const TrainArgs& a, int blocks, hipStream_t st) {
     case 4: return launch_train<4, AMAX>(a, blocks, st);
     case 8: return launch_train<8, AMAX>(a, blocks, st);
   }
-  ppo_set_error("heads: hidden size %d not supported (64, 128, 256, 512)", a.H);
+  ppo_set_error("heads: hidden size %d not supported (<= 512)", a.H);
   return PPO_EARG;
 }
 
@@ -391,13 +398,14 @@ PPO_API int ppo_heads_act(const float* feat, int N, int H, const float* wc, cons
                           unsigned long long counter, int deterministic, const int64_t* given, float* value,
                           int64_t* action, float* logp, float* entropy, void* stream) {
   PPO_REQUIRE(N >= 0 && A >= 1 && A <= 16, "ppo_heads_act: N=%d A=%d (1..16 actions)", N, A);
-  PPO_REQUIRE(H % 64 == 0, "ppo_heads_act: hidden size %d must be a multiple of 64", H);
+  PPO_REQUIRE(H > 0 && H <= 512, "ppo_heads_act: hidden size %d (1..512)", H);
   if (N == 0) return 0;
   hipStream_t st = as_stream(stream);
+  const int HC = hc_of(H);
   if (A <= 8)
-    return dispatch_act<8>(H / 64, feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
+    return dispatch_act<8>(HC, feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
                            action, logp, entropy, st);
-  return dispatch_act<16>(H / 64, feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
+  return dispatch_act<16>(HC, feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
                           action, logp, entropy, st);
 }
 
@@ -410,20 +418,21 @@ PPO_API int ppo_heads_train(const float* feat, int B, int H, const float* wc, co
                             const float* ba, int A, const int64_t* idx, long long row0, const int64_t* actions,
                             const float* old_logp, const float* adv, const float* vpred, const float* ret, float clip,
                             float value_coef, float entropy_coef, float inv_b, int use_clipped_value_loss,
-                            float* dfeat, float* part_w, float* part_b, float* part_loss, void* stream) {
+                            int feat_relu, float* dfeat, float* part_w, float* part_b, float* part_loss, void* stream) {
   PPO_REQUIRE(B > 0 && A >= 1 && A <= 16, "ppo_heads_train: B=%d A=%d", B, A);
-  PPO_REQUIRE(H % 64 == 0, "ppo_heads_train: hidden size %d must be a multiple of 64", H);
+  PPO_REQUIRE(H > 0 && H <= 512, "ppo_heads_train: hidden size %d (1..512)", H);
   TrainArgs a;
   a.feat = feat; a.B = B; a.H = H; a.A = A; a.wc = wc; a.bc = bc; a.wa = wa; a.ba = ba;
   a.idx = idx; a.row0 = row0; a.actions = actions; a.old_logp = old_logp; a.adv = adv; a.vpred = vpred; a.ret = ret;
   a.clip = clip; a.value_coef = value_coef; a.entropy_coef = entropy_coef; a.inv_b = inv_b;
   a.use_clipped_value_loss = use_clipped_value_loss;
+  a.feat_relu = feat_relu;
   a.dfeat = dfeat; a.part_w = part_w; a.part_b = part_b; a.part_loss = part_loss;
   a.rows_per_wave = 32;
   const int blocks = ppo_heads_train_blocks(B);
   hipStream_t st = as_stream(stream);
-  if (A <= 8) return dispatch_train<8>(H / 64, a, blocks, st);
-  return dispatch_train<16>(H / 64, a, blocks, st);
+  if (A <= 8) return dispatch_train<8>(hc_of(H), a, blocks, st);
+  return dispatch_train<16>(hc_of(H), a, blocks, st);
 }
 
 // Σ over the heads_train blocks (fixed order) -> head gradients; losses -> loss_acc

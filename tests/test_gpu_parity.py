@@ -462,3 +462,131 @@ def test_full_size_forward_vs_oracle(gpu):
     c = O.categorical(logits, deterministic=True)
     np.testing.assert_allclose(v.cpu().numpy()[sub, 0], value, atol=1e-4)
     np.testing.assert_allclose(lp.cpu().numpy()[sub, 0], c["log_prob"], atol=1e-4)
+
+
+# ------------------------------------------------------------------ GRU (K12)
+def _load_flat(pol, flat):
+    with torch.no_grad():
+        off = 0
+        for p in pol.parameters():
+            p.copy_(torch.from_numpy(np.ascontiguousarray(flat[off:off + p.numel()])).view_as(p))
+            off += p.numel()
+
+
+def test_gru_golden_evaluate_and_step(gpu):
+    """Recurrent CNNBase + vector obs (T/model.py:89-166,192-199) on the reference's
+    recorded sequence: values / log-probs / entropy / final hidden within 2e-5,
+    and the single-step act path (model.py:112-115)."""
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.synthetic import Discrete
+    d = golden("gru_eval.npz")
+    hidden, V, N, T = (int(x) for x in d["meta"])
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase, base_kwargs={"recurrent": True, "hidden_size": hidden},
+                   vector_obs_len=V)
+    _load_flat(pol, d["params"])
+    pol.to(gpu)
+    obs = _dev(d["obs_u8"].reshape(T * N, 4, 84, 84))
+    vec = _dev(d["vector_obs"].reshape(T * N, V))
+    masks = _dev(d["masks"].reshape(T * N, 1))
+    h0 = _dev(d["h0"])
+    acts = _dev(d["actions"])
+    value, logp, ent, hT = pol.evaluate_actions(obs, vec, h0, masks, acts)
+    np.testing.assert_allclose(value.cpu().numpy(), d["values"], atol=2e-5)
+    np.testing.assert_allclose(logp.cpu().numpy(), d["log_probs"], atol=2e-5)
+    np.testing.assert_allclose(ent.item(), d["entropy"][0], atol=2e-5)
+    np.testing.assert_allclose(hT.cpu().numpy(), d["hT"], atol=2e-5)
+    v1, a1, lp1, h1 = pol.act(obs[:N], vec[:N], h0, _dev(d["masks"][0]), deterministic=True)
+    np.testing.assert_allclose(v1.cpu().numpy(), d["step_value"], atol=2e-5)
+    np.testing.assert_allclose(h1.cpu().numpy(), d["step_h"], atol=2e-5)
+
+
+@pytest.mark.parametrize("H,V", [(64, 14), (256, 14)])
+def test_recurrent_minibatch_grads_vs_oracle(gpu, H, V):
+    """One recurrent_generator minibatch through the fused path (trunk, vector-obs
+    concat, GRU over T with masks, heads/loss, BPTT, all wgrads) vs the oracle's
+    float64 analytic gradients: max |err| <= 2e-5 * max|grad| per tensor."""
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.algo.ppo import FlatAdam
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import Discrete
+    torch.manual_seed(H)
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase, base_kwargs={"recurrent": True, "hidden_size": H},
+                   vector_obs_len=V)
+    with torch.no_grad():
+        pol.dist.linear.weight.mul_(50.0)
+        pol.base.critic_linear.weight.mul_(3.0)
+        pol.base.gru.bias_ih_l0.uniform_(-0.3, 0.3)
+        pol.base.gru.bias_hh_l0.uniform_(-0.3, 0.3)
+    init = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy().astype(np.float64)
+    pol.to(gpu)
+    eng = pol.hip_engine()
+    T, N = 5, 6
+    st = RolloutStorage(T, N, (4, 84, 84), [V], Discrete(8), H, obs_dtype=torch.uint8, device=gpu)
+    g = torch.Generator().manual_seed(H + 1)
+    st.obs.copy_(torch.randint(0, 256, st.obs.shape, dtype=torch.uint8, generator=g).to(gpu))
+    st.vector_obs.copy_(torch.rand(st.vector_obs.shape, generator=g).to(gpu))
+    st.recurrent_hidden_states.copy_(torch.randn(st.recurrent_hidden_states.shape, generator=g).to(gpu) * 0.5)
+    st.masks.copy_((torch.rand(st.masks.shape, generator=g) > 0.3).float().to(gpu))
+    st.actions.copy_(torch.randint(0, 8, st.actions.shape, generator=g).to(gpu))
+    st.action_log_probs.copy_((torch.log(torch.rand(st.action_log_probs.shape, generator=g)) * 0.3 - 2.0).to(gpu))
+    st.value_preds.copy_(torch.randn(st.value_preds.shape, generator=g).to(gpu) * 0.1)
+    st.returns.copy_(torch.randn(st.returns.shape, generator=g).to(gpu))
+    adv = torch.randn(T, N, generator=g).to(gpu)
+    envs = torch.tensor([4, 0, 3], dtype=torch.int64)
+    hp = {"clip": 0.1, "value_coef": 0.5, "entropy_coef": 0.01, "use_clipped_value_loss": True}
+    loss = torch.zeros(3, dtype=torch.float64, device=gpu)
+    opt = FlatAdam(pol.parameters(), lr=0.0, eps=1e-5, max_grad_norm=None)
+    eng.train_minibatch_rec(st, adv, envs.to(gpu), hp, loss, opt)
+    torch.cuda.synchronize()
+    shapes = O.cnn_param_shapes(H, recurrent=True, vector_obs_len=V)
+    p = O.unflatten(init, shapes)
+    e = envs.numpy()
+    rows = (np.arange(T)[:, None] * N + e[None, :]).reshape(-1)
+    obs = st.obs[:-1].reshape(T * N, 4, 84, 84).cpu().numpy()[rows]
+    vec = st.vector_obs[:-1].reshape(T * N, V).cpu().numpy()[rows]
+    h0 = st.recurrent_hidden_states[0].cpu().numpy()[e]
+    masks = st.masks[:-1, :, 0].cpu().numpy()[:, e]
+    value, logits, cache = O.recurrent_forward(p, O.decode_obs(obs), vec, h0, masks)
+    f = lambda t: t.reshape(-1).cpu().numpy()[rows]  # noqa: E731
+    lg = O.loss_head_grads(value, logits, f(st.actions), f(st.action_log_probs), f(adv),
+                           st.value_preds[:-1].reshape(-1).cpu().numpy()[rows],
+                           st.returns[:-1].reshape(-1).cpu().numpy()[rows], 0.1, 0.5, 0.01)
+    grads = O.recurrent_backward(p, cache, lg["g_value"], lg["g_logits"])
+    got = O.unflatten(eng.grad.cpu().numpy(), shapes)
+    for name, _ in shapes:
+        ref = grads[name]
+        err = np.abs(got[name] - ref).max()
+        assert err <= 2e-5 * max(np.abs(ref).max(), 1e-3), (name, err, np.abs(ref).max())
+    np.testing.assert_allclose(loss.cpu().numpy(), [lg["value_loss"], lg["action_loss"], lg["entropy"]],
+                               rtol=2e-5, atol=1e-6)
+
+
+def test_recurrent_ppo_iteration_runs(gpu):
+    """c5-shaped plumbing at small scale: rollout with hidden state carry, GAE,
+    recurrent PPO.update (BPTT), after_update — finite losses, parameters move."""
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.algo import PPO
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import SyntheticVecEnv
+    torch.manual_seed(2)
+    N, T, V, H = 16, 8, 14, 64
+    env = SyntheticVecEnv(N, seed=5, p_done=0.2, device=gpu)
+    pol = M.Policy((4, 84, 84), env.action_space, base=M.CNNBase, base_kwargs={"recurrent": True, "hidden_size": H},
+                   vector_obs_len=V)
+    pol.to(gpu)
+    agent = PPO(pol, 0.1, 2, 4, 0.5, 0.001, lr=1e-3, eps=1e-5, max_grad_norm=0.5)
+    st = RolloutStorage(T, N, (4, 84, 84), [V], env.action_space, H, obs_dtype=torch.uint8, device=gpu)
+    env.reset_into(st.obs[0])
+    before = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).clone()
+    for step in range(T):
+        v, a, lp, h = pol.act(st.obs[step], st.vector_obs[step], st.recurrent_hidden_states[step], st.masks[step])
+        r, m, bm = env.step_into(st.obs[step + 1], a)
+        st.insert(st.obs[step + 1], torch.rand(N, V, device=gpu), h, a, lp, v, r, m, bm)
+    nv = pol.get_value(st.obs[-1], st.vector_obs[-1], st.recurrent_hidden_states[-1], st.masks[-1])
+    st.compute_returns(nv, True, 0.99, 0.95, False)
+    losses = agent.update(st)
+    st.after_update()
+    after = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
+    assert all(np.isfinite(losses))
+    assert (after - before).abs().max().item() > 1e-5
+    assert torch.equal(st.recurrent_hidden_states[0], st.recurrent_hidden_states[-1])

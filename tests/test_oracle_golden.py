@@ -133,3 +133,43 @@ def test_full_iteration_replay():
     np.testing.assert_allclose(r["first"]["clipped_grad"], d["mb0_clipped_grad"], rtol=0, atol=1e-6)
     np.testing.assert_allclose(r["losses"], d["losses"], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(r["final_params"], d["final_params"], rtol=0, atol=1e-6)
+
+
+def test_gru_backward_finite_difference():
+    """The oracle's hand-written BPTT (used to check the HIP GRU backward) against
+    central finite differences of its own forward (float64)."""
+    rng = np.random.default_rng(0)
+    H, I, T, n = 4, 3, 5, 2
+    p = {"base.gru.weight_ih_l0": rng.standard_normal((3 * H, I)) * 0.5,
+         "base.gru.weight_hh_l0": rng.standard_normal((3 * H, H)) * 0.5,
+         "base.gru.bias_ih_l0": rng.standard_normal(3 * H) * 0.1,
+         "base.gru.bias_hh_l0": rng.standard_normal(3 * H) * 0.1}
+    x = rng.standard_normal((T * n, I))
+    h0 = rng.standard_normal((n, H))
+    masks = (rng.random((T, n)) > 0.3).astype(np.float64)
+    wout = rng.standard_normal((T * n, H))
+
+    def loss(pp, xx):
+        out, _ = O.gru_sequence_cache(pp, xx, h0, masks)
+        return (out * wout).sum()
+
+    out, cache = O.gru_sequence_cache(p, x, h0, masks)
+    g, dx = O.gru_backward(p, x, masks, cache, wout)
+    eps = 1e-6
+    for k in p:
+        num = np.zeros_like(p[k])
+        for i in np.ndindex(p[k].shape):
+            pp = {kk: v.copy() for kk, v in p.items()}
+            pp[k][i] += eps
+            lp = loss(pp, x)
+            pp[k][i] -= 2 * eps
+            num[i] = (lp - loss(pp, x)) / (2 * eps)
+        np.testing.assert_allclose(g[k], num, rtol=1e-5, atol=1e-7)
+    num = np.zeros_like(x)
+    for i in np.ndindex(x.shape):
+        xx = x.copy()
+        xx[i] += eps
+        lp = loss(p, xx)
+        xx[i] -= 2 * eps
+        num[i] = (lp - loss(p, xx)) / (2 * eps)
+    np.testing.assert_allclose(dx, num, rtol=1e-5, atol=1e-7)
