@@ -47,7 +47,9 @@ def parse():
     p.add_argument("--num-steps", type=int, default=128)
     p.add_argument("--ppo-epoch", type=int, default=3)
     p.add_argument("--num-mini-batch", type=int, default=8)
-    p.add_argument("--hidden", type=int, default=512)
+    p.add_argument("--hidden", type=int, default=None, help="default 512 (CNN) / 256 (GRU)")
+    p.add_argument("--recurrent", action="store_true", help="c5: GRU policy + vector obs")
+    p.add_argument("--vec-len", type=int, default=14, help="vector obs length with --recurrent (OTC v7: 14)")
     p.add_argument("--profile-kernel", default="conv1_fwd_u8")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-envs", type=int, default=32)
@@ -91,15 +93,16 @@ def gae_roofline(device, lanes, T=128, reps=10):
             "ms_per_launch": round(ms, 4)}
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, workload):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
-    (profiles/roofline_traffic.json, written by tools/pmc_traffic.py)."""
+    (profiles/roofline_traffic.json, written by tools/pmc_traffic.py) — only when
+    they were measured on this same kernel and workload."""
     path = os.path.join(ROOT, "profiles", "roofline_traffic.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None, None
-    if d.get("kernel") != kernel:
+    if d.get("kernel") != kernel or d.get("workload") != workload:
         return None, None
     return d.get("traffic_bytes_per_launch"), f"profiles/{d.get('tag', '?')}_traffic.json"
 
@@ -142,15 +145,19 @@ def main():
     from a2c_ppo_acktr.storage import RolloutStorage
     from a2c_ppo_acktr.synthetic import SyntheticVecEnv
 
-    N, T, E, M, H = args.envs, args.num_steps, args.ppo_epoch, args.num_mini_batch, args.hidden
+    N, T, E, M = args.envs, args.num_steps, args.ppo_epoch, args.num_mini_batch
+    H = args.hidden or (256 if args.recurrent else 512)
+    V = args.vec_len if args.recurrent else 0
     torch.manual_seed(1)
     env = SyntheticVecEnv(N, seed=123 + 7919 * rank, p_done=0.01, device=device)
-    policy = Policy((4, 84, 84), env.action_space, base=CNNBase, base_kwargs={"recurrent": False, "hidden_size": H})
+    policy = Policy((4, 84, 84), env.action_space, base=CNNBase,
+                    base_kwargs={"recurrent": args.recurrent, "hidden_size": H}, vector_obs_len=V)
     policy.to(device)
     agent = PPO(policy, 0.1, E, M, 0.5, 0.001, lr=1e-4, eps=1e-5, max_grad_norm=0.5)
-    rollouts = RolloutStorage(T, N, (4, 84, 84), [0], env.action_space, policy.recurrent_hidden_state_size,
+    rollouts = RolloutStorage(T, N, (4, 84, 84), [V], env.action_space, policy.recurrent_hidden_state_size,
                               obs_dtype=torch.uint8, device=device)
     env.reset_into(rollouts.obs[0])
+    vec_src = torch.rand(N, V, device=device) if V else None   # synthetic vector obs (fixed)
 
     def iteration():
         for step in range(T):
@@ -159,7 +166,8 @@ def main():
                                                       rollouts.recurrent_hidden_states[step], rollouts.masks[step])
             slot = rollouts.obs[step + 1]
             reward, masks, bad_masks = env.step_into(slot, action)
-            rollouts.insert(slot, rollouts.vector_obs[step + 1], hxs, action, logp, value, reward, masks, bad_masks)
+            rollouts.insert(slot, vec_src if V else rollouts.vector_obs[step + 1], hxs, action, logp, value, reward,
+                            masks, bad_masks)
         with torch.no_grad():
             next_value = policy.get_value(rollouts.obs[-1], rollouts.vector_obs[-1],
                                           rollouts.recurrent_hidden_states[-1], rollouts.masks[-1])
@@ -201,10 +209,13 @@ def main():
         return
 
     launches, ms_total, flops = prof.tolist()
+    workload = ((f"c5: CNNBase+GRU H={H} + {V} vector obs" if args.recurrent else f"c3: CNNBase H={H}")
+                + f", {N} env lanes x {T} steps per GPU, PPO {E} epochs x {M} minibatches "
+                  f"(rollout + GAE + update, fp32)")
     roof = None
     if launches > 0 and ms_total > 0:
         tflops = flops / (ms_total * 1e-3) / 1e12
-        traffic, tsrc = pmc_traffic(args.profile_kernel)
+        traffic, tsrc = pmc_traffic(args.profile_kernel, workload)
         roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(tflops / PEAK_FP32_MFMA_TFLOPS, 4),
                 "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch (HBM, PMC)",
@@ -221,8 +232,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic: counter-hash u8 4x84x84 obs, U[0,1) rewards, Bernoulli(0.01) dones; random-init weights",
-        "config": {"workload": f"c3: CNNBase H={H}, {N} env lanes x {T} steps per GPU, PPO {E} epochs x {M} "
-                               f"minibatches (rollout + GAE + update, fp32)",
+        "config": {"workload": workload,
                    "envs_per_gpu": N, "num_steps": T, "ppo_epoch": E, "num_mini_batch": M, "hidden": H,
                    "global_batch": N * T * world, "parallelism": f"dp{world}"},
         "roofline": roof, "cpu_baseline": cpu, "gae_roofline": gae,

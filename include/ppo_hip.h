@@ -76,6 +76,13 @@ int ppo_gather_env_columns(const void* src, const int64_t* envs, void* dst, int 
 int ppo_synth_env_step(uint8_t* obs, int N, long long obs_bytes, float* reward, float* mask, float* bad_mask,
                        unsigned long long seed, unsigned long long step, float p_done, void* stream);
 
+/* CartPole-v1 dynamics (c1's env, restated; gym absent): one step of every lane
+ * (action NULL: reset), obs [N][4] written in place, auto-reset on done /
+ * TimeLimit(max_steps) with bad_mask 0 on truncation; ep_len = finished length or 0 */
+int ppo_cartpole_step(float* state, int* steps, const int64_t* action, float* obs, float* reward, float* mask,
+                      float* bad_mask, float* ep_len, int N, unsigned long long seed, unsigned long long counter,
+                      int max_steps, void* stream);
+
 /* ---------------- CNNBase trunk (model.py:176-180) ------------------------- */
 long long ppo_packed_weights_size(int H);
 int ppo_packed_offsets(int H, long long* off6);
@@ -93,12 +100,16 @@ int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, flo
 /* model.py:180 Linear(1568,H)+ReLU (generic Linear+ReLU) */
 int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, const float* b, int N, float* out,
                         void* stream);
-/* Linear with row strides and optional ReLU / bias (GRU input projection, fc into a
- * padded [x | vector_obs] row) */
-int ppo_linear_fwd_ex(const float* x, int M, int K, int lda, const float* w, const float* b, int N, float* out,
-                      int ldo, int relu, void* stream);
-int ppo_linear_dgrad_ex(const float* dy, int M, int K, const float* wt, int N, const float* act, int ldact, float* dx,
-                        void* stream);
+/* Linear with row strides, optional A-row gather, bias and activation
+ * (0 none, 1 ReLU, 2 tanh): the fc into a padded [x | vector_obs] row, the GRU
+ * input projection, MLPBase's tanh layers (model.py:212-218) */
+int ppo_linear_fwd_ex(const float* x, const int64_t* idx, int M, int K, int lda, const float* w, const float* b,
+                      int N, float* out, int ldo, int act, void* stream);
+/* dgrad through the activation that produced `act` (mode 1 ReLU, 2 tanh) */
+int ppo_linear_dgrad_ex(const float* dy, int M, int K, const float* wt, int N, const float* act, int ldact, int mode,
+                        float* dx, void* stream);
+/* dst [cols][rows] = srcᵀ */
+int ppo_transpose(const float* src, int rows, int cols, float* dst, void* stream);
 /* algo/ppo.py:80-81 loss.backward() through the trunk: dgrad with the ReLU mask
  * of the layer below fused, wgrad as split-K partial slabs + deterministic reduce */
 int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
@@ -147,19 +158,25 @@ int ppo_rec_indices(const int64_t* envs, int n, int T, int N, int64_t* idx, void
 /* ---------------- heads, distribution, loss -------------------------------- */
 /* model.py:54-79 act / get_value / evaluate_actions heads + distributions.py:17-27
  * FixedCategorical: value, logits, logsumexp, sample = argmax(probs/E) (noise =
- * E, host replay) or counter-RNG Exp(1) (noise NULL), mode, log_probs, entropy */
-int ppo_heads_act(const float* feat, int N, int H, const float* wc, const float* bc, const float* wa,
+ * E, host replay) or counter-RNG Exp(1) (noise NULL), mode, log_probs, entropy.
+ * feat_v: critic features when they differ from the policy features (MLPBase,
+ * model.py:231-234); NULL = feat */
+int ppo_heads_act(const float* feat, const float* feat_v, int N, int H, const float* wc, const float* bc,
+                  const float* wa,
                   const float* ba, int A, const float* noise, unsigned long long seed, unsigned long long counter,
                   int deterministic, const int64_t* given, float* value, int64_t* action, float* logp,
                   float* entropy, void* stream);
 /* algo/ppo.py:57-81 evaluate_actions + clipped surrogate + clipped value loss +
- * entropy, forward and analytic backward to dL/dfeature, head-gradient partials */
+ * entropy, forward and analytic backward to dL/dfeature (through the features'
+ * activation feat_act: 0 none, 1 ReLU, 2 tanh), head-gradient partials; with
+ * feat_v the critic branch's gradient goes to dfeat_v */
 int ppo_heads_train_blocks(int B);
-int ppo_heads_train(const float* feat, int B, int H, const float* wc, const float* bc, const float* wa,
+int ppo_heads_train(const float* feat, const float* feat_v, int B, int H, const float* wc, const float* bc,
+                    const float* wa,
                     const float* ba, int A, const int64_t* idx, long long row0, const int64_t* actions,
                     const float* old_logp, const float* adv, const float* vpred, const float* ret, float clip,
-                    float value_coef, float entropy_coef, float inv_b, int use_clipped_value_loss, int feat_relu,
-                    float* dfeat, float* part_w, float* part_b, float* part_loss, void* stream);
+                    float value_coef, float entropy_coef, float inv_b, int use_clipped_value_loss, int feat_act,
+                    float* dfeat, float* dfeat_v, float* part_w, float* part_b, float* part_loss, void* stream);
 int ppo_heads_reduce(const float* part_w, const float* part_b, const float* part_loss, int nblk, int H, int A,
                      float* g_wc, float* g_bc, float* g_wa, float* g_ba, double* loss_acc, double inv_b, float scale,
                      int use_clipped_value_loss, void* stream);

@@ -398,6 +398,129 @@ def recurrent_backward(p, cache, g_value, g_logits):
 
 
 # ---------------------------------------------------------------------------
+# MLPBase (model.py:202-234): actor / critic towers Linear-Tanh-Linear-Tanh
+# ---------------------------------------------------------------------------
+def mlp_param_shapes(num_inputs=4, hidden=64, num_actions=2):
+    """named_parameters() order of Policy((num_inputs,), Discrete(A), MLPBase)."""
+    I, H = num_inputs, hidden
+    return [("base.actor.0.weight", (H, I)), ("base.actor.0.bias", (H,)),
+            ("base.actor.2.weight", (H, H)), ("base.actor.2.bias", (H,)),
+            ("base.critic.0.weight", (H, I)), ("base.critic.0.bias", (H,)),
+            ("base.critic.2.weight", (H, H)), ("base.critic.2.bias", (H,)),
+            ("base.critic_linear.weight", (1, H)), ("base.critic_linear.bias", (1,)),
+            ("dist.linear.weight", (num_actions, H)), ("dist.linear.bias", (num_actions,))]
+
+
+def mlp_forward(p, x):
+    """value = critic_linear(critic(x)), logits = dist.linear(actor(x)) (model.py:222-234)."""
+    x = np.asarray(x, p["base.actor.0.weight"].dtype)
+    cache = dict(x=x)
+    for tower in ("actor", "critic"):
+        h1 = np.tanh(x @ p[f"base.{tower}.0.weight"].T + p[f"base.{tower}.0.bias"])
+        h2 = np.tanh(h1 @ p[f"base.{tower}.2.weight"].T + p[f"base.{tower}.2.bias"])
+        cache[tower] = (h1, h2)
+    value = cache["critic"][1] @ p["base.critic_linear.weight"].T + p["base.critic_linear.bias"]
+    logits = cache["actor"][1] @ p["dist.linear.weight"].T + p["dist.linear.bias"]
+    return value[:, 0], logits, cache
+
+
+def mlp_backward(p, cache, g_value, g_logits):
+    x = cache["x"]
+    g_value = np.asarray(g_value, x.dtype)
+    g_logits = np.asarray(g_logits, x.dtype)
+    a2, c2 = cache["actor"][1], cache["critic"][1]
+    g = {"base.critic_linear.weight": g_value[None, :] @ c2, "base.critic_linear.bias": np.array([g_value.sum()]),
+         "dist.linear.weight": g_logits.T @ a2, "dist.linear.bias": g_logits.sum(0)}
+    douts = {"critic": g_value[:, None] * p["base.critic_linear.weight"], "actor": g_logits @ p["dist.linear.weight"]}
+    for tower in ("actor", "critic"):
+        h1, h2 = cache[tower]
+        dz2 = douts[tower] * (1 - h2 * h2)
+        g[f"base.{tower}.2.weight"] = dz2.T @ h1
+        g[f"base.{tower}.2.bias"] = dz2.sum(0)
+        dz1 = (dz2 @ p[f"base.{tower}.2.weight"]) * (1 - h1 * h1)
+        g[f"base.{tower}.0.weight"] = dz1.T @ x
+        g[f"base.{tower}.0.bias"] = dz1.sum(0)
+    return g
+
+
+# ---------------------------------------------------------------------------
+# CartPole-v1 (gym.envs.classic_control.cartpole, the c1 environment; the
+# reference reaches it through T/envs.py:40-96).  fp32 restatement of the
+# synthetic GPU env's dynamics and its counter-RNG resets.
+# ---------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def mix64(z):
+    """splitmix64 finaliser on uint64 arrays (wrapping arithmetic)."""
+    z = np.asarray(z, np.uint64)
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def u01_open0(h):
+    return ((h >> np.uint64(40)).astype(np.uint32).astype(np.float32) + np.float32(1.0)) * np.float32(1.0 / 16777216.0)
+
+
+def cartpole_reset_state(seed, counter, lanes):
+    lanes = np.asarray(lanes, np.uint64)
+    with np.errstate(over="ignore"):
+        key = np.uint64(seed) ^ mix64(np.uint64(counter) * np.uint64(0x100000001B3) + lanes * np.uint64(0x9E3779B1)
+                                      + np.uint64(0xCA27))
+        st = [(u01_open0(mix64(key + np.uint64(i))) - np.float32(0.5)) * np.float32(0.1) for i in range(4)]
+    return np.stack(st, 1).astype(np.float32)
+
+
+def cartpole_step(state, steps, action, seed, counter, max_steps=500):
+    """One auto-resetting step for every lane.  Returns (state', steps', obs,
+    reward, mask, bad_mask, ep_len); action None = reset all lanes."""
+    state = np.array(state, np.float32)
+    steps = np.array(steps, np.int32)
+    N = state.shape[0]
+    f = np.float32
+    reward = np.zeros(N, f)
+    mask = np.ones(N, f)
+    bad = np.ones(N, f)
+    ep_len = np.zeros(N, f)
+    if action is None:
+        reset = np.ones(N, bool)
+    else:
+        gravity, masscart, masspole = f(9.8), f(1.0), f(0.1)
+        total_mass = masspole + masscart
+        length = f(0.5)
+        pml = masspole * length
+        tau = f(0.02)
+        theta_thr, x_thr = f(12.0 * 2.0 * 3.14159265358979 / 360.0), f(2.4)
+        x, x_dot, theta, theta_dot = (state[:, i].copy() for i in range(4))
+        force = np.where(np.asarray(action).reshape(-1) == 1, f(10.0), f(-10.0)).astype(f)
+        ct, sn = np.cos(theta), np.sin(theta)
+        temp = (force + pml * theta_dot * theta_dot * sn) / total_mass
+        thetaacc = (gravity * sn - ct * temp) / (length * (f(4.0 / 3.0) - masspole * ct * ct / total_mass))
+        xacc = temp - pml * thetaacc * ct / total_mass
+        x = x + tau * x_dot
+        x_dot = x_dot + tau * xacc
+        theta = theta + tau * theta_dot
+        theta_dot = theta_dot + tau * thetaacc
+        state = np.stack([x, x_dot, theta, theta_dot], 1).astype(f)
+        steps = steps + 1
+        done = (x < -x_thr) | (x > x_thr) | (theta < -theta_thr) | (theta > theta_thr)
+        trunc = ~done & (steps >= max_steps)
+        reward[:] = 1.0
+        mask[done | trunc] = 0.0
+        bad[trunc] = 0.0
+        reset = done | trunc
+        ep_len[reset] = steps[reset]
+    if reset.any():
+        lanes = np.nonzero(reset)[0]
+        state[lanes] = cartpole_reset_state(seed, counter, lanes)
+        steps[lanes] = 0
+    return state, steps, state.copy(), reward, mask, bad, ep_len
+
+
+# ---------------------------------------------------------------------------
 # PPO loss and its gradients (algo/ppo.py:61-81) with torch's autograd
 # conventions: min/max split the gradient 1/2-1/2 at ties; clamp passes it
 # inside the closed interval; relu passes it where the output is > 0.

@@ -145,8 +145,8 @@ class CNNEngine:
              self.pv(self.B1), a1.data_ptr(), s)
         call("ppo_conv2_fwd", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), s)
         call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
-        call("ppo_linear_fwd_ex", a3.data_ptr(), B, FEAT, FEAT, self.pk(2), self.pv(self.B4), self.H, out.data_ptr(),
-             ldo, 1, s)
+        call("ppo_linear_fwd_ex", a3.data_ptr(), None, B, FEAT, FEAT, self.pk(2), self.pv(self.B4), self.H,
+             out.data_ptr(), ldo, 1, s)
         return out
 
     def _check_obs(self, obs):
@@ -155,7 +155,8 @@ class CNNEngine:
             raise RuntimeError(f"CNNBase expects [N,{self.C},84,84] observations, got {tuple(obs.shape)}")
         return obs.contiguous()
 
-    def _heads(self, h, B, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False):
+    def _heads(self, h, B, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False,
+               hv=None):
         value = torch.empty(B, 1, device=self.device)
         if value_only:
             action = logp = ent = None
@@ -168,12 +169,18 @@ class CNNEngine:
             if noise.shape != (B, self.A):
                 raise RuntimeError(f"noise must be [{B},{self.A}]")
         self.rng_counter += 1
-        call("ppo_heads_act", h.data_ptr(), B, self.H, self.pv(self.WC), self.pv(self.BC), self.pv(self.WA),
+        call("ppo_heads_act", h.data_ptr(), ptr(hv), B, self.H, self.pv(self.WC), self.pv(self.BC), self.pv(self.WA),
              self.pv(self.BA), self.A, ptr(noise), self.rng_seed, self.rng_counter, int(bool(deterministic)),
              ptr(given.reshape(-1).contiguous() if given is not None else None, torch.int64, "action"),
              value.data_ptr(), None if given is not None or value_only else action.data_ptr(),
              ptr(logp), ptr(ent), stream())
         return value, action, logp, ent
+
+    def mean(self, x):
+        """model.py:77 dist.entropy().mean() on the device (0-d tensor)"""
+        out = torch.empty((), device=self.device)
+        call("ppo_mean_f32", x.data_ptr(), x.numel(), out.data_ptr(), stream())
+        return out
 
     def act(self, obs, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False):
         self.ensure_bound()
@@ -184,18 +191,18 @@ class CNNEngine:
         return self._heads(h, B, deterministic, noise, given, want_entropy, value_only)
 
     # --------------------------------------------------------------- training
-    def _heads_train(self, storage, adv, idx, feat, B, hp, loss_acc, dfeat, feat_relu):
+    def _heads_train(self, storage, adv, idx, feat, B, hp, loss_acc, dfeat, feat_act, feat_v=None, dfeat_v=None):
         ws, dev, H, A, s = self.ws["train"], self.device, self.H, self.A, stream()
         nblk = call("ppo_heads_train_blocks", B)
         part_w = ws.get("part_w", nblk * (1 + A) * H, device=dev)
         part_b = ws.get("part_b", nblk * (1 + A), device=dev)
         part_l = ws.get("part_l", nblk * 3, device=dev)
         inv_b = 1.0 / B
-        call("ppo_heads_train", feat.data_ptr(), B, H, self.pv(self.WC), self.pv(self.BC), self.pv(self.WA),
+        call("ppo_heads_train", feat.data_ptr(), ptr(feat_v), B, H, self.pv(self.WC), self.pv(self.BC), self.pv(self.WA),
              self.pv(self.BA), A, idx.data_ptr(), 0, storage.actions.data_ptr(), storage.action_log_probs.data_ptr(),
              adv.data_ptr(), storage.value_preds.data_ptr(), storage.returns.data_ptr(), hp["clip"], hp["value_coef"],
-             hp["entropy_coef"], inv_b, int(hp["use_clipped_value_loss"]), int(feat_relu), dfeat.data_ptr(),
-             part_w.data_ptr(), part_b.data_ptr(), part_l.data_ptr(), s)
+             hp["entropy_coef"], inv_b, int(hp["use_clipped_value_loss"]), int(feat_act), dfeat.data_ptr(),
+             ptr(dfeat_v), part_w.data_ptr(), part_b.data_ptr(), part_l.data_ptr(), s)
         call("ppo_heads_reduce", part_w.data_ptr(), part_b.data_ptr(), part_l.data_ptr(), nblk, H, A,
              self.gv(self.WC), self.gv(self.BC), self.gv(self.WA), self.gv(self.BA), loss_acc.data_ptr(), inv_b, 1.0,
              int(hp["use_clipped_value_loss"]), s)
@@ -229,7 +236,7 @@ class CNNEngine:
         ws = self.ws["train"]
         h = self.trunk(storage.obs, idx, B, ws)
         dh = ws.get("dh", B * self.H, device=self.device)
-        self._heads_train(storage, adv, idx, h, B, hp, loss_acc, dh, feat_relu=True)
+        self._heads_train(storage, adv, idx, h, B, hp, loss_acc, dh, feat_act=1)
         self._trunk_backward(B, dh, storage.obs, idx)
         self._finish_step(optimizer)
 
@@ -312,8 +319,8 @@ class RecurrentEngine(CNNEngine):
             call("ppo_concat_cols", src.data_ptr(), ptr(rows_vec), B, self.V if vec is not None else 0,
                  x.data_ptr(), Ip, H, Ip - H, s)
         gi = ws.get("gi", B * 3 * H, device=dev)
-        call("ppo_linear_fwd_ex", x.data_ptr(), B, Ip, Ip, self.wih_pad, self.pv(self.GBI), 3 * H, gi.data_ptr(),
-             3 * H, 0, s)
+        call("ppo_linear_fwd_ex", x.data_ptr(), None, B, Ip, Ip, self.wih_pad, self.pv(self.GBI), 3 * H,
+             gi.data_ptr(), 3 * H, 0, s)
         return x, gi
 
     def _vec(self, vec, B):
@@ -387,7 +394,7 @@ class RecurrentEngine(CNNEngine):
                  sv["z"].data_ptr() + o, sv["n"].data_ptr() + o, sv["ghn"].data_ptr() + o, sv["hin"].data_ptr() + o,
                  s)
         dout = ws.get("dout", R * H, device=dev)
-        self._heads_train(storage, adv, idx, hout, R, hp, loss_acc, dout, feat_relu=False)
+        self._heads_train(storage, adv, idx, hout, R, hp, loss_acc, dout, feat_act=0)
         # backward through time
         dgi = ws.get("dgi", R * 3 * H, device=dev)
         dgh = ws.get("dgh", R * 3 * H, device=dev)
@@ -404,6 +411,109 @@ class RecurrentEngine(CNNEngine):
         self._dense_wgrad(dgh, sv["hin"], R, 3 * H, H, 0, 0, self.GHH, self.GBH)
         self._dense_wgrad(dgi, x, R, 3 * H, self.Ip, 3, self.I, self.GIH, self.GBI)
         dh = ws.get("dh", R * H, device=dev)
-        call("ppo_linear_dgrad_ex", dgi.data_ptr(), R, 3 * H, self.wihT, H, x.data_ptr(), self.Ip, dh.data_ptr(), s)
+        call("ppo_linear_dgrad_ex", dgi.data_ptr(), R, 3 * H, self.wihT, H, x.data_ptr(), self.Ip, 1, dh.data_ptr(),
+             s)
         self._trunk_backward(R, dh, storage.obs, idx)
+        self._finish_step(optimizer)
+
+
+class MLPEngine(CNNEngine):
+    """MLPBase (model.py:202-234): actor / critic towers Linear-tanh-Linear-tanh on
+    x = cat(obs, vector_obs); value from the critic tower, logits from the actor's.
+    Parameter order: actor.0, actor.2, critic.0, critic.2, critic_linear, dist."""
+
+    AW1, AB1, AW2, AB2, CW1, CB1, CW2, CB2, WC, BC, WA, BA = range(12)
+
+    def __init__(self, policy, device):   # noqa: D401 — own init, shares the CNNEngine machinery
+        base = policy.base
+        if base.is_recurrent:
+            raise NotImplementedError("recurrent MLPBase is not on the HIP path")
+        self.policy, self.device = policy, device
+        self.H = base._hidden_size
+        self.I = base.actor[0].weight.shape[1]
+        self.V = base.vector_obs_len
+        self.obs_dim = self.I - self.V
+        self.Ip = (self.I + 3) // 4 * 4
+        self.A = policy.dist.linear.weight.shape[0]
+        if self.H % 4 != 0 or self.H > 512:
+            raise NotImplementedError(f"MLPBase hidden_size {self.H}: multiples of 4 up to 512")
+        self.params = list(policy.parameters())
+        self.ws = {"act": _Workspace(), "train": _Workspace()}
+        self.packed = None
+        self._pack_key = None
+        self.epoch = 0
+        self._flatten()
+        self.rng_seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFFFFFF
+        self.rng_counter = 0
+
+    def pack(self, force=False):
+        key = (sum(p._version for p in self.params), self.epoch)
+        if not force and self.packed is not None and key == self._pack_key:
+            return
+        H, Ip, s = self.H, self.Ip, stream()
+        if self.packed is None:
+            self.packed = torch.empty(2 * H * Ip + 2 * H * H, device=self.device)
+        b = self.packed.data_ptr()
+        self.aw1, self.cw1 = b, b + 4 * H * Ip
+        self.aw2T, self.cw2T = b + 8 * H * Ip, b + 8 * H * Ip + 4 * H * H
+        for w, dst in ((self.AW1, self.aw1), (self.CW1, self.cw1)):   # first layers padded to Ip inputs
+            call("ppo_concat_cols", self.pv(w), None, H, self.I, dst, Ip, 0, Ip, s)
+        call("ppo_transpose", self.pv(self.AW2), H, H, self.aw2T, s)
+        call("ppo_transpose", self.pv(self.CW2), H, H, self.cw2T, s)
+        self._pack_key = key
+
+    def _x(self, obs, vec, idx, B, ws):
+        """x_pad [B][Ip] = (obs | vector obs | 0)"""
+        dev, s = self.device, stream()
+        x = ws.get("x", B * self.Ip, device=dev)
+        call("ppo_concat_cols", obs.data_ptr(), ptr(idx), B, self.obs_dim, x.data_ptr(), self.Ip, 0,
+             self.obs_dim if self.V else self.Ip, s)
+        if self.V:
+            call("ppo_concat_cols", vec.data_ptr(), ptr(idx), B, self.V, x.data_ptr(), self.Ip, self.obs_dim,
+                 self.Ip - self.obs_dim, s)
+        return x
+
+    def towers(self, x, B, ws):
+        dev, H, Ip, s = self.device, self.H, self.Ip, stream()
+        out = {}
+        for name, w1, b1, w2, b2 in (("a", self.aw1, self.AB1, self.AW2, self.AB2),
+                                     ("c", self.cw1, self.CB1, self.CW2, self.CB2)):
+            h1 = ws.get(name + "1", B * H, device=dev)
+            h2 = ws.get(name + "2", B * H, device=dev)
+            call("ppo_linear_fwd_ex", x.data_ptr(), None, B, Ip, Ip, w1, self.pv(b1), H, h1.data_ptr(), H, 2, s)
+            call("ppo_linear_fwd_ex", h1.data_ptr(), None, B, H, H, self.pv(w2), self.pv(b2), H, h2.data_ptr(), H, 2, s)
+            out[name] = (h1, h2)
+        return out
+
+    def act(self, obs, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False, vec=None):
+        self.ensure_bound()
+        self.pack()
+        obs = (obs if obs.is_cuda else obs.to(self.device)).to(torch.float32).reshape(obs.shape[0], -1).contiguous()
+        B = obs.shape[0]
+        if obs.shape[1] != self.obs_dim:
+            raise RuntimeError(f"MLPBase expects [N,{self.obs_dim}] observations, got {tuple(obs.shape)}")
+        ws = self.ws["act"]
+        v = vec.to(self.device, torch.float32).reshape(B, self.V).contiguous() if self.V else None
+        x = self._x(obs, v, None, B, ws)
+        t = self.towers(x, B, ws)
+        return self._heads(t["a"][1], B, deterministic, noise, given, want_entropy, value_only, hv=t["c"][1])
+
+    def train_minibatch(self, storage, adv, idx, hp, loss_acc, optimizer):
+        self.ensure_bound()
+        self.pack()
+        dev, H, B = self.device, self.H, idx.numel()
+        ws = self.ws["train"]
+        x = self._x(storage.obs, storage.vector_obs if self.V else None, idx, B, ws)
+        t = self.towers(x, B, ws)
+        da2 = ws.get("da2", B * H, device=dev)
+        dc2 = ws.get("dc2", B * H, device=dev)
+        self._heads_train(storage, adv, idx, t["a"][1], B, hp, loss_acc, da2, feat_act=2, feat_v=t["c"][1],
+                          dfeat_v=dc2)
+        for name, d2, w1, b1, w2, b2, w2T in (("a", da2, self.AW1, self.AB1, self.AW2, self.AB2, self.aw2T),
+                                               ("c", dc2, self.CW1, self.CB1, self.CW2, self.CB2, self.cw2T)):
+            h1 = t[name][0]
+            self._dense_wgrad(d2, h1, B, H, H, 0, 0, w2, b2)
+            d1 = ws.get("d1" + name, B * H, device=dev)
+            call("ppo_linear_dgrad_ex", d2.data_ptr(), B, H, w2T, H, h1.data_ptr(), H, 2, d1.data_ptr(), stream())
+            self._dense_wgrad(d1, x, B, H, self.Ip, 3, self.I, w1, b1)
         self._finish_step(optimizer)

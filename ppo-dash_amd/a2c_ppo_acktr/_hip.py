@@ -35,6 +35,7 @@ SIGNATURES = {
     "ppo_gather_rows": [c_p, c_p, c_p, c_ll, c_ll, c_p],
     "ppo_gather_env_columns": [c_p, c_p, c_p, c_int, c_int, c_int, c_ll, c_p],
     "ppo_synth_env_step": [c_p, c_int, c_ll, c_p, c_p, c_p, c_ull, c_ull, c_f, c_p],
+    "ppo_cartpole_step": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_ull, c_ull, c_int, c_p],
     # gemm.hip
     "ppo_packed_weights_size": [c_int],
     "ppo_packed_offsets": [c_int, c_p],
@@ -55,13 +56,14 @@ SIGNATURES = {
     "ppo_colsum": [c_p, c_ll, c_int, c_ll, c_p, c_f, c_int, c_p],
     "ppo_tune_set": [ctypes.c_char_p, c_int],
     # heads.hip
-    "ppo_heads_act": [c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_ull, c_ull, c_int, c_p, c_p, c_p, c_p,
-                      c_p, c_p],
+    "ppo_heads_act": [c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_ull, c_ull, c_int, c_p, c_p, c_p,
+                      c_p, c_p, c_p],
     "ppo_heads_train_blocks": [c_int],
-    "ppo_heads_train": [c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_ll, c_p, c_p, c_p, c_p, c_p, c_f, c_f,
-                        c_f, c_f, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
-    "ppo_linear_fwd_ex": [c_p, c_int, c_int, c_int, c_p, c_p, c_int, c_p, c_int, c_int, c_p],
-    "ppo_linear_dgrad_ex": [c_p, c_int, c_int, c_p, c_int, c_p, c_int, c_p, c_p],
+    "ppo_heads_train": [c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_ll, c_p, c_p, c_p, c_p, c_p, c_f,
+                        c_f, c_f, c_f, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p],
+    "ppo_linear_fwd_ex": [c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_int, c_p, c_int, c_int, c_p],
+    "ppo_linear_dgrad_ex": [c_p, c_int, c_int, c_p, c_int, c_p, c_int, c_int, c_p, c_p],
+    "ppo_transpose": [c_p, c_int, c_int, c_p, c_p],
     "ppo_gru_step_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "ppo_gru_cell_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p],
     "ppo_gru_step_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p],

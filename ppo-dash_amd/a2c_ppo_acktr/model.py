@@ -13,7 +13,8 @@ Differences from the reference, all documented in DESIGN.md:
     Policy can build it (the reference mis-calls it, model.py:28 vs :203).
   * evaluate_actions returns values without an autograd graph; PPO.update runs
     its own fused HIP backward.
-  * MLPBase's forward pass is not on the HIP path yet.
+  * MLPBase's forward uses cat(obs, vector_obs) as its input (the reference
+    builds a tuple there, model.py:225-226).
 """
 import numpy as np
 import torch
@@ -88,19 +89,19 @@ class Policy(nn.Module):
 
     def hip_engine(self, device=None):
         require_device()
-        if not isinstance(self.base, CNNBase):
-            raise NotImplementedError("the MI355X engine runs CNNBase policies (feed-forward or GRU); "
-                                      "MLPBase is on the roadmap (DESIGN.md)")
         if not isinstance(self.dist, Categorical):
             raise NotImplementedError("only Discrete action spaces run on the MI355X engine")
         if device is None:
             p = next(self.parameters())
             device = p.device if p.is_cuda else torch.device("cuda", torch.cuda.current_device())
         if self._engine is None or self._engine.device != device:
-            from ._engine import CNNEngine, RecurrentEngine
+            from ._engine import CNNEngine, MLPEngine, RecurrentEngine
             if not next(self.parameters()).is_cuda:
                 self.to(device)
-            self._engine = (RecurrentEngine if self.base.is_recurrent else CNNEngine)(self, device)
+            if isinstance(self.base, MLPBase):
+                self._engine = MLPEngine(self, device)
+            else:
+                self._engine = (RecurrentEngine if self.base.is_recurrent else CNNEngine)(self, device)
         self._engine.ensure_bound()
         return self._engine
 
@@ -119,6 +120,10 @@ class Policy(nn.Module):
             value, action, logp, _, rnn_hxs = eng.act(visual_inputs, deterministic=deterministic, noise=noise,
                                                       vec=vector_inputs, hxs=rnn_hxs, masks=masks)
             return value, action, logp, rnn_hxs
+        if isinstance(self.base, MLPBase):
+            value, action, logp, _ = eng.act(visual_inputs, deterministic=deterministic, noise=noise,
+                                             vec=vector_inputs)
+            return value, action, logp, rnn_hxs
         value, action, logp, _ = eng.act(visual_inputs, deterministic=deterministic, noise=noise)
         return value, action, logp, rnn_hxs
 
@@ -127,6 +132,8 @@ class Policy(nn.Module):
         eng = self.hip_engine()
         if self.is_recurrent:
             return eng.act(visual_inputs, value_only=True, vec=vector_inputs, hxs=rnn_hxs, masks=masks)[0]
+        if isinstance(self.base, MLPBase):
+            return eng.act(visual_inputs, value_only=True, vec=vector_inputs)[0]
         value, _, _, _ = eng.act(visual_inputs, value_only=True)
         return value
 
@@ -141,9 +148,12 @@ class Policy(nn.Module):
             else:                                             # model.py:116-165 sequence branch
                 value, logp, ent, rnn_hxs = eng.evaluate_sequence(visual_inputs, vector_inputs, rnn_hxs, masks,
                                                                   action)
-            return value, logp, ent.mean(), rnn_hxs
-        value, _, logp, ent = eng.act(visual_inputs, given=action, want_entropy=True)
-        return value, logp, ent.mean(), rnn_hxs
+            return value, logp, eng.mean(ent), rnn_hxs
+        if isinstance(self.base, MLPBase):
+            value, _, logp, ent = eng.act(visual_inputs, given=action, want_entropy=True, vec=vector_inputs)
+        else:
+            value, _, logp, ent = eng.act(visual_inputs, given=action, want_entropy=True)
+        return value, logp, eng.mean(ent), rnn_hxs
 
 
 class NNBase(nn.Module):
@@ -206,6 +216,7 @@ class MLPBase(NNBase):
         num_inputs = num_inputs + vector_obs_len
         if recurrent:
             num_inputs = hidden_size
+        self.vector_obs_len = vector_obs_len
         init_ = lambda m: init(m, nn.init.orthogonal_, lambda x: nn.init.constant_(x, 0), np.sqrt(2))
         self.actor = nn.Sequential(
             init_(nn.Linear(num_inputs, hidden_size)), nn.Tanh(),
@@ -217,4 +228,4 @@ class MLPBase(NNBase):
         self.train()
 
     def forward(self, visual_inputs, vector_inputs, rnn_hxs, masks):
-        raise NotImplementedError("MLPBase is not on the HIP path yet (DESIGN.md roadmap)")
+        raise NotImplementedError("MLPBase runs through Policy.act/get_value/evaluate_actions on the HIP engine")

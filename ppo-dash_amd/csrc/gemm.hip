@@ -367,27 +367,50 @@ PPO_API int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, co
   return launch(p, M, N, 1, as_stream(stream), "linear_relu_fwd", 2.0 * M * N * K);
 }
 
-// Linear with row strides: out[m*ldo + n] = act(x[m*lda + k] · w[n][k] + b[n]); b may be NULL
-PPO_API int ppo_linear_fwd_ex(const float* x, int M, int K, int lda, const float* w, const float* b, int N, float* out,
-                              int ldo, int relu, void* stream) {
+// Linear with row strides: out[m*ldo + n] = act(x[idx(m)*lda + k] · w[n][k] + b[n]); b, idx may be NULL;
+// act 0 none, 1 ReLU, 2 tanh
+PPO_API int ppo_linear_fwd_ex(const float* x, const int64_t* idx, int M, int K, int lda, const float* w, const float* b,
+                              int N, float* out, int ldo, int act, void* stream) {
   PPO_REQUIRE(K % 4 == 0 && lda % 4 == 0, "ppo_linear_fwd_ex: K=%d lda=%d must be multiples of 4", K, lda);
+  PPO_REQUIRE(act >= 0 && act <= 2, "ppo_linear_fwd_ex: act=%d", act);
   if (N % 128 == 0) {
     DenseReluFwd<CfgN128> p;
-    p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = relu;
+    p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = act;
+    p.idx = idx;
     return launch(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);
   }
   DenseReluFwd<CfgN64> p;
-  p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = relu;
+  p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = act;
+  p.idx = idx;
   return launch(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);
 }
 
-// dx [M][N] = (act > 0) * (dy [M][K] · wt [N][K]^T); act row stride ldact (act NULL: no mask)
+// dx [M][N] = g(act) * (dy [M][K] · wt [N][K]^T); act row stride ldact (act NULL: no mask);
+// mode 1: g = [act > 0] (ReLU), 2: g = 1 - act² (tanh)
 PPO_API int ppo_linear_dgrad_ex(const float* dy, int M, int K, const float* wt, int N, const float* act, int ldact,
-                                float* dx, void* stream) {
+                                int mode, float* dx, void* stream) {
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_dgrad_ex: K=%d must be a multiple of 4", K);
   DenseDgradMask<CfgN128> p;
-  p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K; p.ldact = ldact;
+  p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K; p.ldact = ldact; p.mode = mode;
   return launch(p, M, N, 1, as_stream(stream), "linear_dgrad_ex", 2.0 * M * N * K);
+}
+
+__global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ src, int rows, int cols,
+                                                        float* __restrict__ dst) {
+  const long long total = (long long)rows * cols;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int c = (int)(i / rows), r = (int)(i - (long long)c * rows);
+    dst[i] = src[(size_t)r * cols + c];
+  }
+}
+
+// dst [cols][rows] = src [rows][cols]ᵀ (weight transposes for dgrad B operands)
+PPO_API int ppo_transpose(const float* src, int rows, int cols, float* dst, void* stream) {
+  PPO_REQUIRE(rows > 0 && cols > 0, "ppo_transpose: %d x %d", rows, cols);
+  long long b = ((long long)rows * cols + 255) / 256;
+  transpose_kernel<<<(unsigned)(b < 2048 ? b : 2048), 256, 0, as_stream(stream)>>>(src, rows, cols, dst);
+  PPO_LAUNCH_CHECK("transpose_kernel");
+  return 0;
 }
 
 // dx [M][N] = (act > 0) * (dy [M][K] · wt [N][K]^T)

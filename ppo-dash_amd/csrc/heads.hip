@@ -42,13 +42,14 @@ __device__ __forceinline__ void load_head_w(HeadW<HC, AMAX>& w, const float* __r
     for (int c = 0; c < HC; ++c) w.wa[o][c] = (o < A && lane + 64 * c < H) ? wa[o * H + lane + 64 * c] : 0.f;
 }
 
-// value and logits of one row (all lanes end up with the totals)
+// value (from fv) and logits (from f) of one row; all lanes end up with the totals
 template <int HC, int AMAX>
-__device__ __forceinline__ void head_dots(const HeadW<HC, AMAX>& w, const float (&f)[HC], float& value,
-                                          float (&z)[AMAX], float bc, const float* __restrict__ ba, int A) {
+__device__ __forceinline__ void head_dots(const HeadW<HC, AMAX>& w, const float (&f)[HC], const float (&fv)[HC],
+                                          float& value, float (&z)[AMAX], float bc, const float* __restrict__ ba,
+                                          int A) {
   float v = 0.f;
 #pragma unroll
-  for (int c = 0; c < HC; ++c) v += f[c] * w.wc[c];
+  for (int c = 0; c < HC; ++c) v += fv[c] * w.wc[c];
   value = wave_sum(v) + bc;
 #pragma unroll
   for (int o = 0; o < AMAX; ++o) {
@@ -99,8 +100,9 @@ __device__ __forceinline__ float exp_noise(uint64_t seed, uint64_t counter, long
 // act / evaluate: value, action (sample | mode | given), log_prob, entropy
 template <int HC, int AMAX>
 __global__ __launch_bounds__(64 * HW) void heads_act_kernel(
-    const float* __restrict__ feat, int N, int H, const float* __restrict__ wc, const float* __restrict__ bc,
-    const float* __restrict__ wa, const float* __restrict__ ba, int A, const float* __restrict__ noise,
+    const float* __restrict__ feat, const float* __restrict__ feat_v, int N, int H, const float* __restrict__ wc,
+    const float* __restrict__ bc, const float* __restrict__ wa, const float* __restrict__ ba, int A,
+    const float* __restrict__ noise,
     unsigned long long seed, unsigned long long counter, int deterministic, const int64_t* __restrict__ given,
     float* __restrict__ value_out, int64_t* __restrict__ action_out, float* __restrict__ logp_out,
     float* __restrict__ ent_out, int rows_per_wave) {
@@ -112,11 +114,15 @@ __global__ __launch_bounds__(64 * HW) void heads_act_kernel(
   for (int rr = 0; rr < rows_per_wave; ++rr) {
     const long long row = r0 + rr;
     if (row >= N) break;
-    float f[HC];
+    float f[HC], fv[HC];
 #pragma unroll
-    for (int c = 0; c < HC; ++c) f[c] = lane + 64 * c < H ? feat[row * H + lane + 64 * c] : 0.f;
+    for (int c = 0; c < HC; ++c) {
+      const bool in = lane + 64 * c < H;
+      f[c] = in ? feat[row * H + lane + 64 * c] : 0.f;
+      fv[c] = feat_v ? (in ? feat_v[row * H + lane + 64 * c] : 0.f) : f[c];
+    }
     float value, z[AMAX], nl[AMAX], p[AMAX];
-    head_dots(w, f, value, z, b0, ba, A);
+    head_dots(w, f, fv, value, z, b0, ba, A);
     categorical(z, A, nl, p);
     int act;
     if (given) {
@@ -147,8 +153,16 @@ __global__ __launch_bounds__(64 * HW) void heads_act_kernel(
   }
 }
 
+// d(pre-activation) from d(output) for the activation that produced y
+__device__ __forceinline__ float act_grad(float d, float y, int act) {
+  if (act == 1) return y > 0.f ? d : 0.f;     // ReLU (threshold_backward)
+  if (act == 2) return d * (1.0f - y * y);    // tanh
+  return d;
+}
+
 struct TrainArgs {
-  const float* feat;  // [B][H] post-ReLU fc output
+  const float* feat;  // [B][H] policy features (CNNBase: post-ReLU fc; MLPBase: actor tanh output)
+  const float* feat_v;  // [B][H] critic features (MLPBase) or NULL (= feat)
   int B, H, A;
   const float *wc, *bc, *wa, *ba;
   const int64_t* idx;      // storage row of each sample (nullable: row0 + b)
@@ -157,8 +171,9 @@ struct TrainArgs {
   const float *old_logp, *adv, *vpred, *ret;
   float clip, value_coef, entropy_coef, inv_b;
   int use_clipped_value_loss;
-  int feat_relu;           // features are a ReLU output (CNNBase fc): mask dfeat by f > 0
-  float* dfeat;            // [B][H] dL/d(feature pre-activation)
+  int feat_act;            // activation producing the features: 0 none (GRU), 1 ReLU, 2 tanh
+  float* dfeat;            // [B][H] dL/d(feature pre-activation) (both heads when dfeat_v is NULL)
+  float* dfeat_v;          // [B][H] critic-branch gradient (MLPBase) or NULL
   float* part_w;           // [blocks][1+A][H]
   float* part_b;           // [blocks][1+A]
   float* part_loss;        // [blocks][3]: Σ max(l1,l2), Σ min(s1,s2), Σ H
@@ -187,11 +202,15 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
   for (int rr = 0; rr < a.rows_per_wave; ++rr) {
     const long long row = r0 + rr;
     if (row >= a.B) break;
-    float f[HC];
+    float f[HC], fv[HC];
 #pragma unroll
-    for (int c = 0; c < HC; ++c) f[c] = lane + 64 * c < H ? a.feat[row * H + lane + 64 * c] : 0.f;
+    for (int c = 0; c < HC; ++c) {
+      const bool in = lane + 64 * c < H;
+      f[c] = in ? a.feat[row * H + lane + 64 * c] : 0.f;
+      fv[c] = a.feat_v ? (in ? a.feat_v[row * H + lane + 64 * c] : 0.f) : f[c];
+    }
     float value, z[AMAX], nl[AMAX], p[AMAX];
-    head_dots(w, f, value, z, b0, a.ba, A);
+    head_dots(w, f, fv, value, z, b0, a.ba, A);
     categorical(z, A, nl, p);
     const long long sr = a.idx ? (long long)a.idx[row] : a.row0 + row;
     const int act = (int)a.actions[sr];
@@ -238,11 +257,16 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
     // dL/dh for this lane's columns, masked by the fc ReLU; head grads
 #pragma unroll
     for (int c = 0; c < HC; ++c) {
-      float d = g_v * w.wc[c];
+      const float dv = g_v * w.wc[c];
+      float d = a.dfeat_v ? 0.f : dv;
 #pragma unroll
       for (int o = 0; o < AMAX; ++o) d += gz[o] * w.wa[o][c];
-      if (lane + 64 * c < H) a.dfeat[row * H + lane + 64 * c] = (!a.feat_relu || f[c] > 0.f) ? d : 0.f;
-      gwc[c] += g_v * f[c];
+      if (lane + 64 * c < H) {
+        const size_t q = (size_t)row * H + lane + 64 * c;
+        a.dfeat[q] = act_grad(d, f[c], a.feat_act);
+        if (a.dfeat_v) a.dfeat_v[q] = act_grad(dv, fv[c], a.feat_act);
+      }
+      gwc[c] += g_v * fv[c];
 #pragma unroll
       for (int o = 0; o < AMAX; ++o) gwa[o][c] += gz[o] * f[c];
     }
@@ -342,26 +366,29 @@ static inline int hc_of(int H) {
 }
 
 template <int HC, int AMAX>
-int launch_act(const float* feat, int N, int H, const float* wc, const float* bc, const float* wa, const float* ba,
+int launch_act(const float* feat, const float* feat_v, int N, int H, const float* wc, const float* bc, const float* wa,
+               const float* ba,
                int A, const float* noise, unsigned long long seed, unsigned long long counter, int det,
                const int64_t* given, float* v, int64_t* act, float* lp, float* ent, hipStream_t st) {
   const int rpw = 8;
   const unsigned blocks = ceil_div(N, HW * rpw);
-  heads_act_kernel<HC, AMAX><<<blocks, 64 * HW, 0, st>>>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det,
+  heads_act_kernel<HC, AMAX><<<blocks, 64 * HW, 0, st>>>(feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter,
+                                                        det,
                                                         given, v, act, lp, ent, rpw);
   PPO_LAUNCH_CHECK("heads_act_kernel");
   return 0;
 }
 
 template <int AMAX>
-int dispatch_act(int HC, const float* feat, int N, int H, const float* wc, const float* bc, const float* wa,
+int dispatch_act(int HC, const float* feat, const float* feat_v, int N, int H, const float* wc, const float* bc,
+                 const float* wa,
                  const float* ba, int A, const float* noise, unsigned long long seed, unsigned long long counter,
                  int det, const int64_t* given, float* v, int64_t* act, float* lp, float* ent, hipStream_t st) {
   switch (HC) {
-    case 1: return launch_act<1, AMAX>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
-    case 2: return launch_act<2, AMAX>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
-    case 4: return launch_act<4, AMAX>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
-    case 8: return launch_act<8, AMAX>(feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
+    case 1: return launch_act<1, AMAX>(feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
+    case 2: return launch_act<2, AMAX>(feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
+    case 4: return launch_act<4, AMAX>(feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
+    case 8: return launch_act<8, AMAX>(feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter, det, given, v, act, lp, ent, st);
   }
   ppo_set_error("heads: hidden size %d not supported (<= 512)", H);
   return PPO_EARG;
@@ -393,7 +420,8 @@ int dispatch_train(int HC, const TrainArgs& a, int blocks, hipStream_t st) {
 //   noise   == NULL: Exp(1) noise from the counter RNG (seed, counter, row)
 //   given   != NULL: log_prob/entropy of the given actions (evaluate_actions)
 //   deterministic: mode = argmax(probs)
-PPO_API int ppo_heads_act(const float* feat, int N, int H, const float* wc, const float* bc, const float* wa,
+PPO_API int ppo_heads_act(const float* feat, const float* feat_v, int N, int H, const float* wc, const float* bc,
+                          const float* wa,
                           const float* ba, int A, const float* noise, unsigned long long seed,
                           unsigned long long counter, int deterministic, const int64_t* given, float* value,
                           int64_t* action, float* logp, float* entropy, void* stream) {
@@ -403,9 +431,9 @@ PPO_API int ppo_heads_act(const float* feat, int N, int H, const float* wc, cons
   hipStream_t st = as_stream(stream);
   const int HC = hc_of(H);
   if (A <= 8)
-    return dispatch_act<8>(HC, feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
+    return dispatch_act<8>(HC, feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
                            action, logp, entropy, st);
-  return dispatch_act<16>(HC, feat, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
+  return dispatch_act<16>(HC, feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
                           action, logp, entropy, st);
 }
 
@@ -414,19 +442,22 @@ PPO_API int ppo_heads_train_blocks(int B) {
   return (int)ceil_div(B, HW * rpw);
 }
 
-PPO_API int ppo_heads_train(const float* feat, int B, int H, const float* wc, const float* bc, const float* wa,
+PPO_API int ppo_heads_train(const float* feat, const float* feat_v, int B, int H, const float* wc, const float* bc,
+                            const float* wa,
                             const float* ba, int A, const int64_t* idx, long long row0, const int64_t* actions,
                             const float* old_logp, const float* adv, const float* vpred, const float* ret, float clip,
                             float value_coef, float entropy_coef, float inv_b, int use_clipped_value_loss,
-                            int feat_relu, float* dfeat, float* part_w, float* part_b, float* part_loss, void* stream) {
+                            int feat_act, float* dfeat, float* dfeat_v, float* part_w, float* part_b,
+                            float* part_loss, void* stream) {
   PPO_REQUIRE(B > 0 && A >= 1 && A <= 16, "ppo_heads_train: B=%d A=%d", B, A);
   PPO_REQUIRE(H > 0 && H <= 512, "ppo_heads_train: hidden size %d (1..512)", H);
   TrainArgs a;
-  a.feat = feat; a.B = B; a.H = H; a.A = A; a.wc = wc; a.bc = bc; a.wa = wa; a.ba = ba;
+  a.feat = feat; a.feat_v = feat_v; a.B = B; a.H = H; a.A = A; a.wc = wc; a.bc = bc; a.wa = wa; a.ba = ba;
   a.idx = idx; a.row0 = row0; a.actions = actions; a.old_logp = old_logp; a.adv = adv; a.vpred = vpred; a.ret = ret;
   a.clip = clip; a.value_coef = value_coef; a.entropy_coef = entropy_coef; a.inv_b = inv_b;
   a.use_clipped_value_loss = use_clipped_value_loss;
-  a.feat_relu = feat_relu;
+  a.feat_act = feat_act;
+  a.dfeat_v = dfeat_v;
   a.dfeat = dfeat; a.part_w = part_w; a.part_b = part_b; a.part_loss = part_loss;
   a.rows_per_wave = 32;
   const int blocks = ppo_heads_train_blocks(B);

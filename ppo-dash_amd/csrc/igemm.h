@@ -236,10 +236,14 @@ __device__ __forceinline__ long long obs_row(const int64_t* idx, long long row0,
 template <class C_>
 struct DenseReluFwd : C_ {
   const float* x; const float* w; const float* bias; float* out; int M, N, K;
-  int lda = 0, ldo = 0, relu = 1;   // row strides (0: K / N); relu 0: plain Linear (+bias)
+  int lda = 0, ldo = 0, relu = 1;   // row strides (0: K / N); activation 0 none, 1 ReLU, 2 tanh
+  const int64_t* idx = nullptr;      // A-row gather (row idx[m] of x)
   using ACtx = typename C_::ACtx;
   using BCtx = typename C_::BCtx;
-  __device__ ACtx a_ctx(int m, int) const { return {x + (size_t)m * (lda ? lda : K), 0, 0, m < M}; }
+  __device__ ACtx a_ctx(int m, int) const {
+    if (m >= M) return {x, 0, 0, false};
+    return {x + (size_t)(idx ? idx[m] : m) * (lda ? lda : K), 0, 0, true};
+  }
   __device__ f32x4 a_load(const ACtx& c, int k) const {
     return (c.ok && k < K) ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
   }
@@ -251,7 +255,7 @@ struct DenseReluFwd : C_ {
   __device__ void store(int m, int n, int, float v) const {
     if (m < M && n < N) {
       float y = bias ? v + bias[n] : v;
-      out[(size_t)m * (ldo ? ldo : N) + n] = relu ? fmaxf(y, 0.f) : y;
+      out[(size_t)m * (ldo ? ldo : N) + n] = relu == 1 ? fmaxf(y, 0.f) : (relu == 2 ? tanhf(y) : y);
     }
   }
 };
@@ -260,7 +264,8 @@ struct DenseReluFwd : C_ {
 template <class C_>
 struct DenseDgradMask : C_ {
   const float* dy; const float* wt; const float* act; float* dx; int M, N, K;
-  int ldact = 0;   // act row stride (0: N); act NULL: no ReLU mask
+  int ldact = 0;   // act row stride (0: N); act NULL: no mask
+  int mode = 1;    // 1: ReLU mask (act > 0), 2: tanh derivative (1 - act²)
   using ACtx = typename C_::ACtx;
   using BCtx = typename C_::BCtx;
   __device__ ACtx a_ctx(int m, int) const { return {dy + (size_t)m * K, 0, 0, m < M}; }
@@ -275,7 +280,12 @@ struct DenseDgradMask : C_ {
   __device__ void store(int m, int n, int, float v) const {
     if (m < M && n < N) {
       const size_t i = (size_t)m * N + n;
-      dx[i] = (!act || act[(size_t)m * (ldact ? ldact : N) + n] > 0.f) ? v : 0.f;
+      if (!act) {
+        dx[i] = v;
+      } else {
+        const float y = act[(size_t)m * (ldact ? ldact : N) + n];
+        dx[i] = mode == 2 ? v * (1.0f - y * y) : (y > 0.f ? v : 0.f);
+      }
     }
   }
 };

@@ -171,6 +171,57 @@ __global__ __launch_bounds__(256) void synth_env_kernel(uint8_t* __restrict__ ob
   }
 }
 
+// CartPole-v1 (gym's classic-control cart-pole, the c1 config's env; gym is not
+// a dependency here, its published dynamics are restated): Euler integration at
+// tau = 0.02, force ±10 N, termination at |x| > 2.4 or |θ| > 12°, reward 1 per
+// step, TimeLimit 500 -> bad_transition (bad_mask 0), reset U(-0.05, 0.05)^4
+// from the counter RNG, auto-reset as baselines' VecEnv does.  fp32 state
+// (gym keeps float64 and returns float32 observations).
+__global__ __launch_bounds__(256) void cartpole_kernel(float* __restrict__ state, int* __restrict__ steps,
+                                                       const int64_t* __restrict__ action, float* __restrict__ obs,
+                                                       float* __restrict__ reward, float* __restrict__ mask,
+                                                       float* __restrict__ bad_mask, float* __restrict__ ep_len,
+                                                       int N, uint64_t seed, uint64_t counter, int max_steps) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float* st = state + 4 * (size_t)n;
+  bool reset = action == nullptr;
+  float ended = 0.f;
+  if (!reset) {
+    const float gravity = 9.8f, masscart = 1.0f, masspole = 0.1f, total_mass = masspole + masscart;
+    const float length = 0.5f, polemass_length = masspole * length, force_mag = 10.0f, tau = 0.02f;
+    const float theta_thr = 12.0f * 2.0f * 3.14159265358979f / 360.0f, x_thr = 2.4f;
+    float x = st[0], x_dot = st[1], theta = st[2], theta_dot = st[3];
+    const float force = action[n] == 1 ? force_mag : -force_mag;
+    const float ct = cosf(theta), sn = sinf(theta);
+    const float temp = (force + polemass_length * theta_dot * theta_dot * sn) / total_mass;
+    const float thetaacc = (gravity * sn - ct * temp) / (length * (4.0f / 3.0f - masspole * ct * ct / total_mass));
+    const float xacc = temp - polemass_length * thetaacc * ct / total_mass;
+    x = x + tau * x_dot;
+    x_dot = x_dot + tau * xacc;
+    theta = theta + tau * theta_dot;
+    theta_dot = theta_dot + tau * thetaacc;
+    st[0] = x; st[1] = x_dot; st[2] = theta; st[3] = theta_dot;
+    const int k = ++steps[n];
+    const bool done = x < -x_thr || x > x_thr || theta < -theta_thr || theta > theta_thr;
+    const bool trunc = !done && k >= max_steps;
+    if (reward) reward[n] = 1.0f;
+    if (mask) mask[n] = (done || trunc) ? 0.0f : 1.0f;
+    if (bad_mask) bad_mask[n] = trunc ? 0.0f : 1.0f;
+    if (done || trunc) {
+      ended = (float)k;
+      reset = true;
+    }
+  }
+  if (reset) {
+    const uint64_t key = seed ^ mix64(counter * 0x100000001B3ull + (uint64_t)n * 0x9E3779B1ull + 0xCA27ull);
+    for (int i = 0; i < 4; ++i) st[i] = (u01_open0(mix64(key + i)) - 0.5f) * 0.1f;
+    steps[n] = 0;
+  }
+  if (ep_len) ep_len[n] = ended;
+  for (int i = 0; i < 4; ++i) obs[4 * (size_t)n + i] = st[i];
+}
+
 __global__ __launch_bounds__(256) void fill_f32_kernel(float* __restrict__ p, long long n, float v) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) p[i] = v;
 }
@@ -253,5 +304,15 @@ PPO_API int ppo_synth_env_step(uint8_t* obs, int N, long long obs_bytes, float* 
   synth_env_kernel<<<(unsigned)b, 256, 0, as_stream(stream)>>>(obs, N, obs_bytes, reward, mask, bad_mask, seed, step,
                                                                p_done);
   PPO_LAUNCH_CHECK("synth_env_kernel");
+  return 0;
+}
+
+PPO_API int ppo_cartpole_step(float* state, int* steps, const int64_t* action, float* obs, float* reward, float* mask,
+                              float* bad_mask, float* ep_len, int N, unsigned long long seed,
+                              unsigned long long counter, int max_steps, void* stream) {
+  PPO_REQUIRE(N > 0 && max_steps > 0, "ppo_cartpole_step: N=%d max_steps=%d", N, max_steps);
+  cartpole_kernel<<<ceil_div(N, 256), 256, 0, as_stream(stream)>>>(state, steps, action, obs, reward, mask, bad_mask,
+                                                                   ep_len, N, seed, counter, max_steps);
+  PPO_LAUNCH_CHECK("cartpole_kernel");
   return 0;
 }

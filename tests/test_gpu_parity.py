@@ -345,12 +345,12 @@ def test_categorical_golden(gpu):
     noise = _dev(d["exp_noise"])
     val = torch.empty(N, device=gpu); act = torch.empty(N, dtype=torch.int64, device=gpu)
     lp = torch.empty(N, device=gpu); ent = torch.empty(N, device=gpu)
-    Hh.call("ppo_heads_act", fd.data_ptr(), N, Hp, wc.data_ptr(), bc.data_ptr(), wad.data_ptr(), bad.data_ptr(), A,
+    Hh.call("ppo_heads_act", fd.data_ptr(), None, N, Hp, wc.data_ptr(), bc.data_ptr(), wad.data_ptr(), bad.data_ptr(), A,
             noise.data_ptr(), 0, 0, 0, None, val.data_ptr(), act.data_ptr(), lp.data_ptr(), ent.data_ptr(), _s())
     assert np.array_equal(act.cpu().numpy(), d["action"][:, 0])                  # bit-exact sampling
     np.testing.assert_allclose(lp.cpu().numpy(), d["log_probs"][:, 0], atol=2e-6)
     np.testing.assert_allclose(ent.cpu().numpy(), d["entropy"], atol=2e-6)
-    Hh.call("ppo_heads_act", fd.data_ptr(), N, Hp, wc.data_ptr(), bc.data_ptr(), wad.data_ptr(), bad.data_ptr(), A,
+    Hh.call("ppo_heads_act", fd.data_ptr(), None, N, Hp, wc.data_ptr(), bc.data_ptr(), wad.data_ptr(), bad.data_ptr(), A,
             None, 0, 0, 1, None, val.data_ptr(), act.data_ptr(), lp.data_ptr(), ent.data_ptr(), _s())
     assert np.array_equal(act.cpu().numpy(), d["mode"][:, 0])
 
@@ -364,7 +364,7 @@ def test_device_sampling_distribution(gpu):
     ba = torch.zeros(A, device=gpu)
     wc, bc = torch.zeros(Hp, device=gpu), torch.zeros(1, device=gpu)
     act = torch.empty(N, dtype=torch.int64, device=gpu)
-    Hh.call("ppo_heads_act", f.data_ptr(), N, Hp, wc.data_ptr(), bc.data_ptr(), wa.data_ptr(), ba.data_ptr(), A,
+    Hh.call("ppo_heads_act", f.data_ptr(), None, N, Hp, wc.data_ptr(), bc.data_ptr(), wa.data_ptr(), ba.data_ptr(), A,
             None, 1234, 1, 0, None, None, act.data_ptr(), None, None, _s())
     freq = np.bincount(act.cpu().numpy(), minlength=A) / N
     p = torch.softmax(torch.linspace(-1, 1.5, A), 0).numpy()
@@ -590,3 +590,151 @@ def test_recurrent_ppo_iteration_runs(gpu):
     assert all(np.isfinite(losses))
     assert (after - before).abs().max().item() > 1e-5
     assert torch.equal(st.recurrent_hidden_states[0], st.recurrent_hidden_states[-1])
+
+
+# ------------------------------------------------------------- MLPBase (c1)
+def _mlp_policy(gpu, I, V, H, A, seed):
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.synthetic import Discrete
+    torch.manual_seed(seed)
+    return M.Policy((I,), Discrete(A), base=M.MLPBase, base_kwargs={"recurrent": False, "hidden_size": H},
+                    vector_obs_len=V)
+
+
+def test_mlp_golden_evaluate(gpu):
+    """MLPBase + Categorical(64, 2) with the reference's parameters (mlp.npz):
+    value, log-prob and entropy through Policy.evaluate_actions within 1e-5."""
+    d = golden("mlp.npz")
+    pol = _mlp_policy(gpu, 4, 0, 64, 2, 0)
+    _load_flat(pol, np.concatenate([d["base_params"], d["head_params"]]))
+    pol.to(gpu)
+    x = _dev(d["x"])
+    B = x.shape[0]
+    for a in (0, 1):
+        act = torch.full((B, 1), a, dtype=torch.int64, device=gpu)
+        v, lp, ent, _ = pol.evaluate_actions(x, None, None, None, act)
+        np.testing.assert_allclose(v.cpu().numpy(), d["value"], atol=1e-5)
+        np.testing.assert_allclose(lp.cpu().numpy()[:, 0], d["norm_logits"][:, a], atol=1e-5)
+        np.testing.assert_allclose(float(ent), d["entropy"].mean(), atol=1e-5)
+    v2 = pol.get_value(x, None, None, None)
+    np.testing.assert_allclose(v2.cpu().numpy(), d["value"], atol=1e-5)
+    _, a, lp, _ = pol.act(x, None, None, None, deterministic=True)
+    assert np.array_equal(a.cpu().numpy()[:, 0], d["norm_logits"].argmax(1))
+
+
+@pytest.mark.parametrize("I,V,H,A,B", [(4, 0, 64, 2, 256), (5, 3, 128, 6, 37)])
+def test_mlp_minibatch_grads_vs_oracle(gpu, I, V, H, A, B):
+    """One feed-forward minibatch of an MLPBase policy (input gather + vector-obs
+    concat + padding, tanh towers, heads/loss, every dgrad/wgrad) vs the oracle's
+    float64 analytic gradients: max |err| <= 1e-5 * max|grad| per tensor."""
+    from a2c_ppo_acktr.algo.ppo import FlatAdam
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import Discrete
+    pol = _mlp_policy(gpu, I, V, H, A, B)
+    with torch.no_grad():
+        pol.dist.linear.weight.mul_(20.0)
+        pol.base.critic_linear.weight.mul_(3.0)
+    init = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy().astype(np.float64)
+    pol.to(gpu)
+    eng = pol.hip_engine()
+    T, N = 4, (B + 1) // 2
+    st = RolloutStorage(T, N, (I,), [V], Discrete(A), 1, device=gpu)
+    g = torch.Generator().manual_seed(B + 1)
+    st.obs.copy_(torch.randn(st.obs.shape, generator=g).to(gpu))
+    if V:
+        st.vector_obs.copy_(torch.rand(st.vector_obs.shape, generator=g).to(gpu))
+    st.actions.copy_(torch.randint(0, A, st.actions.shape, generator=g).to(gpu))
+    st.action_log_probs.copy_((torch.log(torch.rand(st.action_log_probs.shape, generator=g)) * 0.3 - 1.0).to(gpu))
+    st.value_preds.copy_(torch.randn(st.value_preds.shape, generator=g).to(gpu) * 0.1)
+    st.returns.copy_(torch.randn(st.returns.shape, generator=g).to(gpu))
+    adv = torch.randn(T, N, generator=g).to(gpu)
+    idx = torch.randperm(T * N, generator=g)[:B].to(gpu)
+    hp = {"clip": 0.1, "value_coef": 0.5, "entropy_coef": 0.01, "use_clipped_value_loss": True}
+    loss = torch.zeros(3, dtype=torch.float64, device=gpu)
+    opt = FlatAdam(pol.parameters(), lr=0.0, eps=1e-5, max_grad_norm=None)
+    eng.train_minibatch(st, adv, idx, hp, loss, opt)
+    torch.cuda.synchronize()
+    shapes = O.mlp_param_shapes(I + V, H, A)
+    p = O.unflatten(init, shapes)
+    ii = idx.cpu().numpy()
+    x = st.obs[:-1].reshape(T * N, I).cpu().numpy()[ii]
+    if V:
+        x = np.concatenate([x, st.vector_obs[:-1].reshape(T * N, V).cpu().numpy()[ii]], 1)
+    value, logits, cache = O.mlp_forward(p, x.astype(np.float64))
+    f = lambda t: t.reshape(-1).cpu().numpy()[ii]  # noqa: E731
+    lg = O.loss_head_grads(value, logits, f(st.actions), f(st.action_log_probs), f(adv),
+                           st.value_preds[:-1].reshape(-1).cpu().numpy()[ii],
+                           st.returns[:-1].reshape(-1).cpu().numpy()[ii], 0.1, 0.5, 0.01)
+    grads = O.mlp_backward(p, cache, lg["g_value"], lg["g_logits"])
+    got = O.unflatten(eng.grad.cpu().numpy(), shapes)
+    for name, _ in shapes:
+        ref = grads[name]
+        err = np.abs(got[name] - ref).max()
+        assert err <= 1e-5 * max(np.abs(ref).max(), 1e-3), (name, err, np.abs(ref).max())
+    np.testing.assert_allclose(loss.cpu().numpy(), [lg["value_loss"], lg["action_loss"], lg["entropy"]],
+                               rtol=2e-5, atol=1e-6)
+
+
+def test_cartpole_env_vs_oracle(gpu):
+    """CartPoleVecEnv (one fp32 kernel) vs the numpy restatement, step by step
+    from the same state: observations within 1e-5, reward/mask/bad_mask/episode
+    length and every counter-RNG reset exact."""
+    from a2c_ppo_acktr.synthetic import CartPoleVecEnv
+    N = 512
+    env = CartPoleVecEnv(N, seed=11, max_steps=60, device=gpu)
+    obs = torch.empty(N, 4, device=gpu)
+    env.reset_into(obs)
+    st0, k0 = O.cartpole_step(np.zeros((N, 4)), np.zeros(N), None, 11, 0)[:2]
+    np.testing.assert_array_equal(env.state.cpu().numpy(), st0)
+    g = torch.Generator().manual_seed(0)
+    ended = 0
+    for c in range(1, 150):
+        st, k = env.state.cpu().numpy(), env.steps.cpu().numpy()
+        a = torch.randint(0, 2, (N, 1), generator=g)
+        r, m, bm = env.step_into(obs, a.to(gpu))
+        est, ek, eobs, er, em, ebm, eep = O.cartpole_step(st, k, a.numpy(), 11, c, max_steps=60)
+        np.testing.assert_array_equal(m.cpu().numpy()[:, 0], em)
+        np.testing.assert_array_equal(bm.cpu().numpy()[:, 0], ebm)
+        np.testing.assert_array_equal(r.cpu().numpy()[:, 0], er)
+        np.testing.assert_array_equal(env.ep_len.cpu().numpy(), eep)
+        np.testing.assert_array_equal(env.steps.cpu().numpy(), ek)
+        np.testing.assert_allclose(obs.cpu().numpy(), eobs, rtol=1e-5, atol=1e-6)
+        ended += int((em == 0).sum())
+    assert ended > N   # plenty of terminations and TimeLimit truncations exercised
+
+
+def test_ppo_learns_cartpole(gpu):
+    """c1 end to end (MLPBase hidden 64, GPU CartPole, GAE, PPO.update): the
+    mean finished-episode length must rise well above a random policy's ~22."""
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.algo import PPO
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import CartPoleVecEnv
+    torch.manual_seed(0)
+    N, T = 16, 128
+    env = CartPoleVecEnv(N, seed=3, device=gpu)
+    pol = M.Policy(env.obs_shape, env.action_space, base=M.MLPBase, base_kwargs={"recurrent": False})
+    pol.to(gpu)
+    agent = PPO(pol, 0.2, 4, 4, 0.5, 0.0, lr=2.5e-3, eps=1e-5, max_grad_norm=0.5)
+    st = RolloutStorage(T, N, env.obs_shape, [0], env.action_space, 1, device=gpu)
+    env.reset_into(st.obs[0])
+    hist = []
+    for it in range(60):
+        tot = torch.zeros(2, device=gpu)
+        for step in range(T):
+            v, a, lp, h = pol.act(st.obs[step], st.vector_obs[step], st.recurrent_hidden_states[step],
+                                  st.masks[step])
+            r, m, bm = env.step_into(st.obs[step + 1], a)
+            tot[0] += env.ep_len.sum()
+            tot[1] += (env.ep_len > 0).sum()
+            st.insert(st.obs[step + 1], st.vector_obs[step + 1], h, a, lp, v, r, m, bm)
+        nv = pol.get_value(st.obs[-1], st.vector_obs[-1], st.recurrent_hidden_states[-1], st.masks[-1])
+        st.compute_returns(nv, True, 0.99, 0.95, True)
+        losses = agent.update(st)
+        st.after_update()
+        t = tot.cpu().numpy()
+        hist.append(t[0] / max(t[1], 1))
+        assert all(np.isfinite(losses))
+    early, late = np.mean(hist[:3]), np.mean(hist[-5:])
+    print("cartpole mean episode length", early, "->", late)
+    assert early < 40 and late > 150, hist

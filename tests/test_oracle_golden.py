@@ -75,101 +75,63 @@ def test_adam_clip():
 
 
 def test_mlp_submodules():
+    """oracle.mlp_forward against MLPBase's submodules (actor / critic /
+    critic_linear) and Categorical driven by the reference (mlp.npz)."""
     d = golden("mlp.npz")
-    sh = [("actor.0.weight", (64, 4)), ("actor.0.bias", (64,)), ("actor.2.weight", (64, 64)),
-          ("actor.2.bias", (64,)), ("critic.0.weight", (64, 4)), ("critic.0.bias", (64,)),
-          ("critic.2.weight", (64, 64)), ("critic.2.bias", (64,)), ("critic_linear.weight", (1, 64)),
-          ("critic_linear.bias", (1,))]
-    assert [str(n) for n in d["base_names"]] == [n for n, _ in sh]
-    p = O.unflatten(d["base_params"], sh)
-    x = d["x"].astype(np.float64)
-
-    def mlp(pre):
-        h = np.tanh(x @ p[pre + ".0.weight"].T + p[pre + ".0.bias"])
-        return np.tanh(h @ p[pre + ".2.weight"].T + p[pre + ".2.bias"])
-
-    value = mlp("critic") @ p["critic_linear.weight"].T + p["critic_linear.bias"]
-    feat = mlp("actor")
-    np.testing.assert_allclose(value, d["value"], atol=1e-6)
-    np.testing.assert_allclose(feat, d["actor_features"], atol=1e-6)
-    hp = d["head_params"]
-    logits = feat @ hp[:128].reshape(2, 64).T + hp[128:]
+    sh = O.mlp_param_shapes(4, 64, 2)
+    assert ["base." + str(n) for n in d["base_names"]] == [n for n, _ in sh[:10]]
+    p = O.unflatten(np.concatenate([d["base_params"], d["head_params"]]), sh)
+    value, logits, cache = O.mlp_forward(p, d["x"])
+    np.testing.assert_allclose(value, d["value"][:, 0], atol=1e-6)
+    np.testing.assert_allclose(cache["actor"][1], d["actor_features"], atol=1e-6)
     c = O.categorical(logits)
     np.testing.assert_allclose(c["norm_logits"], d["norm_logits"], atol=1e-6)
     np.testing.assert_allclose(c["entropy"], d["entropy"], atol=1e-6)
 
 
-def test_gru_evaluate_actions():
-    d = golden("gru_eval.npz")
-    hidden, V, N, T = [int(x) for x in d["meta"]]
-    shapes = O.cnn_param_shapes(hidden, recurrent=True, vector_obs_len=V)
-    assert [str(n) for n in d["names"]] == [n for n, _ in shapes]
-    p = O.unflatten(d["params"], shapes)
-    x = O.decode_obs(d["obs_u8"].reshape(T * N, 4, 84, 84))
-    feat, _ = O.cnn_trunk(p, x)
-    xin = np.concatenate([feat, d["vector_obs"].reshape(T * N, V)], 1)
-    out, hT = O.gru_sequence(p, xin, d["h0"], d["masks"])
-    value = out @ p["base.critic_linear.weight"].T + p["base.critic_linear.bias"]
-    c = O.categorical(out @ p["dist.linear.weight"].T + p["dist.linear.bias"])
-    logp = np.take_along_axis(c["norm_logits"], d["actions"], -1)
-    np.testing.assert_allclose(value, d["values"], atol=2e-6)
-    np.testing.assert_allclose(logp, d["log_probs"], atol=2e-6)
-    np.testing.assert_allclose(c["entropy"].mean(), d["entropy"][0], atol=2e-6)
-    np.testing.assert_allclose(hT, d["hT"], atol=2e-6)
+def test_mlp_backward_finite_difference():
+    """oracle.mlp_backward (tanh towers) against central differences of the
+    PPO loss in float64."""
+    rng = np.random.default_rng(3)
+    sh = O.mlp_param_shapes(6, 8, 3)
+    p = {n: rng.standard_normal(s) * 0.5 for n, s in sh}
+    B = 5
+    x = rng.standard_normal((B, 6))
+    act = rng.integers(0, 3, B)
+    olp, adv = np.log(rng.random(B)) * 0.3 - 1.0, rng.standard_normal(B)
+    vp, ret = rng.standard_normal(B) * 0.1, rng.standard_normal(B)
+
+    def loss(q):
+        v, lg, _ = O.mlp_forward(q, x)
+        r = O.loss_head_grads(v, lg, act, olp, adv, vp, ret, 0.2, 0.5, 0.01)
+        return 0.5 * r["value_loss"] + r["action_loss"] - 0.01 * r["entropy"]
+
+    v, lg, cache = O.mlp_forward(p, x)
+    r = O.loss_head_grads(v, lg, act, olp, adv, vp, ret, 0.2, 0.5, 0.01)
+    g = O.mlp_backward(p, cache, r["g_value"], r["g_logits"])
+    for name, shp in sh:
+        for j in rng.choice(int(np.prod(shp)), size=min(3, int(np.prod(shp))), replace=False):
+            q = {k: a.copy() for k, a in p.items()}
+            q[name].reshape(-1)[j] += 1e-6
+            lp = loss(q)
+            q[name].reshape(-1)[j] -= 2e-6
+            lm = loss(q)
+            fd = (lp - lm) / 2e-6
+            assert abs(fd - g[name].reshape(-1)[j]) < 1e-6 + 1e-5 * abs(fd), (name, j, fd, g[name].reshape(-1)[j])
 
 
-def test_full_iteration_replay():
-    """One T/run.py iteration replayed through the oracle matches the reference."""
-    d = golden("cnn_update.npz")
-    hidden, N, T, E, Mb = [int(x) for x in d["meta"]]
-    shapes = O.cnn_param_shapes(hidden)
-    assert [str(n) for n in d["names"]] == [n for n, _ in shapes]
-    r = O.run_iteration(d["init_params"], shapes, d["obs_u8"], d["exp_noise"], d["rewards"][..., 0],
-                        d["masks"][..., 0], d["perms"], num_mini_batch=Mb, lr=float(d["lr"][0]))
-    assert np.array_equal(r["actions"], d["actions"][..., 0])
-    np.testing.assert_allclose(r["values"], d["values"][..., 0], atol=1e-6)
-    np.testing.assert_allclose(r["log_probs"], d["action_log_probs"][..., 0], atol=1e-6)
-    np.testing.assert_allclose(r["returns"], d["returns"][..., 0], atol=1e-6)
-    np.testing.assert_allclose(r["first"]["clipped_grad"], d["mb0_clipped_grad"], rtol=0, atol=1e-6)
-    np.testing.assert_allclose(r["losses"], d["losses"], rtol=1e-5, atol=1e-6)
-    np.testing.assert_allclose(r["final_params"], d["final_params"], rtol=0, atol=1e-6)
-
-
-def test_gru_backward_finite_difference():
-    """The oracle's hand-written BPTT (used to check the HIP GRU backward) against
-    central finite differences of its own forward (float64)."""
-    rng = np.random.default_rng(0)
-    H, I, T, n = 4, 3, 5, 2
-    p = {"base.gru.weight_ih_l0": rng.standard_normal((3 * H, I)) * 0.5,
-         "base.gru.weight_hh_l0": rng.standard_normal((3 * H, H)) * 0.5,
-         "base.gru.bias_ih_l0": rng.standard_normal(3 * H) * 0.1,
-         "base.gru.bias_hh_l0": rng.standard_normal(3 * H) * 0.1}
-    x = rng.standard_normal((T * n, I))
-    h0 = rng.standard_normal((n, H))
-    masks = (rng.random((T, n)) > 0.3).astype(np.float64)
-    wout = rng.standard_normal((T * n, H))
-
-    def loss(pp, xx):
-        out, _ = O.gru_sequence_cache(pp, xx, h0, masks)
-        return (out * wout).sum()
-
-    out, cache = O.gru_sequence_cache(p, x, h0, masks)
-    g, dx = O.gru_backward(p, x, masks, cache, wout)
-    eps = 1e-6
-    for k in p:
-        num = np.zeros_like(p[k])
-        for i in np.ndindex(p[k].shape):
-            pp = {kk: v.copy() for kk, v in p.items()}
-            pp[k][i] += eps
-            lp = loss(pp, x)
-            pp[k][i] -= 2 * eps
-            num[i] = (lp - loss(pp, x)) / (2 * eps)
-        np.testing.assert_allclose(g[k], num, rtol=1e-5, atol=1e-7)
-    num = np.zeros_like(x)
-    for i in np.ndindex(x.shape):
-        xx = x.copy()
-        xx[i] += eps
-        lp = loss(p, xx)
-        xx[i] -= 2 * eps
-        num[i] = (lp - loss(p, xx)) / (2 * eps)
-    np.testing.assert_allclose(dx, num, rtol=1e-5, atol=1e-7)
+def test_cartpole_restatement_terminates_and_resets():
+    """oracle.cartpole_step: always pushing right topples the pole within gym's
+    thresholds; ended lanes report their length and restart in U(-0.05, 0.05)."""
+    N = 16
+    st, k, obs, *_ = O.cartpole_step(np.zeros((N, 4)), np.zeros(N), None, 7, 0)
+    assert np.all(np.abs(obs) <= 0.05) and np.all(k == 0)
+    lens = []
+    for c in range(1, 200):
+        st, k, obs, rew, mask, bad, ep = O.cartpole_step(st, k, np.ones(N, np.int64), 7, c)
+        assert np.all(rew == 1) and np.all(bad == 1)
+        lens += list(ep[mask == 0])
+        assert np.all(np.abs(obs[mask == 0]) <= 0.05)
+    assert len(lens) >= N and 5 <= min(lens) and max(lens) <= 30
+    st, k, *_ = O.cartpole_step(np.zeros((2, 4)), np.array([0, 9]), np.array([0, 1]), 7, 0, max_steps=10)
+    assert list(k) == [1, 0]

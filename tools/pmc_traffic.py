@@ -50,6 +50,7 @@ def main():
            "source": "tools/profile_round.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) of "
                      "`python3 bench.py --no-cpu-baseline --no-gae-roofline`"}
     out["tag"] = tag
+    out["workload"] = json.loads(line)["config"]["workload"]   # bench.py only uses traffic of the same workload
     json.dump(out, open(os.path.join(prof, f"{tag}_traffic.json"), "w"), indent=1)
     # the file bench.py reads to fill roofline.traffic for this kernel
     json.dump(out, open(os.path.join(prof, "roofline_traffic.json"), "w"), indent=1)
