@@ -42,12 +42,11 @@ struct Conv1Fwd : C_ {
     const int b = m / 400, pp = m - b * 400, oy = pp / 20, ox = pp - oy * 20;
     return {obs + obs_row(idx, row0, b) * (long long)(C * IMG2) + (oy * 4) * IMG + ox * 4, true};
   }
-  __device__ f32x4 a_load(const ACtx& c, int k) const {
-    if (!c.ok) return zero4();
+  using Raw = std::conditional_t<sizeof(InT) == 1, uint32_t, f32x4>;
+  __device__ Raw a_load(const ACtx& c, int k) const {
+    if (!c.ok) return Raw{};
     const int ch = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
-    const InT* q = c.base + ch * IMG2 + ky * IMG + kx;
-    if constexpr (sizeof(InT) == 1) return u8x4(*reinterpret_cast<const uint32_t*>(q));
-    else return *reinterpret_cast<const f32x4*>(q);
+    return *reinterpret_cast<const Raw*>(c.base + ch * IMG2 + ky * IMG + kx);
   }
   __device__ BCtx b_ctx(int n, int) const { return {w + n * (C * 64), 0, n < 32}; }
   __device__ f32x4 b_load(const BCtx& c, int k) const {
@@ -123,15 +122,17 @@ struct ConvDgradS1 : C_ {
   }
 };
 
-// conv2 dgrad (4x4 stride 2, 20x20 <- 9x9): split by output-pixel phase
-// (y&1, x&1) = blockIdx.z so each phase is a dense 2x2-tap problem:
-// m = (b, yy, xx) with y = 2yy+py; k = (ty, tx, co): ky = py+2ty,
-// oy = yy - ty.  wd packed [4 phases][CIN][4*COUT].
+// conv2 dgrad (4x4 stride 2, 20x20 <- 9x9), the four output-pixel phases
+// (py, px) = (y&1, x&1) merged into one GEMM: every phase of the 2x2 pixel
+// block (yy, xx) reads the same dy taps (oy, ox) = (yy-ty, xx-tx) and differs
+// only in its weights (ky = py+2ty), so m = (b, yy, xx), k = (ty, tx, co) and
+// n = (phase, ci) with wd packed [4 phases][CIN][4*COUT] = [128][256] —
+// a 128-wide B operand instead of four 32-wide passes over the same A rows.
 template <class C_>
 struct Conv2Dgrad : C_ {
   using BCtx = typename C_::BCtx;
-  static constexpr int HIN = 20, CIN = 32, HOUT = 9, COUT = 64, K = 4 * COUT, PPH = 100;
-  const float* dy; const float* wd; const float* act; float* dx; int M;  // M = B*100 per phase
+  static constexpr int HIN = 20, CIN = 32, HOUT = 9, COUT = 64, K = 4 * COUT, PPH = 100, N = 4 * CIN;
+  const float* dy; const float* wd; const float* act; float* dx; int M;  // M = B*100
   struct ACtx { const float* p; int yy; int xx; bool ok; };
   __device__ ACtx a_ctx(int m, int) const {
     if (m >= M) return {dy, 0, 0, false};
@@ -144,16 +145,16 @@ struct Conv2Dgrad : C_ {
     if (!c.ok || oy < 0 || oy >= HOUT || ox < 0 || ox >= HOUT) return zero4();
     return *reinterpret_cast<const f32x4*>(c.p + (oy * HOUT + ox) * COUT + co);
   }
-  __device__ BCtx b_ctx(int n, int z) const { return {wd + ((size_t)z * CIN + n) * K, 0, n < CIN}; }
+  __device__ BCtx b_ctx(int n, int) const { return {wd + (size_t)n * K, 0, n < N}; }
   __device__ f32x4 b_load(const BCtx& c, int k) const {
     return c.ok ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
   }
   __device__ void k_range(int, int& b, int& e) const { b = 0; e = K; }
-  __device__ void store(int m, int n, int z, float v) const {
-    if (m < M && n < CIN) {
-      const int b = m / PPH, pp = m - b * PPH, yy = pp / 10, xx = pp - yy * 10;
-      const int y = 2 * yy + (z >> 1), x = 2 * xx + (z & 1);
-      const size_t i = ((size_t)(b * HIN + y) * HIN + x) * CIN + n;
+  __device__ void store(int m, int n, int, float v) const {
+    if (m < M && n < N) {
+      const int b = m / PPH, pp = m - b * PPH, yy = pp / 10, xx = pp - yy * 10, ph = n >> 5;
+      const int y = 2 * yy + (ph >> 1), x = 2 * xx + (ph & 1);
+      const size_t i = ((size_t)(b * HIN + y) * HIN + x) * CIN + (n & 31);
       dx[i] = act[i] > 0.f ? v : 0.f;
     }
   }
@@ -167,20 +168,29 @@ struct Conv2Dgrad : C_ {
 // bias partial (db[co] = Σ_r dz[r][co]).
 // ---------------------------------------------------------------------------
 // conv1 wgrad: X(r, kk) = decoded obs[idx[b]][c][4oy+ky][4ox+kx], kk = (c,ky,kx)
+// A k-tile (BK rows, BK | 400, chunks BK-aligned) never straddles two images,
+// so the image (and its minibatch row gather) is resolved once per tile from
+// the block-uniform tile start — a scalar load, not one per operand load.
 template <typename InT, class C_>
 struct Conv1Wgrad : WgradBase<C_> {
+  static_assert(400 % C_::BK == 0, "conv1 wgrad k-tiles must not straddle images");
+  static constexpr bool B_TILE = true;
   const InT* obs; const int64_t* idx; long long row0; int C;
   struct BCtx { int off; bool ok; };
+  struct TCtx { const InT* img; int r0; };
+  using Raw = std::conditional_t<sizeof(InT) == 1, uint32_t, f32x4>;
   __device__ BCtx b_ctx(int n, int) const {
     const int ch = n >> 6, ky = (n >> 3) & 7, kx = n & 7;
     return {ch * IMG2 + ky * IMG + kx, n < C * 64};
   }
-  __device__ f32x4 b_load(const BCtx& c, int r) const {
-    if (!c.ok || r >= this->R) return zero4();
-    const int b = r / 400, pp = r - b * 400, oy = pp / 20, ox = pp - oy * 20;
-    const InT* q = obs + obs_row(idx, row0, b) * (long long)(C * IMG2) + (oy * 4) * IMG + ox * 4 + c.off;
-    if constexpr (sizeof(InT) == 1) return u8x4(*reinterpret_cast<const uint32_t*>(q));
-    else return *reinterpret_cast<const f32x4*>(q);
+  __device__ TCtx tile(int k0) const {
+    const int b = k0 / 400;
+    return {obs + obs_row(idx, row0, b) * (long long)(C * IMG2), b * 400};
+  }
+  __device__ Raw b_load_t(const BCtx& c, const TCtx& t, int r) const {
+    if (!c.ok || r >= this->R) return Raw{};
+    const int pp = r - t.r0, oy = pp / 20, ox = pp - oy * 20;
+    return *reinterpret_cast<const Raw*>(t.img + (oy * 4) * IMG + ox * 4 + c.off);
   }
 };
 
@@ -278,9 +288,10 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // Tile-configuration variants (A/B knobs for tools/kbench.py; defaults are the
 // measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
 // ---------------------------------------------------------------------------
-enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_N };
-static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad"};
-static int g_tune[TK_N] = {1, 1, 1, 1, 1};  // measured best (kbench sweep, profiles/)
+enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_N };
+static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
+                                         "fc_fwd", "conv2_fwd"};
+static int g_tune[TK_N] = {0, 3, 3, 1, 1, 0, 0};  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   for (int i = 0; i < TK_N; ++i)
@@ -312,6 +323,49 @@ using V64_2 = Cfg<128, 64, 4, 1, true, true>;
     default: { TEMPL(V32_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
   }
 
+// N = 128 problems (conv2 dgrad, phases merged)
+using V128_0 = Cfg<128, 128, 2, 2, true, true>;           // 2x2 waves of 64x64, 32 KB
+using V128_1 = Cfg<256, 128, 4, 2, true, true>;           // 8 waves of 64x64, 48 KB
+using V128_2 = Cfg<128, 128, 4, 1, true, true>;           // 4 waves of 32x128, 32 KB
+using V128_3 = Cfg<64, 128, 2, 2, true, true>;            // 2x2 waves of 32x64, 24 KB
+
+#define PPO_VARIANTS128(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                        \
+  switch (g_tune[tk]) {                                                                            \
+    case 1: { TEMPL(V128_1) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+    case 2: { TEMPL(V128_2) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+    case 3: { TEMPL(V128_3) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+    default: { TEMPL(V128_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+  }
+
+// dense-core experiments (fc forward, N multiple of 128; conv2 forward, N = 64)
+using VD_1 = Cfg<128, 128, 2, 2, true, true, false, 32>;  // BK 32
+using VD_2 = Cfg<256, 128, 4, 2, true, true>;             // 8 waves of 64x64
+using VD_3 = Cfg<256, 128, 2, 2, true, true>;             // 4 waves of 128x64
+using VD_4 = Cfg<128, 128, 1, 2, true, true>;             // 2 waves of 128x64
+using VD_5 = Cfg<256, 128, 4, 2, true, true, false, 32>;  // 8 waves, BK 32
+using V64_3 = Cfg<256, 64, 4, 1, true, true>;             // 4 waves of 64x64
+using V64_4 = Cfg<256, 64, 2, 1, true, true>;             // 2 waves of 128x64
+using V64_5 = Cfg<128, 64, 2, 2, true, true, false, 32>;  // BK 32
+using V64_6 = Cfg<256, 64, 4, 2, true, true>;             // 8 waves of 64x32
+
+#define PPO_VARIANTS_FC(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                       \
+  switch (g_tune[tk]) {                                                                           \
+    case 1: { TEMPL(VD_1) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
+    case 2: { TEMPL(VD_2) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
+    case 3: { TEMPL(VD_3) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
+    case 4: { TEMPL(VD_4) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
+    case 5: { TEMPL(VD_5) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
+    default: { TEMPL(CfgN128) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+  }
+#define PPO_VARIANTS_C2F(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                       \
+  switch (g_tune[tk]) {                                                                            \
+    case 3: { TEMPL(V64_3) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
+    case 4: { TEMPL(V64_4) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
+    case 5: { TEMPL(V64_5) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
+    case 6: { TEMPL(V64_6) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
+    default: { TEMPL(V64_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
+  }
+
 #define PPO_VARIANTS64(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                        \
   switch (g_tune[tk]) {                                                                           \
     case 1: { TEMPL(V64_1) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
@@ -340,9 +394,11 @@ PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, lo
 }
 
 PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream) {
-  ConvFwd<20, 32, 4, 2, 9, 64, V64_0> p;
-  p.in = a1; p.w = w2p; p.bias = b2; p.out = out; p.M = B * 81;
-  return launch(p, (long long)B * 81, 64, 1, as_stream(stream), "conv2_fwd", 2.0 * B * 81 * 64 * 512);
+  const int tk = TK_CONV2_FWD;
+#define T2(C_) ConvFwd<20, 32, 4, 2, 9, 64, C_>
+  PPO_VARIANTS_C2F(T2, (p.in = a1, p.w = w2p, p.bias = b2, p.out = out, p.M = B * 81), (long long)B * 81, 64, 1,
+                   "conv2_fwd", 2.0 * B * 81 * 64 * 512)
+#undef T2
 }
 
 PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream) {
@@ -358,9 +414,11 @@ PPO_API int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, co
                                 void* stream) {
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_relu_fwd: K=%d must be a multiple of 4", K);
   if (N % 128 == 0) {
-    DenseReluFwd<CfgN128> p;
-    p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K;
-    return launch(p, M, N, 1, as_stream(stream), "linear_relu_fwd", 2.0 * M * N * K);
+    const int tk = TK_FC_FWD;
+#define TF(C_) DenseReluFwd<C_>
+    PPO_VARIANTS_FC(TF, (p.x = x, p.w = w, p.bias = b, p.out = out, p.M = M, p.N = N, p.K = K), M, N, 1,
+                    "linear_relu_fwd", 2.0 * M * N * K)
+#undef TF
   }
   DenseReluFwd<CfgN64> p;
   p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K;
@@ -433,8 +491,8 @@ PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const flo
 PPO_API int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const float* a1, float* dz1, void* stream) {
   const int tk = TK_CONV2_DGRAD;
 #define TD2(C_) Conv2Dgrad<C_>
-  PPO_VARIANTS32(TD2, (p.dy = dz2, p.wd = w2d, p.act = a1, p.dx = dz1, p.M = B * 100), (long long)B * 100, 32, 4,
-                 "conv2_dgrad", 2.0 * B * 81 * 64 * 512)
+  PPO_VARIANTS128(TD2, (p.dy = dz2, p.wd = w2d, p.act = a1, p.dx = dz1, p.M = B * 100), (long long)B * 100, 128, 1,
+                  "conv2_dgrad", 2.0 * B * 81 * 64 * 512)
 #undef TD2
 }
 

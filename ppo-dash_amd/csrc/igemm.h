@@ -54,6 +54,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nb) {
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
+// Operand loaders return their raw global data (f32x4, or uint32_t = 4 u8
+// pixels); the conversion to the f32 MFMA operand runs at the LDS store, after
+// the current tile's MFMAs, so a tile's global loads stay in flight across the
+// whole compute phase instead of stalling the wave right after issue.
+__device__ __forceinline__ f32x4 to_f32x4(const f32x4& v) { return v; }
+__device__ __forceinline__ f32x4 to_f32x4(uint32_t u) {
+  return f32x4{(float)(u & 255u), (float)((u >> 8) & 255u), (float)((u >> 16) & 255u), (float)(u >> 24)};
+}
+
 // ---------------------------------------------------------------------------
 // Core: C[m][n] = Σ_k A[m][k] B[n][k]; problem P supplies loaders + epilogue.
 // ---------------------------------------------------------------------------
@@ -115,22 +124,31 @@ __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
     }
   }
 
-  f32x4 ra[NVA], rb[NVB];
+  using ARaw = decltype(p.a_load(actx[0], 0));
+  ARaw ra[NVA];
+  // B loaders may take a per-k-tile context computed once from the (block-
+  // uniform) tile start, e.g. the image a 16-row wgrad tile lies in.
+  auto bload = [&](int i, int k0) {
+    if constexpr (P::B_TILE) return p.b_load_t(bctx[i], p.tile(k0), k0 + bk[i]);
+    else return p.b_load(bctx[i], k0 + bk[i]);
+  };
+  using BRaw = decltype(bload(0, 0));
+  BRaw rb[NVB];
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < NVA; ++i) ra[i] = aon[i] ? p.a_load(actx[i], k0 + ak[i]) : zero4();
+    for (int i = 0; i < NVA; ++i) ra[i] = aon[i] ? p.a_load(actx[i], k0 + ak[i]) : ARaw{};
 #pragma unroll
-    for (int i = 0; i < NVB; ++i) rb[i] = bon[i] ? p.b_load(bctx[i], k0 + bk[i]) : zero4();
+    for (int i = 0; i < NVB; ++i) rb[i] = bon[i] ? bload(i, k0) : BRaw{};
   };
   auto sstore = [&](int buf) {
     float* As = smem + buf * STAGE;
     float* Bs = As + TA::SIZE;
 #pragma unroll
     for (int i = 0; i < NVA; ++i)
-      if (aon[i]) *reinterpret_cast<f32x4*>(As + aoff[i]) = ra[i];
+      if (aon[i]) *reinterpret_cast<f32x4*>(As + aoff[i]) = to_f32x4(ra[i]);
 #pragma unroll
     for (int i = 0; i < NVB; ++i)
-      if (bon[i]) *reinterpret_cast<f32x4*>(Bs + boff[i]) = rb[i];
+      if (bon[i]) *reinterpret_cast<f32x4*>(Bs + boff[i]) = to_f32x4(rb[i]);
   };
 
   f32x16 acc[TM][TN];
@@ -154,10 +172,12 @@ __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
     const float* As = smem + buf * STAGE;
     const float* Bs = As + TA::SIZE;
     if constexpr (P::BIAS_FROM_A) {
-      static_assert(!P::A_KC, "bias partials read the row-contiguous A tile");
-      if (blockIdx.y == 0 && tid < BM) {
+      // db partial: every thread sums BK/G rows of one A-tile column
+      static_assert(!P::A_KC && NT % BM == 0 && BK % (NT / BM) == 0, "bias partials");
+      constexpr int G = NT / BM;
+      if (blockIdx.y == 0) {
 #pragma unroll
-        for (int k = 0; k < BK; ++k) bias_acc += As[k * BM + tid];
+        for (int k = tid / BM; k < BK; k += G) bias_acc += As[k * BM + tid % BM];
       }
     }
 #pragma unroll
@@ -207,25 +227,33 @@ __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
         }
   }
   if constexpr (P::BIAS_FROM_A) {
-    if (blockIdx.y == 0 && tid < BM) p.store_bias(m0 + tid, z, bias_acc);
+    if (blockIdx.y == 0) {   // fixed-order combine of the G row-group partials
+      constexpr int G = NT / BM;
+      smem[tid] = bias_acc;   // the main loop ended on a barrier
+      __syncthreads();
+      if (tid < BM) {
+        float t = smem[tid];
+#pragma unroll
+        for (int g = 1; g < G; ++g) t += smem[g * BM + tid];
+        p.store_bias(m0 + tid, z, t);
+      }
+    }
   }
 }
 
 template <int BM_, int BN_, int WM_, int WN_, bool AKC, bool BKC, bool BIASA = false, int BK_ = BK16>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NT = 64 * WM_ * WN_, BK = BK_;
-  static constexpr bool A_KC = AKC, B_KC = BKC, BIAS_FROM_A = BIASA, TILE_EPI = false;
+  static constexpr bool A_KC = AKC, B_KC = BKC, BIAS_FROM_A = BIASA, TILE_EPI = false, B_TILE = false;
   struct ACtx { const float* p; int a; int b; bool ok; };
   struct BCtx { const float* p; int a; bool ok; };
 };
 
-// u8 operand as exact integers 0..255; the 1/255 of the decode is folded into
-// the epilogue (forward) or the slab reduce (wgrad): Σ w·u/255 instead of
+// u8 operands are staged as exact integers 0..255 (loaders return the raw
+// uint32_t, to_f32x4 widens it); the 1/255 of the decode is folded into the
+// epilogue (forward) or the slab reduce (wgrad): Σ w·u/255 instead of
 // Σ w·fl(u/255), a ≤ 1-ulp-per-term difference (within the fp32 tolerance of
 // the GEMM's own summation order) for 16 fewer VALU ops per 4 bytes.
-__device__ __forceinline__ f32x4 u8x4(uint32_t u) {
-  return f32x4{(float)(u & 255u), (float)((u >> 8) & 255u), (float)((u >> 16) & 255u), (float)(u >> 24)};
-}
 
 // obs row of minibatch sample b: storage row idx[b] (gather) or row0 + b
 __device__ __forceinline__ long long obs_row(const int64_t* idx, long long row0, int b) {
