@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 #include <stdio.h>
 
 #include "../../include/ppo_hip.h"  // every PPO_API definition must match its declaration
@@ -10,6 +11,31 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// Exact three-way bf16 split of an fp32 value: v == hi + mid + lo (each part
+// rounded to nearest-even from the remaining residual; 3 x 8 significand bits
+// cover fp32's 24).  Used where one GEMM operand is exactly representable in
+// bf16 (u8 pixels): every bf16 x bf16 product is then exact in fp32 and the
+// MFMA accumulates in fp32, i.e. fp32 arithmetic on the bf16 matrix cores.
+__host__ __device__ __forceinline__ uint32_t bf16_rne_bits(float v) {
+  uint32_t u;
+  memcpy(&u, &v, 4);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__host__ __device__ __forceinline__ float bf16_bits_to_f32(uint32_t h) {
+  const uint32_t u = h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+__host__ __device__ __forceinline__ void split_bf16x3(float v, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
+  hi = bf16_rne_bits(v);
+  const float r1 = v - bf16_bits_to_f32(hi);
+  mid = bf16_rne_bits(r1);
+  const float r2 = r1 - bf16_bits_to_f32(mid);
+  lo = bf16_rne_bits(r2);
+}
 
 // Error plumbing: every C-ABI entry point returns 0 on success, a hipError_t
 // value or a library code otherwise; ppo_last_error() returns the message.

@@ -59,6 +59,215 @@ struct Conv1Fwd : C_ {
   }
 };
 
+// conv1 forward, image-resident (u8 observations, C = 4).  One persistent
+// block of 8 waves per CU walks image pairs with two LDS stages of 2 x 28,224 B:
+// while the waves compute the pair in one stage, LDS-DMA loads (gathered by
+// the minibatch index) fill the other, so HBM latency never meets the MFMAs.
+// Wave w computes image (w >> 2), output channels 16 * ((w >> 1) & 1) + [0, 16),
+// row tiles {w & 1, (w & 1) + 2, ...} of 16 output pixels, with
+// v_mfma_f32_16x16x4_f32 fed straight from the image: a lane's im2col fragment
+// is one 4-byte LDS read (4 adjacent kx); the wave's weight fragments stay in
+// registers.  k order inside a 16-deep group: MFMA s takes k = 16q + 4g + s
+// from lane group g = lane >> 4.  No per-k-step staging and no barrier in the
+// k loop.
+template <int C>
+__global__ __launch_bounds__(512) void conv1_fwd_img_kernel(const uint8_t* __restrict__ obs,
+                                                            const int64_t* __restrict__ idx, long long row0, int B,
+                                                            const float* __restrict__ w,
+                                                            const float* __restrict__ bias, float* __restrict__ out) {
+  constexpr int IMGB = C * IMG2, CH = IMGB / 16, K = C * 64, NQ = K / 16, NT = 13;
+  static_assert(IMGB % 16 == 0, "16-B chunks");
+  __shared__ __attribute__((aligned(16))) uint8_t img[2][2 * IMGB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int npairs = (B + 1) / 2;
+  const int im = wave >> 2, ct = (wave >> 1) & 1, half = wave & 1;
+  const int ntile = half ? 12 : 13;   // row tiles half, half + 2, ... < 25
+  const int i16 = lane & 15, g = lane >> 4;
+  const float* wp = w + (size_t)(ct * 16 + i16) * K + 4 * g;
+  const int col = ct * 16 + i16;
+  const float bv = bias[col];
+  f32x4 wreg[NQ];   // this wave's 16 x K weight fragments, resident for the block's lifetime
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) wreg[q] = *reinterpret_cast<const f32x4*>(wp + 16 * q);
+  auto fetch = [&](int pair, uint8_t* dst) {   // LDS-DMA: 64 lanes x 16 B contiguous per instruction
+    const int b0 = 2 * pair, n = B - b0 < 2 ? B - b0 : 2;
+    const uint8_t* s0 = obs + obs_row(idx, row0, b0) * (long long)IMGB;
+    const uint8_t* s1 = n > 1 ? obs + obs_row(idx, row0, b0 + 1) * (long long)IMGB : s0;
+    for (int c0 = wave * 64; c0 < n * CH; c0 += 512) {
+      const int c = c0 + lane;
+      if (c < n * CH) {
+        const uint8_t* src = c < CH ? s0 + 16 * c : s1 + 16 * (c - CH);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                         (__attribute__((address_space(3))) void*)(dst + 16 * c0), 16, 0, 0);
+      }
+    }
+  };
+  int pair = blockIdx.x, cur = 0;
+  if (pair < npairs) fetch(pair, img[0]);
+  __syncthreads();
+  for (; pair < npairs; pair += gridDim.x) {
+    const int nxt = pair + gridDim.x;
+    if (nxt < npairs) fetch(nxt, img[cur ^ 1]);
+    const int b0 = 2 * pair, nimg = B - b0 < 2 ? B - b0 : 2;
+    if (im < nimg) {   // wave-uniform
+      const uint8_t* I = img[cur] + im * IMGB;
+      f32x4 acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = zero4();
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const f32x4 bf = wreg[q];
+        const int k16 = 16 * q + 4 * g;
+        const uint8_t* Iq = I + (k16 >> 6) * IMG2 + ((k16 >> 3) & 7) * IMG + (k16 & 7);
+        f32x4 a[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int row = (half + 2 * t) * 16 + i16, oy = row / 20, ox = row - oy * 20;
+          a[t] = t < ntile ? to_f32x4(*reinterpret_cast<const uint32_t*>(Iq + oy * (4 * IMG) + ox * 4)) : zero4();
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            if (t < ntile) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], bf[s], acc[t], 0, 0, 0);
+      }
+      float* o = out + (size_t)(b0 + im) * (400 * 32) + col;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (t < ntile) {
+          const int rt = half + 2 * t;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[(rt * 16 + 4 * g + r) * 32] = fmaxf(acc[t][r] * (1.0f / 255.0f) + bv, 0.f);
+        }
+    }
+    __syncthreads();   // the next stage has landed; every wave is done with this one
+    cur ^= 1;
+  }
+}
+
+// conv1 forward on the bf16 matrix cores, exact (u8 observations, C = 4).
+// A pixel u in 0..255 is exact in bf16 and W = W_hi + W_mid + W_lo exactly
+// (split_bf16x3), so conv1 = Σ u·W_hi + Σ u·W_mid + Σ u·W_lo where every
+// product is exact in fp32 and v_mfma_f32_16x16x32_bf16 accumulates in fp32:
+// fp32 arithmetic (as exact per product as v_mfma_f32_*_f32), at 3 bf16 MFMAs
+// per 16x16x32 block instead of 8 f32 16x16x4 MFMAs of twice the cycles.
+// One persistent block (8 waves) per CU walks images: the image being computed
+// sits in LDS as bf16 (2 x 28,224 B -> 56,448 B; two stages), the next image is
+// in flight into registers and converted/stored behind the compute.  Wave w:
+// output channels 16 * (w & 1) + [0, 16), row tiles {w >> 1, (w >> 1) + 4, ...}
+// of 16 output pixels.  k-step s covers k = 32s + [0, 32); lane group
+// g = lane >> 4 supplies k = 32s + 8g + j, j = 0..7 — one kx row of the patch,
+// 8 adjacent pixels, so an A fragment is one 16-byte LDS read.
+template <int C>
+__global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __restrict__ obs,
+                                                               const int64_t* __restrict__ idx, long long row0,
+                                                               int B, const float* __restrict__ w,
+                                                               const float* __restrict__ bias,
+                                                               float* __restrict__ out) {
+  constexpr int NPX = C * IMG2, CH = NPX / 16, K = C * 64, KS = K / 32, PER = (CH + 511) / 512, NT = 7;
+  static_assert(NPX % 16 == 0, "16-pixel chunks");
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][NPX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ct = wave & 1, rq = wave >> 1, ntile = rq == 0 ? 7 : 6;
+  const int i16 = lane & 15, g = lane >> 4;
+  const int col = ct * 16 + i16;
+  const float bv = bias[col];
+  // this wave's weight fragments, split once per block: B[k][n] = W[n][k]
+  bf16x8 wf[3][KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const float* wp = w + (size_t)col * K + 32 * s + 8 * g;
+    uint32_t h[8], m[8], l[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) split_bf16x3(wp[j], h[j], m[j], l[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      wf[0][s][j] = __builtin_bit_cast(__bf16, (uint16_t)h[j]);
+      wf[1][s][j] = __builtin_bit_cast(__bf16, (uint16_t)m[j]);
+      wf[2][s][j] = __builtin_bit_cast(__bf16, (uint16_t)l[j]);
+    }
+  }
+  uint4 stage[PER];
+  auto fetch = [&](int b) {   // 16 u8 pixels per chunk -> registers
+    const uint4* src = reinterpret_cast<const uint4*>(obs + obs_row(idx, row0, b) * (long long)NPX);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = tid + 512 * j;
+      if (c < CH) stage[j] = src[c];
+    }
+  };
+  auto put = [&](int buf) {   // u8 -> bf16 (exact: the high half of the fp32 integer), 2 x 16 B stores
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = tid + 512 * j;
+      if (c < CH) {
+        const uint32_t v[4] = {stage[j].x, stage[j].y, stage[j].z, stage[j].w};
+        uint32_t o[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 f = to_f32x4(v[q]);
+          o[2 * q] = __builtin_amdgcn_perm(__float_as_uint(f[1]), __float_as_uint(f[0]), 0x07060302u);
+          o[2 * q + 1] = __builtin_amdgcn_perm(__float_as_uint(f[3]), __float_as_uint(f[2]), 0x07060302u);
+        }
+        uint4* d = reinterpret_cast<uint4*>(img[buf] + 16 * c);
+        d[0] = uint4{o[0], o[1], o[2], o[3]};
+        d[1] = uint4{o[4], o[5], o[6], o[7]};
+      }
+    }
+  };
+  const int G = gridDim.x;
+  int b = blockIdx.x, cur = 0;
+  if (b < B) {
+    fetch(b);
+    put(0);
+    if (b + G < B) fetch(b + G);
+  }
+  __syncthreads();
+  for (; b < B; b += G) {
+    if (b + G < B) put(cur ^ 1);          // read two iterations ago; the last barrier retired it
+    if (b + 2 * G < B) fetch(b + 2 * G);
+    const uint16_t* I = img[cur];
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = zero4();
+    int pix[NT];   // pixel offset of this lane's output row, per row tile
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int row = (rq + 4 * t) * 16 + i16, oy = row / 20, ox = row - oy * 20;
+      pix[t] = oy * (4 * IMG) + ox * 4;
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k0 = 32 * s + 8 * g;
+      const uint16_t* Is = I + (k0 >> 6) * IMG2 + ((k0 >> 3) & 7) * IMG;
+      bf16x8 a[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (t < ntile) {
+          const uint2* p2 = reinterpret_cast<const uint2*>(Is + pix[t]);   // 8-B aligned: 4ox bf16
+          const uint2 lo = p2[0], hi = p2[1];
+          const uint4 v = uint4{lo.x, lo.y, hi.x, hi.y};
+          a[t] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+      for (int part = 0; part < 3; ++part)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          if (t < ntile) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t], wf[part][s], acc[t], 0, 0, 0);
+    }
+    float* o = out + (size_t)b * (400 * 32) + col;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      if (t < ntile) {
+        const int rt = rq + 4 * t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[(rt * 16 + 4 * g + r) * 32] = fmaxf(acc[t][r] * (1.0f / 255.0f) + bv, 0.f);
+      }
+    __syncthreads();   // every wave is done with img[cur]; img[cur ^ 1] is complete
+    cur ^= 1;
+  }
+}
+
 // NHWC conv (conv2, conv3): k = (ky, kx, ci), weights packed [COUT][K]
 template <int HIN, int CIN, int KS, int ST, int HOUT, int COUT, class C_>
 struct ConvFwd : C_ {
@@ -382,6 +591,29 @@ PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, lo
   const double fl = 2.0 * M * 32 * C * 64;
 #define SETUP1(T_)                                                                                 \
   p.obs = (const T_*)obs; p.idx = idx; p.row0 = row0; p.C = C; p.M = (int)M; p.w = w1; p.bias = b1; p.out = out
+  if (obs_is_u8 && C == 4 && g_tune[tk] != 9) {
+    if (B == 0) return 0;
+    static int n_cu = 0;
+    if (!n_cu) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+        n_cu = 256;
+    }
+    const int npairs = (B + 1) / 2;
+    const unsigned blocks = (unsigned)(npairs < n_cu ? npairs : n_cu);   // persistent, one per CU
+    int slot;
+    const bool prof = ppo_prof_begin("conv1_fwd_u8", as_stream(stream), &slot);
+    if (g_tune[tk] == 8) {
+      conv1_fwd_img_kernel<4><<<blocks, 512, 0, as_stream(stream)>>>((const uint8_t*)obs, idx, row0, B, w1, b1, out);
+    } else {
+      const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+      conv1_fwd_bf16x3_kernel<4><<<nb, 512, 0, as_stream(stream)>>>((const uint8_t*)obs, idx, row0, B, w1, b1, out);
+    }
+    if (prof) ppo_prof_end(slot, as_stream(stream), fl);
+    PPO_LAUNCH_CHECK("conv1_fwd_u8 (image-resident)");
+    return 0;
+  }
   if (obs_is_u8) {
 #define T1(C_) Conv1Fwd<uint8_t, C_>
     PPO_VARIANTS32(T1, SETUP1(uint8_t), M, 32, 1, "conv1_fwd_u8", fl)

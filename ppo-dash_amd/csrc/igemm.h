@@ -76,7 +76,16 @@ __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
   using TB = Tile<BN, P::B_KC, BK>;
   constexpr int NVA = (TA::NV4 + NT - 1) / NT, NVB = (TB::NV4 + NT - 1) / NT;
   constexpr int STAGE = TA::SIZE + TB::SIZE;
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+#ifndef PPO_GEMM_STAGES
+#define PPO_GEMM_STAGES 2
+#endif
+  // 2: double-buffered LDS, fragments read at the start of each 8-deep k group.
+  // 3: triple-buffered LDS; a wave reads the next k group's fragments (across
+  //    the k-tile boundary too: tile t+1 is already staged) while its MFMAs on
+  //    the current group run, so LDS latency never sits in front of an MFMA.
+  constexpr int NS = PPO_GEMM_STAGES;
+  static_assert(NS == 2 || NS == 3, "stages");
+  __shared__ __attribute__((aligned(16))) float smem[NS * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -160,17 +169,8 @@ __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   float bias_acc = 0.f;
 
-  if (nk > 0) {
-    gload(kbeg);
-    sstore(0);
-  }
-  __syncthreads();
   const int frow = lane & 31, fk = 4 * (lane >> 5);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload(kbeg + (kt + 1) * BK);
-    const float* As = smem + buf * STAGE;
-    const float* Bs = As + TA::SIZE;
+  auto bias_part = [&](const float* As) {
     if constexpr (P::BIAS_FROM_A) {
       // db partial: every thread sums BK/G rows of one A-tile column
       static_assert(!P::A_KC && NT % BM == 0 && BK % (NT / BM) == 0, "bias partials");
@@ -180,23 +180,80 @@ __global__ __launch_bounds__(P::NT) void igemm_kernel(const P p) {
         for (int k = tid / BM; k < BK; k += G) bias_acc += As[k * BM + tid % BM];
       }
     }
+  };
+  auto read_frags = [&](const float* As, int kb, f32x4 (&af)[TM], f32x4 (&bf)[TN]) {
+    const float* Bs = As + TA::SIZE;
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 8) {
-      f32x4 af[TM], bf[TN];
+    for (int i = 0; i < TM; ++i) af[i] = frag<BM, P::A_KC, BK>(As, (wm * TM + i) * 32 + frow, kb + fk);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag<BM, P::A_KC, BK>(As, (wm * TM + i) * 32 + frow, kk + fk);
+    for (int j = 0; j < TN; ++j) bf[j] = frag<BN, P::B_KC, BK>(Bs, (wn * TN + j) * 32 + frow, kb + fk);
+  };
+  auto mfma_group = [&](const f32x4 (&af)[TM], const f32x4 (&bf)[TN]) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = frag<BN, P::B_KC, BK>(Bs, (wn * TN + j) * 32 + frow, kk + fk);
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+  };
+
+  if constexpr (NS == 2) {
+    if (nk > 0) {
+      gload(kbeg);
+      sstore(0);
     }
-    if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) gload(kbeg + (kt + 1) * BK);
+      const float* As = smem + buf * STAGE;
+      bias_part(As);
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 8) {
+        f32x4 af[TM], bf[TN];
+        read_frags(As, kk, af, bf);
+        mfma_group(af, bf);
+      }
+      if (kt + 1 < nk) sstore(buf ^ 1);
+      __syncthreads();
+    }
+  } else {
+    // tile t lives in buffer t % 3; tile t+2 is loaded during step t and
+    // staged at its end; the barrier closing step t-1 published tile t+1 and
+    // retired every read of buffer (t+2) % 3.
+    if (nk > 0) {
+      gload(kbeg);
+      sstore(0);
+    }
+    if (nk > 1) {
+      gload(kbeg + BK);
+      sstore(1);
+    }
+    __syncthreads();
+    f32x4 fa[TM], fb[TN];
+    if (nk > 0) read_frags(smem, 0, fa, fb);
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int nxt = cur == 2 ? 0 : cur + 1, stg = nxt == 2 ? 0 : nxt + 1;
+      if (kt + 2 < nk) gload(kbeg + (kt + 2) * BK);
+      const float* As = smem + cur * STAGE;
+      bias_part(As);
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 8) {
+        f32x4 ga[TM], gb[TN];
+        if (kk + 8 < BK) read_frags(As, kk + 8, ga, gb);
+        else if (kt + 1 < nk) read_frags(smem + nxt * STAGE, 0, ga, gb);
+        mfma_group(fa, fb);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = ga[i];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = gb[j];
+      }
+      if (kt + 2 < nk) sstore(stg);
+      __syncthreads();
+      cur = nxt;
+    }
   }
 
   const int hi = lane >> 5;
