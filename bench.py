@@ -35,7 +35,24 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "env-steps/sec (rollout+GAE+PPO update) at 4096 envs×128 steps, 1/2/4/8 MI355X"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA = vector peak (dense)
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 PEAK_HBM_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+# The kernels timed with HIP events inside the timed region, and the roofline
+# that bounds each one.  "work" is algorithmic fp32 FLOP per
+# launch (2·M·N·K of the layer); for the exact-split bf16 kernels the matrix
+# cores execute 3 (u8 operand) or 9 bf16 products per fp32 product, so their
+# MFMA ceiling is the bf16 peak / 3 or / 9 in fp32-FLOP units.
+PROFILED = {
+    "conv2_dgrad": ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"),
+    "conv1_wgrad_u8": ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"),
+    "conv2_wgrad": ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"),
+    "conv2_fwd": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9, "v_mfma_f32_16x16x32_bf16 x9 (exact split)"),
+    # conv1 forward: 79,424 B of compulsory HBM traffic per sample (28,224 B u8 in, 51,200 B f32 out)
+    # against 6.55 MFLOP at bf16/3 -> HBM-bound
+    "conv1_fwd_u8": ("hbm", PEAK_HBM_GBPS, "v_mfma_f32_16x16x32_bf16 x3 (u8 exact), image-resident"),
+}
+CONV1_FWD_BYTES_PER_FLOP = 79424.0 / (2.0 * 400 * 32 * 256)
 
 
 def parse():
@@ -50,7 +67,8 @@ def parse():
     p.add_argument("--hidden", type=int, default=None, help="default 512 (CNN) / 256 (GRU)")
     p.add_argument("--recurrent", action="store_true", help="c5: GRU policy + vector obs")
     p.add_argument("--vec-len", type=int, default=14, help="vector obs length with --recurrent (OTC v7: 14)")
-    p.add_argument("--profile-kernel", default="conv1_fwd_u8")
+    p.add_argument("--profile-kernels", default=",".join(PROFILED),
+                   help="kernels timed with HIP events; the one with the most time is the roofline kernel")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-envs", type=int, default=32)
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -185,7 +203,8 @@ def main():
         gae = gae_roofline(device, args.gae_lanes)
 
     cap = args.steps * (T + 2 * E * M + 8) + 16
-    _hip.call("ppo_prof_enable", args.profile_kernel.encode(), cap)
+    names = [k for k in args.profile_kernels.split(",") if k]
+    _hip.call("ppo_prof_enable", ",".join(names).encode(), cap * len(names))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -197,8 +216,11 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    prof = (torch.zeros(3, dtype=torch.float64))
-    _hip.call("ppo_prof_collect", prof.data_ptr())
+    per_kernel = {}
+    for ki, name in enumerate(names):
+        prof = torch.zeros(3, dtype=torch.float64)
+        _hip.call("ppo_prof_collect_one", ki, prof.data_ptr())
+        per_kernel[name] = prof.tolist()
     _hip.call("ppo_prof_enable", None, 0)
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
@@ -208,21 +230,33 @@ def main():
         dist.destroy_process_group()
         return
 
-    launches, ms_total, flops = prof.tolist()
     workload = ((f"c5: CNNBase+GRU H={H} + {V} vector obs" if args.recurrent else f"c3: CNNBase H={H}")
                 + f", {N} env lanes x {T} steps per GPU, PPO {E} epochs x {M} minibatches "
                   f"(rollout + GAE + update, fp32)")
-    roof = None
-    if launches > 0 and ms_total > 0:
+    kernels = {}
+    for name, (launches, ms_total, flops) in per_kernel.items():
+        if launches <= 0 or ms_total <= 0:
+            continue
+        bound, peak, how = PROFILED.get(name, ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"))
         tflops = flops / (ms_total * 1e-3) / 1e12
-        traffic, tsrc = pmc_traffic(args.profile_kernel, workload)
-        roof = {"bound": "mfma", "achieved": round(tflops, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(tflops / PEAK_FP32_MFMA_TFLOPS, 4),
-                "traffic": round(traffic) if traffic else None, "traffic_unit": "bytes/launch (HBM, PMC)",
-                "traffic_source": tsrc,
-                "kernel": args.profile_kernel, "launches": int(launches),
-                "avg_launch_ms": round(ms_total / launches, 4),
-                "flop_per_launch": round(flops / launches)}
+        if bound == "hbm":
+            achieved, unit = flops * CONV1_FWD_BYTES_PER_FLOP / (ms_total * 1e-3) / 1e9, "GB/s"
+        else:
+            achieved, unit = tflops, "TFLOP/s"
+        kernels[name] = {"bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": unit,
+                         "frac": round(achieved / peak, 4), "ms_total": round(ms_total, 2),
+                         "launches": int(launches), "avg_launch_ms": round(ms_total / launches, 4),
+                         "fp32_tflops": round(tflops, 2), "instructions": how}
+    roof = None
+    if kernels:
+        dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
+        kd = kernels[dom]
+        traffic, tsrc = pmc_traffic(dom, workload)
+        roof = {"bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"], "unit": kd["unit"],
+                "frac": kd["frac"], "traffic": round(traffic) if traffic else None,
+                "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tsrc, "kernel": dom,
+                "launches": kd["launches"], "avg_launch_ms": kd["avg_launch_ms"],
+                "flop_per_launch": round(per_kernel[dom][2] / per_kernel[dom][0])}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_envs, T, E, M, H, args.cpu_threads)
@@ -235,7 +269,7 @@ def main():
         "config": {"workload": workload,
                    "envs_per_gpu": N, "num_steps": T, "ppo_epoch": E, "num_mini_batch": M, "hidden": H,
                    "global_batch": N * T * world, "parallelism": f"dp{world}"},
-        "roofline": roof, "cpu_baseline": cpu, "gae_roofline": gae,
+        "roofline": roof, "cpu_baseline": cpu, "gae_roofline": gae, "kernel_rooflines": kernels,
         "losses": [round(x, 6) for x in losses],
     }
     print(json.dumps(out))

@@ -35,8 +35,9 @@ const char* ppo_last_error(void);
 int ppo_abi_version(void);
 /* launch-level event profiler used by bench.py: time every launch of the named
  * kernel (NULL disables); collect -> {launches, Σ ms, Σ algorithmic FLOP} */
-int ppo_prof_enable(const char* name, int capacity);
-int ppo_prof_collect(double* out3);
+int ppo_prof_enable(const char* names, int capacity);   /* comma-separated kernel names */
+int ppo_prof_collect(double* out3);                       /* all listed: {launches, ms, work} */
+int ppo_prof_collect_one(int idx, double* out3);          /* the idx-th listed name only */
 
 /* ---------------- returns / advantages ------------------------------------ */
 /* storage.py:82-121 RolloutStorage.compute_returns (all four branches,
@@ -86,7 +87,8 @@ int ppo_cartpole_step(float* state, int* steps, const int64_t* action, float* ob
 /* ---------------- CNNBase trunk (model.py:176-180) ------------------------- */
 long long ppo_packed_weights_size(int H);
 int ppo_packed_offsets(int H, long long* off6);
-/* once per optimizer step: torch-layout conv2/conv3/fc weights -> loader orders */
+/* once per optimizer step: torch-layout conv2/conv3/fc weights -> loader orders; every packed f32
+ * segment is followed by its exact bf16 split (hi, mid, lo planes), the B operand of the bf16 cores */
 int ppo_pack_weights(const float* w2, const float* w3, const float* w4, int H, float* packed, void* stream);
 /* model.py:177 Conv2d(C,32,8,s4)+ReLU over obs rows (idx: storage-row gather,
  * storage.py:143; NULL: rows row0..row0+B-1); u8 staged as integers, 1/255 applied
@@ -98,6 +100,9 @@ int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, flo
 /* model.py:179 Conv2d(64,32,3,s1)+ReLU */
 int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream);
 /* model.py:180 Linear(1568,H)+ReLU (generic Linear+ReLU) */
+/* model.py:181 CNNBase fc + ReLU from the packed W4p segment (ppo_pack_weights; its bf16 planes follow it):
+ * out[m * ldo + n] = relu(x[m] · W4p[n] + b[n]), x [M][1568] (p, c) order */
+int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, int H, float* out, int ldo, void* stream);
 int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, const float* b, int N, float* out,
                         void* stream);
 /* Linear with row strides, optional A-row gather, bias and activation

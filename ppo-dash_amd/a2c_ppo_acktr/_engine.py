@@ -145,8 +145,7 @@ class CNNEngine:
              self.pv(self.B1), a1.data_ptr(), s)
         call("ppo_conv2_fwd", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), s)
         call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
-        call("ppo_linear_fwd_ex", a3.data_ptr(), None, B, FEAT, FEAT, self.pk(2), self.pv(self.B4), self.H,
-             out.data_ptr(), ldo, 1, s)
+        call("ppo_fc_fwd", a3.data_ptr(), B, self.pk(2), self.pv(self.B4), self.H, out.data_ptr(), ldo, s)
         return out
 
     def _check_obs(self, obs):

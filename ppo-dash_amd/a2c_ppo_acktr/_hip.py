@@ -21,6 +21,7 @@ SIGNATURES = {
     "ppo_last_error": [],
     "ppo_prof_enable": [ctypes.c_char_p, c_int],
     "ppo_prof_collect": [c_p],
+    "ppo_prof_collect_one": [c_int, c_p],
     # gae.hip
     "ppo_gae_partials_count": [c_int],
     "ppo_compute_returns": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_d, c_d, c_int, c_int, c_p],
@@ -44,6 +45,7 @@ SIGNATURES = {
     "ppo_conv2_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv3_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_linear_relu_fwd": [c_p, c_int, c_int, c_p, c_p, c_int, c_p, c_p],
+    "ppo_fc_fwd": [c_p, c_int, c_p, c_p, c_int, c_p, c_int, c_p],
     "ppo_linear_dgrad_mask": [c_p, c_int, c_int, c_p, c_int, c_p, c_p, c_p],
     "ppo_conv3_dgrad": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv2_dgrad": [c_p, c_int, c_p, c_p, c_p, c_p],

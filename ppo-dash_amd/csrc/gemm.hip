@@ -23,6 +23,7 @@
 // as 4 ds_read_b32); the 4 k values of a lane feed 4 successive MFMAs, so the
 // physical k order inside a BK=16 step is a fixed permutation common to A and B.
 #include "igemm.h"
+#include "igemm_x9.h"
 
 namespace {
 // ---------------------------------------------------------------------------
@@ -424,38 +425,56 @@ struct ConvWgrad : WgradBase<C_> {
 //   W2p [64][512]  (ky,kx,ci)       W3p [32][576] (ky,kx,ci)
 //   W4p [H][1568]  (p,c)            W4T [1568][H] (p,c) x n
 //   W3d [64][288]  ci x (ky,kx,co)  W2d [4][32][256] phase x ci x (ty,tx,co)
+// Each f32 segment of n values is followed by its exact bf16 split (hi, mid, lo
+// planes of n bf16 each = 1.5 n floats), the B operand of the igemm_x9 core.
+__host__ __device__ inline void pack_segments(int H, long long* n) {
+  n[0] = 64 * 512; n[1] = 32 * 576; n[2] = (long long)H * 1568; n[3] = n[2]; n[4] = 64 * 288; n[5] = 4 * 32 * 256;
+}
+
 __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restrict__ w2, const float* __restrict__ w3,
                                                            const float* __restrict__ w4, int H,
                                                            float* __restrict__ out) {
-  const long long n2 = 64 * 512, n3 = 32 * 576, n4 = (long long)H * 1568, n3d = 64 * 288, n2d = 4 * 32 * 256;
-  const long long total = n2 + n3 + 2 * n4 + n3d + n2d;
+  long long n[6];
+  pack_segments(H, n);
+  const long long total = n[0] + n[1] + n[2] + n[3] + n[4] + n[5];
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    long long j = i;
+    long long j = i, base = 0;
+    int seg = 0;
+    while (j >= n[seg]) {
+      j -= n[seg];
+      base += n[seg] * 5 / 2;
+      ++seg;
+    }
     float v;
-    if (j < n2) {
+    if (seg == 0) {
       const int co = (int)(j / 512), k = (int)(j % 512), ky = k / 128, kx = (k / 32) % 4, ci = k % 32;
       v = w2[co * 512 + ci * 16 + ky * 4 + kx];
-    } else if ((j -= n2) < n3) {
+    } else if (seg == 1) {
       const int co = (int)(j / 576), k = (int)(j % 576), ky = k / 192, kx = (k / 64) % 3, ci = k % 64;
       v = w3[co * 576 + ci * 9 + ky * 3 + kx];
-    } else if ((j -= n3) < n4) {
-      const long long n = j / 1568;
+    } else if (seg == 2) {
+      const long long nn = j / 1568;
       const int k = (int)(j % 1568), pp = k / 32, c = k % 32;
-      v = w4[n * 1568 + c * 49 + pp];
-    } else if ((j -= n4) < n4) {
-      const int k = (int)(j / H), n = (int)(j % H), pp = k / 32, c = k % 32;
-      v = w4[(long long)n * 1568 + c * 49 + pp];
-    } else if ((j -= n4) < n3d) {
+      v = w4[nn * 1568 + c * 49 + pp];
+    } else if (seg == 3) {
+      const int k = (int)(j / H), nn = (int)(j % H), pp = k / 32, c = k % 32;
+      v = w4[(long long)nn * 1568 + c * 49 + pp];
+    } else if (seg == 4) {
       const int ci = (int)(j / 288), k = (int)(j % 288), ky = k / 96, kx = (k / 32) % 3, co = k % 32;
       v = w3[co * 576 + ci * 9 + ky * 3 + kx];
     } else {
-      j -= n3d;
       const int ph = (int)(j / 8192), rem = (int)(j % 8192), ci = rem / 256, k = rem % 256;
       const int ty = k >> 7, tx = (k >> 6) & 1, co = k & 63;
       const int ky = (ph >> 1) + 2 * ty, kx = (ph & 1) + 2 * tx;
       v = w2[co * 512 + ci * 16 + ky * 4 + kx];
     }
-    out[i] = v;
+    out[base + j] = v;
+    uint32_t h, m, l;
+    split_bf16x3(v, h, m, l);
+    uint16_t* pl = reinterpret_cast<uint16_t*>(out + base + n[seg]);
+    pl[j] = (uint16_t)h;
+    pl[n[seg] + j] = (uint16_t)m;
+    pl[2 * n[seg] + j] = (uint16_t)l;
   }
 }
 
@@ -469,24 +488,32 @@ using CfgN64s = Cfg<256, 64, 4, 1, true, true>;
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+// floats: every segment is followed by its three bf16 planes (1.5 x its size)
 PPO_API long long ppo_packed_weights_size(int H) {
-  return 64LL * 512 + 32 * 576 + 2LL * H * 1568 + 64 * 288 + 4 * 32 * 256;
+  long long n[6];
+  pack_segments(H, n);
+  return (n[0] + n[1] + n[2] + n[3] + n[4] + n[5]) * 5 / 2;
 }
 
-// offsets (floats) of the packed segments inside the pack buffer
+// offsets (floats) of the packed f32 segments W2p W3p W4p W4T W3d W2d inside the pack buffer
 PPO_API int ppo_packed_offsets(int H, long long* off6) {
-  off6[0] = 0;                         // W2p
-  off6[1] = off6[0] + 64 * 512;        // W3p
-  off6[2] = off6[1] + 32 * 576;        // W4p
-  off6[3] = off6[2] + (long long)H * 1568;  // W4T
-  off6[4] = off6[3] + (long long)H * 1568;  // W3d
-  off6[5] = off6[4] + 64 * 288;        // W2d
+  long long n[6];
+  pack_segments(H, n);
+  off6[0] = 0;
+  for (int i = 1; i < 6; ++i) off6[i] = off6[i - 1] + n[i - 1] * 5 / 2;
   return 0;
+}
+
+// bf16 planes of a packed segment of n floats (they follow it)
+static inline const uint16_t* planes_of(const float* seg, long long n) {
+  return reinterpret_cast<const uint16_t*>(seg + n);
 }
 
 PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, int H, float* packed, void* stream) {
   PPO_REQUIRE(H > 0 && H % 4 == 0, "ppo_pack_weights: hidden size %d must be a positive multiple of 4", H);
-  const long long total = ppo_packed_weights_size(H);
+  long long n[6];
+  pack_segments(H, n);
+  const long long total = n[0] + n[1] + n[2] + n[3] + n[4] + n[5];
   long long b = (total + 255) / 256;
   pack_weights_kernel<<<(unsigned)(b < 2048 ? b : 2048), 256, 0, as_stream(stream)>>>(w2, w3, w4, H, packed);
   PPO_LAUNCH_CHECK("pack_weights_kernel");
@@ -497,10 +524,12 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // Tile-configuration variants (A/B knobs for tools/kbench.py; defaults are the
 // measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
 // ---------------------------------------------------------------------------
-enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_N };
+enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_X9,
+       TK_N };
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
-                                         "fc_fwd", "conv2_fwd"};
-static int g_tune[TK_N] = {0, 3, 3, 1, 1, 0, 0};  // measured best (kbench sweep, profiles/)
+                                         "fc_fwd", "conv2_fwd", "x9"};
+// x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
+static int g_tune[TK_N] = {0, 3, 3, 1, 1, 0, 0, 1};  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   for (int i = 0; i < TK_N; ++i)
@@ -545,6 +574,25 @@ using V128_3 = Cfg<64, 128, 2, 2, true, true>;            // 2x2 waves of 32x64,
     case 3: { TEMPL(V128_3) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
     default: { TEMPL(V128_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
   }
+
+// exact-split bf16 core (igemm_x9.h)
+using X32 = CfgX<128, 32, 4, 1, true, true>;          // N = 32: waves of 32x32
+using X64 = CfgX<128, 64, 2, 2, true, true>;          // N = 64: waves of 64x32
+using X128 = CfgX<128, 128, 2, 2, true, true>;        // N >= 128: waves of 64x64
+using XW32 = CfgX<32, 128, 1, 4, false, false, true>;   // wgrad, 32 output channels
+using XW64 = CfgX<64, 128, 2, 2, false, false, true>;   // wgrad, 64 output channels
+using XW128 = CfgX<128, 128, 2, 2, false, false, true>; // wgrad, >= 128 output channels
+using XP32 = CfgX<128, 32, 4, 1, true, true, false, false, false, true>;    // B from planes, waves 32x32
+using XP64 = CfgX<128, 64, 4, 1, true, true, false, false, false, true>;    // waves 32x64
+using XP128 = CfgX<128, 128, 4, 1, true, true, false, false, false, true>;  // waves 32x128
+// x9 = 1: the split-bf16 core where it measured faster (forward GEMMs, fc dgrad); the gather-heavy
+// conv dgrads and the wgrads stay on fp32 MFMA (their split path is VALU-bound); x9 = 2: everywhere
+static inline bool use_x9() { return g_tune[TK_X9] != 0; }
+static inline bool use_x9_all() { return g_tune[TK_X9] == 2; }
+template <class P>
+static inline void set_planes(P& p, const float* seg, long long n, int rows, int K) {
+  p.bpl = planes_of(seg, n); p.bps = n; p.bld = K; p.bnr = rows;
+}
 
 // dense-core experiments (fc forward, N multiple of 128; conv2 forward, N = 64)
 using VD_1 = Cfg<128, 128, 2, 2, true, true, false, 32>;  // BK 32
@@ -626,6 +674,12 @@ PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, lo
 }
 
 PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream) {
+  if (use_x9()) {
+    ConvFwd<20, 32, 4, 2, 9, 64, XP64> p;
+    p.in = a1; p.w = w2p; p.bias = b2; p.out = out; p.M = B * 81;
+    set_planes(p, w2p, 64 * 512, 64, 512);
+    return launch_x9(p, (long long)B * 81, 64, 1, as_stream(stream), "conv2_fwd", 2.0 * B * 81 * 64 * 512);
+  }
   const int tk = TK_CONV2_FWD;
 #define T2(C_) ConvFwd<20, 32, 4, 2, 9, 64, C_>
   PPO_VARIANTS_C2F(T2, (p.in = a1, p.w = w2p, p.bias = b2, p.out = out, p.M = B * 81), (long long)B * 81, 64, 1,
@@ -634,6 +688,12 @@ PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float*
 }
 
 PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream) {
+  if (use_x9()) {
+    ConvFwd<9, 64, 3, 1, 7, 32, XP32> p;
+    p.in = a2; p.w = w3p; p.bias = b3; p.out = out; p.M = B * 49;
+    set_planes(p, w3p, 32 * 576, 32, 576);
+    return launch_x9(p, (long long)B * 49, 32, 1, as_stream(stream), "conv3_fwd", 2.0 * B * 49 * 32 * 576);
+  }
   const int tk = TK_CONV3_FWD;
 #define T3(C_) ConvFwd<9, 64, 3, 1, 7, 32, C_>
   PPO_VARIANTS32(T3, (p.in = a2, p.w = w3p, p.bias = b3, p.out = out, p.M = B * 49), (long long)B * 49, 32, 1,
@@ -641,10 +701,32 @@ PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float*
 #undef T3
 }
 
+// CNNBase fc (model.py:181): out[m * ldo + n] = relu(x [M][1568] · W4p [H][1568]^T + b), W4p the packed
+// segment of ppo_pack_weights (its bf16 planes follow it)
+PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, int H, float* out, int ldo,
+                       void* stream) {
+  PPO_REQUIRE(H > 0 && H % 8 == 0 && ldo >= H, "ppo_fc_fwd: H=%d ldo=%d", H, ldo);
+  const int K = 1568;
+  if (use_x9()) {
+    DenseReluFwd<XP128> p;
+    p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1;
+    set_planes(p, w4p, (long long)H * K, H, K);
+    return launch_x9(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);
+  }
+  DenseReluFwd<CfgN128> p;
+  p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1;
+  return launch(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);
+}
+
 // Linear + ReLU: out [M][N] = relu(x [M][K] · w [N][K]^T + b)
 PPO_API int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, const float* b, int N, float* out,
                                 void* stream) {
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_relu_fwd: K=%d must be a multiple of 4", K);
+  if (use_x9()) {
+    DenseReluFwd<X128> p;
+    p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K;
+    return launch_x9(p, M, N, 1, as_stream(stream), "linear_relu_fwd", 2.0 * M * N * K);
+  }
   if (N % 128 == 0) {
     const int tk = TK_FC_FWD;
 #define TF(C_) DenseReluFwd<C_>
@@ -663,6 +745,18 @@ PPO_API int ppo_linear_fwd_ex(const float* x, const int64_t* idx, int M, int K, 
                               int N, float* out, int ldo, int act, void* stream) {
   PPO_REQUIRE(K % 4 == 0 && lda % 4 == 0, "ppo_linear_fwd_ex: K=%d lda=%d must be multiples of 4", K, lda);
   PPO_REQUIRE(act >= 0 && act <= 2, "ppo_linear_fwd_ex: act=%d", act);
+  if (use_x9()) {
+    if (N <= 64) {
+      DenseReluFwd<X64> p;
+      p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = act;
+      p.idx = idx;
+      return launch_x9(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);
+    }
+    DenseReluFwd<X128> p;
+    p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = act;
+    p.idx = idx;
+    return launch_x9(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);
+  }
   if (N % 128 == 0) {
     DenseReluFwd<CfgN128> p;
     p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = act;
@@ -680,6 +774,11 @@ PPO_API int ppo_linear_fwd_ex(const float* x, const int64_t* idx, int M, int K, 
 PPO_API int ppo_linear_dgrad_ex(const float* dy, int M, int K, const float* wt, int N, const float* act, int ldact,
                                 int mode, float* dx, void* stream) {
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_dgrad_ex: K=%d must be a multiple of 4", K);
+  if (use_x9()) {
+    DenseDgradMask<X128> p;
+    p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K; p.ldact = ldact; p.mode = mode;
+    return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_ex", 2.0 * M * N * K);
+  }
   DenseDgradMask<CfgN128> p;
   p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K; p.ldact = ldact; p.mode = mode;
   return launch(p, M, N, 1, as_stream(stream), "linear_dgrad_ex", 2.0 * M * N * K);
@@ -707,12 +806,25 @@ PPO_API int ppo_transpose(const float* src, int rows, int cols, float* dst, void
 PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
                                   void* stream) {
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 4", K);
+  if (use_x9()) {   // wt = the packed W4T segment [1568][H] (planes follow)
+    PPO_REQUIRE(K % 8 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 8", K);
+    DenseDgradMask<XP128> p;
+    p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;
+    set_planes(p, wt, (long long)N * K, N, K);
+    return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);
+  }
   DenseDgradMask<CfgN128> p;
   p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;
   return launch(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);
 }
 
 PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream) {
+  if (use_x9_all()) {
+    ConvDgradS1<9, 64, 3, 7, 32, XP64> p;
+    p.dy = dz3; p.wd = w3d; p.act = a2; p.dx = dz2; p.M = B * 81;
+    set_planes(p, w3d, 64 * 288, 64, 288);
+    return launch_x9(p, (long long)B * 81, 64, 1, as_stream(stream), "conv3_dgrad", 2.0 * B * 49 * 32 * 576);
+  }
   const int tk = TK_CONV3_DGRAD;
 #define TD3(C_) ConvDgradS1<9, 64, 3, 7, 32, C_>
   PPO_VARIANTS64(TD3, (p.dy = dz3, p.wd = w3d, p.act = a2, p.dx = dz2, p.M = B * 81), (long long)B * 81, 64, 1,
@@ -721,6 +833,12 @@ PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const flo
 }
 
 PPO_API int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const float* a1, float* dz1, void* stream) {
+  if (use_x9_all()) {
+    Conv2Dgrad<XP128> p;
+    p.dy = dz2; p.wd = w2d; p.act = a1; p.dx = dz1; p.M = B * 100;
+    set_planes(p, w2d, 128 * 256, 128, 256);
+    return launch_x9(p, (long long)B * 100, 128, 1, as_stream(stream), "conv2_dgrad", 2.0 * B * 81 * 64 * 512);
+  }
   const int tk = TK_CONV2_DGRAD;
 #define TD2(C_) Conv2Dgrad<C_>
   PPO_VARIANTS128(TD2, (p.dy = dz2, p.wd = w2d, p.act = a1, p.dx = dz1, p.M = B * 100), (long long)B * 100, 128, 1,
@@ -739,9 +857,10 @@ PPO_API int ppo_wgrad_splits(long long R, int tiles, int target_blocks, int min_
   return (int)z;
 }
 
+// chunks are multiples of 32 rows: whole k-tiles of both cores (BK 16 and 32)
 static inline int wgrad_chunk(long long R, int Z) {
-  long long kt = (R + BK16 - 1) / BK16;
-  return (int)(((kt + Z - 1) / Z) * BK16);
+  long long kt = (R + 31) / 32;
+  return (int)(((kt + Z - 1) / Z) * 32);
 }
 
 template <class P>
@@ -781,6 +900,12 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
 
 PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, float* slab, float* slab_bias,
                             void* stream) {
+  if (use_x9_all()) {
+    ConvWgrad<20, 32, 4, 2, 9, XW64> p;
+    set_wgrad(p, dz2, 64, (long long)B * 81, Z, slab, slab_bias, 512);
+    p.in = a1;
+    return launch_x9(p, 64, 512, Z, as_stream(stream), "conv2_wgrad", 2.0 * B * 81 * 64 * 512);
+  }
   ConvWgrad<20, 32, 4, 2, 9, CfgW64> p;
   set_wgrad(p, dz2, 64, (long long)B * 81, Z, slab, slab_bias, 512);
   p.in = a1;
@@ -789,6 +914,12 @@ PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, flo
 
 PPO_API int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, float* slab, float* slab_bias,
                             void* stream) {
+  if (use_x9_all()) {
+    ConvWgrad<9, 64, 3, 1, 7, XW32> p;
+    set_wgrad(p, dz3, 32, (long long)B * 49, Z, slab, slab_bias, 576);
+    p.in = a2;
+    return launch_x9(p, 32, 576, Z, as_stream(stream), "conv3_wgrad", 2.0 * B * 49 * 32 * 576);
+  }
   ConvWgrad<9, 64, 3, 1, 7, CfgW32b> p;
   set_wgrad(p, dz3, 32, (long long)B * 49, Z, slab, slab_bias, 576);
   p.in = a2;
@@ -799,6 +930,18 @@ PPO_API int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, flo
 PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int K, int Z, float* slab,
                              float* slab_bias, void* stream) {
   PPO_REQUIRE(N % 4 == 0 && K % 4 == 0, "ppo_linear_wgrad: N=%d K=%d must be multiples of 4", N, K);
+  if (use_x9_all()) {
+    if (N <= 64) {
+      DenseWgrad<XW64> p;
+      set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);
+      p.x = x; p.K = K;
+      return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K);
+    }
+    DenseWgrad<XW128> p;
+    set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);
+    p.x = x; p.K = K;
+    return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K);
+  }
   DenseWgrad<CfgWfc> p;
   set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);
   p.x = x; p.K = K;

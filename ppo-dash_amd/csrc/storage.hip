@@ -26,15 +26,35 @@ void ppo_set_error(const char* fmt, ...) {
 PPO_API const char* ppo_last_error(void) { return g_err; }
 
 // ---------------------------------------------------------------- profiler
-static char g_prof_name[64] = "";
+// HIP events around the launches of the named kernels (comma-separated list),
+// on the stream each launch goes to.
+static char g_prof_names[256] = "";
 static int g_prof_cap = 0, g_prof_n = 0;
 static hipEvent_t* g_ev0 = nullptr;
 static hipEvent_t* g_ev1 = nullptr;
 static double* g_work = nullptr;
+static int* g_which = nullptr;   // index of the name in the list
+
+static int prof_index(const char* name) {
+  const size_t n = strlen(name);
+  int idx = 0;
+  for (const char* p = g_prof_names; *p;) {
+    const char* e = strchr(p, ',');
+    const size_t len = e ? (size_t)(e - p) : strlen(p);
+    if (len == n && strncmp(p, name, n) == 0) return idx;
+    if (!e) break;
+    p = e + 1;
+    ++idx;
+  }
+  return -1;
+}
 
 bool ppo_prof_begin(const char* name, hipStream_t st, int* slot) {
-  if (g_prof_cap == 0 || g_prof_n >= g_prof_cap || strcmp(name, g_prof_name) != 0) return false;
+  if (g_prof_cap == 0 || g_prof_n >= g_prof_cap) return false;
+  const int w = prof_index(name);
+  if (w < 0) return false;
   *slot = g_prof_n++;
+  g_which[*slot] = w;
   (void)hipEventRecord(g_ev0[*slot], st);
   return true;
 }
@@ -52,19 +72,22 @@ static void prof_free() {
   delete[] g_ev0;
   delete[] g_ev1;
   delete[] g_work;
+  delete[] g_which;
   g_ev0 = g_ev1 = nullptr;
   g_work = nullptr;
+  g_which = nullptr;
   g_prof_cap = g_prof_n = 0;
 }
 
-// name == NULL disables.  Not thread-safe; call outside captured regions.
-PPO_API int ppo_prof_enable(const char* name, int capacity) {
+// names == NULL disables.  Not thread-safe; call outside captured regions.
+PPO_API int ppo_prof_enable(const char* names, int capacity) {
   prof_free();
-  if (!name || capacity <= 0) return 0;
-  snprintf(g_prof_name, sizeof(g_prof_name), "%s", name);
+  if (!names || capacity <= 0) return 0;
+  snprintf(g_prof_names, sizeof(g_prof_names), "%s", names);
   g_ev0 = new hipEvent_t[capacity];
   g_ev1 = new hipEvent_t[capacity];
   g_work = new double[capacity];
+  g_which = new int[capacity];
   for (int i = 0; i < capacity; ++i) {
     PPO_HIP_CHECK(hipEventCreate(&g_ev0[i]), "ppo_prof_enable");
     PPO_HIP_CHECK(hipEventCreate(&g_ev1[i]), "ppo_prof_enable");
@@ -74,21 +97,27 @@ PPO_API int ppo_prof_enable(const char* name, int capacity) {
   return 0;
 }
 
-// Waits for the recorded launches; out3 = {launches, Σ ms, Σ work}.
-PPO_API int ppo_prof_collect(double* out3) {
+// Waits for the recorded launches of the idx-th listed name (-1: all);
+// out3 = {launches, Σ ms, Σ work}.
+PPO_API int ppo_prof_collect_one(int idx, double* out3) {
   double ms_total = 0.0, work = 0.0;
+  int n = 0;
   for (int i = 0; i < g_prof_n; ++i) {
+    if (idx >= 0 && g_which[i] != idx) continue;
     PPO_HIP_CHECK(hipEventSynchronize(g_ev1[i]), "ppo_prof_collect");
     float ms = 0.f;
     PPO_HIP_CHECK(hipEventElapsedTime(&ms, g_ev0[i], g_ev1[i]), "ppo_prof_collect");
     ms_total += ms;
     work += g_work[i];
+    ++n;
   }
-  out3[0] = g_prof_n;
+  out3[0] = n;
   out3[1] = ms_total;
   out3[2] = work;
   return 0;
 }
+
+PPO_API int ppo_prof_collect(double* out3) { return ppo_prof_collect_one(-1, out3); }
 PPO_API int ppo_abi_version(void) { return 1; }
 
 namespace {

@@ -264,8 +264,7 @@ def test_trunk_forward_vs_torch_fp32(gpu, B, H):
             d["base.main.0.bias"].data_ptr(), o1.data_ptr(), _s())
     Hh.call("ppo_conv2_fwd", o1.data_ptr(), B, pk[0], d["base.main.2.bias"].data_ptr(), o2.data_ptr(), _s())
     Hh.call("ppo_conv3_fwd", o2.data_ptr(), B, pk[1], d["base.main.4.bias"].data_ptr(), o3.data_ptr(), _s())
-    Hh.call("ppo_linear_relu_fwd", o3.data_ptr(), B, 1568, pk[2], d["base.main.7.bias"].data_ptr(), H,
-            o4.data_ptr(), _s())
+    Hh.call("ppo_fc_fwd", o3.data_ptr(), B, pk[2], d["base.main.7.bias"].data_ptr(), H, o4.data_ptr(), H, _s())
     for got, ref in ((o1, a1.permute(0, 2, 3, 1)), (o2, a2.permute(0, 2, 3, 1)), (o3, a3.permute(0, 2, 3, 1)),
                      (o4, hh)):
         ref = ref.contiguous()

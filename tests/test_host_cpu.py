@@ -44,7 +44,9 @@ def test_ctypes_table_matches_header():
 def test_host_only_queries():
     from a2c_ppo_acktr import _hip
     assert _hip.call("ppo_gae_partials_count", 4096) == 16
-    assert _hip.call("ppo_packed_weights_size", 512) == 64 * 512 + 32 * 576 + 2 * 512 * 1568 + 64 * 288 + 4 * 32 * 256
+    # f32 segments, each followed by its three bf16 planes (1.5x its size in floats)
+    assert _hip.call("ppo_packed_weights_size", 512) == (64 * 512 + 32 * 576 + 2 * 512 * 1568 + 64 * 288
+                                                         + 4 * 32 * 256) * 5 // 2
     z = _hip.call("ppo_wgrad_splits", 65536 * 400, 1, 2048, 16)
     assert 1 <= z <= 4096
     assert _hip.call("ppo_heads_train_blocks", 65536) == 65536 // 128

@@ -73,8 +73,10 @@ def main():
                       2.0 * B * 81 * 64 * 512),
         "conv3_fwd": (lambda: call("ppo_conv3_fwd", a2.data_ptr(), B, pk[1], b3.data_ptr(), a3.data_ptr(), s),
                       2.0 * B * 49 * 32 * 576),
-        "fc_fwd": (lambda: call("ppo_linear_relu_fwd", a3.data_ptr(), B, 1568, pk[2], b4.data_ptr(), H, h.data_ptr(),
-                                s), 2.0 * B * 1568 * H),
+        "fc_fwd": (lambda: call("ppo_fc_fwd", a3.data_ptr(), B, pk[2], b4.data_ptr(), H, h.data_ptr(), H, s),
+                   2.0 * B * 1568 * H),
+        "fc_fwd_generic": (lambda: call("ppo_linear_relu_fwd", a3.data_ptr(), B, 1568, pk[2], b4.data_ptr(), H,
+                                        h.data_ptr(), s), 2.0 * B * 1568 * H),
         "fc_dgrad": (lambda: call("ppo_linear_dgrad_mask", dh.data_ptr(), B, H, pk[3], 1568, a3.data_ptr(),
                                   dz3.data_ptr(), s), 2.0 * B * 1568 * H),
         "fc_wgrad": (lambda: call("ppo_linear_wgrad", dh.data_ptr(), a3.data_ptr(), B, H, 1568, z4, slab.data_ptr(),

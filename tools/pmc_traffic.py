@@ -28,8 +28,8 @@ def per_launch(path, counter, sub):
 
 def main():
     tag = sys.argv[1]
-    sub = sys.argv[2] if len(sys.argv) > 2 else "Conv1Fwd"
-    bench_kernel = sys.argv[3] if len(sys.argv) > 3 else "conv1_fwd_u8"
+    sub = sys.argv[2] if len(sys.argv) > 2 else "Conv2Dgrad"
+    bench_kernel = sys.argv[3] if len(sys.argv) > 3 else "conv2_dgrad"
     prof = os.path.join(ROOT, "profiles")
     shutil.copy(os.path.join(OUT, "prof", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
     line = [l for l in open(os.path.join(OUT, "bench_full.log")) if l.startswith("{")][-1]

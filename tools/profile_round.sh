@@ -5,7 +5,7 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-K="${KERNEL_REGEX:-Conv1Fwd}"
+K="${KERNEL_REGEX:-Conv2Dgrad}"
 BENCH_ARGS="${BENCH_ARGS:-}"
 step() { echo "== $1"; shift; "$@"; rc=$?; echo "rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 step bench timeout -k 10 900 python bench.py $BENCH_ARGS > gpurun_out/bench_full.log 2>&1
