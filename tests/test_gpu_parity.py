@@ -737,3 +737,30 @@ def test_ppo_learns_cartpole(gpu):
     early, late = np.mean(hist[:3]), np.mean(hist[-5:])
     print("cartpole mean episode length", early, "->", late)
     assert early < 40 and late > 150, hist
+
+
+def test_packed_weight_planes_exact(gpu):
+    """ppo_pack_weights writes, after every packed fp32 segment, its exact bf16
+    split (hi, mid, lo planes): hi + mid + lo reproduces each fp32 value bit for bit."""
+    Hh = _hip()
+    H = 64
+    g = torch.Generator().manual_seed(3)
+    w2 = (torch.randn(64, 32, 4, 4, generator=g) * 0.1).cuda()
+    w3 = (torch.randn(32, 64, 3, 3, generator=g) * 0.1).cuda()
+    w4 = (torch.randn(H, 1568, generator=g) * 0.02).cuda()
+    packed = torch.zeros(Hh.call("ppo_packed_weights_size", H), device=gpu)
+    offs = torch.zeros(6, dtype=torch.int64)
+    Hh.call("ppo_packed_offsets", H, offs.data_ptr())
+    Hh.call("ppo_pack_weights", w2.data_ptr(), w3.data_ptr(), w4.data_ptr(), H, packed.data_ptr(), _s())
+    torch.cuda.synchronize()
+    buf = packed.cpu().numpy()
+    sizes = [64 * 512, 32 * 576, H * 1568, H * 1568, 64 * 288, 4 * 32 * 256]
+    for o, n in zip(offs.tolist(), sizes):
+        seg = buf[o:o + n]
+        planes = buf[o + n:o + n + 3 * n // 2].view(np.uint16).astype(np.uint32)
+        parts = [(planes[i * n:(i + 1) * n] << 16).view(np.float32).astype(np.float64) for i in range(3)]
+        assert np.array_equal(parts[0] + parts[1] + parts[2], seg.astype(np.float64))
+    # and the packed values themselves are the torch weights, reordered (spot check of W4p)
+    w4p = buf[offs[2]:offs[2] + H * 1568].reshape(H, 49, 32)   # [n][p][c]
+    ref = w4.cpu().numpy().reshape(H, 32, 49).transpose(0, 2, 1)
+    assert np.array_equal(w4p, ref)

@@ -116,3 +116,32 @@ def test_storage_host_errors():
         st.half()
     with pytest.raises(AssertionError):
         next(st.feed_forward_generator(torch.zeros(4, 2, 1), 100))
+
+
+def test_bf16x3_split_is_exact():
+    """The exact three-way bf16 split behind the matrix-core fp32 paths
+    (csrc/common.h split_bf16x3): v == hi + mid + lo bit for bit,
+    each part a round-to-nearest-even bf16 of the remaining residual (for
+    |v| > ~1e-30; below that lo is subnormal and the split is off by < 2^-133)."""
+    import numpy as np
+
+    def rne(v):
+        u = v.view(np.uint32).astype(np.uint64)
+        return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint32)
+
+    def tof(h):
+        return (h.astype(np.uint32) << 16).view(np.float32)
+
+    rng = np.random.default_rng(0)
+    for scale in (1e-30, 1e-6, 1e-3, 0.05, 1.0, 1e3, 1e30):
+        v = (rng.standard_normal(500_000) * scale).astype(np.float32)
+        hi = rne(v)
+        r1 = (v - tof(hi)).astype(np.float32)
+        mid = rne(r1)
+        r2 = (r1 - tof(mid)).astype(np.float32)
+        lo = rne(r2)
+        back = tof(hi).astype(np.float64) + tof(mid) + tof(lo)
+        if scale >= 1e-20:
+            assert np.array_equal(back, v.astype(np.float64)), scale
+        else:   # lo falls into the subnormal range: off by at most its spacing, 2^-133
+            assert np.abs(back - v).max() <= 2.0 ** -133, scale
