@@ -269,6 +269,176 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
   }
 }
 
+// conv1 weight gradient on the bf16 matrix cores, exact (u8 observations,
+// C = 4): dW[co][(c,ky,kx)] = Σ_pixels dz1[px][co] · u[c][4oy+ky][4ox+kx].  The
+// pixel is exact in bf16 and dz = dz_hi + dz_mid + dz_lo exactly, so three
+// v_mfma_f32_32x32x16_bf16 per block pair give exact products with fp32
+// accumulation.  A block (8 waves, 2 per SIMD) walks its images;
+// per image the LDS holds
+//   E  [c][y][kx][ox]  bf16  the image "kx-expanded" (E = u[c][y][4ox+kx]), so
+//                           the 4 pixels of an output-row quad are 4 adjacent
+//                           elements for every (c, ky, kx); the 8 kx rows of
+//                           one (c, y) take 81 dwords (odd: the staging stores
+//                           of 32 lanes hit 32 banks)                   108,864 B
+//   dzT[co][404]       f32   dz1 transposed (row padded: conflict-free reads) 51,712 B
+// and the next image is in flight into registers.  The reduction runs over
+// pixels in natural order: k-step s covers pixels 16s .. 16s+15, lane half h the
+// 8 pixels 16s + 8h .. +7 (two output-row quads 4Q .. 4Q+3).  Wave w: n tiles
+// 4 (w & 1) .. +3 (128 of the 256 (c,ky,kx) columns), k-steps s ≡ (w >> 1) mod 4;
+// the k-groups' partial sums are combined in a fixed order at the end.
+// Output: the usual split-K slab [Z][32][256] (u8 integers: the reduce applies
+// 1/255) and bias partials [Z][32].
+template <int C>
+__global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __restrict__ dz1,
+                                                                 const uint8_t* __restrict__ obs,
+                                                                 const int64_t* __restrict__ idx, long long row0,
+                                                                 int B, float* __restrict__ slab,
+                                                                 float* __restrict__ slab_bias) {
+  static_assert(C == 4, "LDS budget sized for 4 input channels");
+  constexpr int EROW = 162, NE = C * IMG * EROW, DZL = 404, NPX = 400, KS = 25, NT = 512;
+  __shared__ __attribute__((aligned(16))) uint16_t E[NE];
+  __shared__ __attribute__((aligned(16))) float dzT[32 * DZL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ng = __builtin_amdgcn_readfirstlane(wave & 1), kg = __builtin_amdgcn_readfirstlane(wave >> 1);
+  const int l32 = lane & 31, h = lane >> 5;
+  int ecol[4];   // lane's B column n = 128 ng + 32 t + l32 -> (c, ky, kx)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int n = 128 * ng + 32 * t + l32, c = n >> 6, ky = (n >> 3) & 7, kx = n & 7;
+    ecol[t] = (c * IMG + ky) * EROW + kx * 20;   // + 4 oy * EROW + ox0 per quad
+  }
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  const int cq = tid & 7;                 // dz staging: channel quad of this thread
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};   // bias partial of channels 4 cq .. +3
+
+  f32x4 dzr[2][4];        // up to 2 units of 4 pixels x 4 channels
+  uint32_t imr[21];       // one image row (84 bytes)
+  auto fetch = [&](int b) {
+    const float* dzb = dz1 + (size_t)b * NPX * 32;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int u = tid + NT * i;
+      if (u < 800) {
+        const int p4 = u >> 3;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dzr[i][r] = *reinterpret_cast<const f32x4*>(dzb + (4 * p4 + r) * 32 + 4 * cq);
+      }
+    }
+    if (tid < C * IMG) {
+      const uint32_t* row =
+          reinterpret_cast<const uint32_t*>(obs + obs_row(idx, row0, b) * (long long)(C * IMG2) + tid * IMG);
+#pragma unroll
+      for (int j = 0; j < 21; ++j) imr[j] = row[j];
+    }
+  };
+  auto put = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int u = tid + NT * i;
+      if (u < 800) {
+        const int p4 = u >> 3;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 v = f32x4{dzr[i][0][q], dzr[i][1][q], dzr[i][2][q], dzr[i][3][q]};
+          *reinterpret_cast<f32x4*>(dzT + (4 * cq + q) * DZL + 4 * p4) = v;
+          bsum[q] += (v[0] + v[1]) + (v[2] + v[3]);
+        }
+      }
+    }
+    if (tid < C * IMG) {
+#pragma unroll
+      for (int kx = 0; kx < 8; ++kx) {   // E[cy][kx][ox] = byte (kx & 3) of dword ox + (kx >> 2)
+        const int kh = kx >> 2, kk = kx & 3;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(E + tid * EROW + kx * 20);
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+          const uint32_t w0 = imr[2 * q + kh], w1 = imr[2 * q + 1 + kh];
+          const float f0 = (float)((w0 >> (8 * kk)) & 255u), f1 = (float)((w1 >> (8 * kk)) & 255u);
+          dst[q] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+        }
+      }
+    }
+  };
+  auto rd = [&](int st, f32x4& x0, f32x4& x1, bf16x8 (&bb)[4]) {
+    const int px = 16 * st + 8 * h;   // this lane half's 8 pixels: quads px/4, px/4 + 1
+    x0 = *reinterpret_cast<const f32x4*>(dzT + l32 * DZL + px);
+    x1 = *reinterpret_cast<const f32x4*>(dzT + l32 * DZL + px + 4);
+    const int q1 = px >> 2, q2 = q1 + 1;
+    const int e1 = (q1 / 5) * (4 * EROW) + 4 * (q1 % 5), e2 = (q2 / 5) * (4 * EROW) + 4 * (q2 % 5);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {   // 40-B kx rows: quads only 4-byte aligned -> dword reads
+      const uint32_t* p1 = reinterpret_cast<const uint32_t*>(E + ecol[t] + e1);
+      const uint32_t* p2 = reinterpret_cast<const uint32_t*>(E + ecol[t] + e2);
+      bb[t] = __builtin_bit_cast(bf16x8, uint4{p1[0], p1[1], p2[0], p2[1]});
+    }
+  };
+
+  int b = blockIdx.x;
+  if (b < B) fetch(b);
+  for (; b < B; b += gridDim.x) {
+    put();
+    __syncthreads();
+    if (b + (int)gridDim.x < B) fetch(b + gridDim.x);
+    // k-steps kg, kg + 4, ...: the fragments of step s + 4 are read while the
+    // 12 MFMAs of step s run
+    f32x4 xa0, xa1;
+    bf16x8 bq[4];
+    if (kg < KS) rd(kg, xa0, xa1, bq);
+    for (int st = kg; st < KS; st += 4) {
+      Frag3 fa;
+      split8(xa0, xa1, fa, false);
+      bf16x8 bc[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bc[t] = bq[t];
+      if (st + 4 < KS) rd(st + 4, xa0, xa1, bq);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.l, bc[t], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.m, bc[t], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.h, bc[t], acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();   // before the next image overwrites E / dzT
+  }
+  // ---- combine the four k-groups (fixed order), write the slab ----
+  float* red = reinterpret_cast<float*>(E);   // [k-group 1..3][ng][t][r][lane]: 98,304 B <= 108,864
+  if (kg > 0) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((((kg - 1) * 2 + ng) * 4 + t) * 16 + r) * 64 + lane] = acc[t][r];
+  }
+  __syncthreads();
+  float* out = slab + (size_t)blockIdx.x * 32 * 256;
+  if (kg == 0) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = acc[t][r];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) v += red[(((g * 2 + ng) * 4 + t) * 16 + r) * 64 + lane];
+        const int co = (r & 3) + 8 * (r >> 2) + 4 * h, n = 128 * ng + 32 * t + l32;
+        out[co * 256 + n] = v;
+      }
+  }
+  __syncthreads();
+  float* bred = dzT;   // [512 threads][4]
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bred[tid * 4 + q] = bsum[q];
+  __syncthreads();
+  if (tid < 32) {   // channel tid: the 64 threads of its quad, fixed order
+    const int q = tid & 3, c8 = tid >> 2;
+    float t = 0.f;
+    for (int j = c8; j < NT; j += 8) t += bred[j * 4 + q];
+    slab_bias[(size_t)blockIdx.x * 32 + tid] = t;
+  }
+}
+
 // NHWC conv (conv2, conv3): k = (ky, kx, ci), weights packed [COUT][K]
 template <int HIN, int CIN, int KS, int ST, int HOUT, int COUT, class C_>
 struct ConvFwd : C_ {
@@ -880,8 +1050,18 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
   const long long R = (long long)B * 400;
   PPO_REQUIRE(R < 0x7fffffffLL, "ppo_conv1_wgrad: B too large");
   const double fl = 2.0 * R * 32 * C * 64;
+  if (obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] != 9) {
+    if (B <= 0 || Z <= 0) return 0;
+    int slot;
+    const bool prof = ppo_prof_begin("conv1_wgrad_u8", as_stream(stream), &slot);
+    conv1_wgrad_bf16x3_kernel<4><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
+                                                                   slab_bias);
+    if (prof) ppo_prof_end(slot, as_stream(stream), fl);
+    PPO_LAUNCH_CHECK("conv1_wgrad_bf16x3_kernel");
+    return 0;
+  }
   if (obs_is_u8) {
-    if (g_tune[TK_CONV1_WGRAD] == 1) {
+    if (g_tune[TK_CONV1_WGRAD] == 1 || g_tune[TK_CONV1_WGRAD] == 9) {
       Conv1Wgrad<uint8_t, CfgW32n> p;
       set_wgrad(p, dz1, 32, R, Z, slab, slab_bias, C * 64);
       p.obs = (const uint8_t*)obs; p.idx = idx; p.row0 = row0; p.C = C;
