@@ -764,3 +764,38 @@ def test_packed_weight_planes_exact(gpu):
     w4p = buf[offs[2]:offs[2] + H * 1568].reshape(H, 49, 32)   # [n][p][c]
     ref = w4.cpu().numpy().reshape(H, 32, 49).transpose(0, 2, 1)
     assert np.array_equal(w4p, ref)
+
+
+def test_two_rank_update_one_gpu():
+    """The N>1 protocol end to end on the device (two processes sharing the one
+    GPU, gloo collectives on device tensors; RCCL takes the same calls on an
+    8-GPU node): ranks start from different inits, PPO broadcasts rank 0's
+    parameters, each rank rolls out its own lanes, the advantage statistics and
+    every minibatch gradient are all-reduced -> bit-identical parameters on both
+    ranks after the update, and they moved."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    import os
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = str(s.getsockname()[1])
+    s.close()
+    worker = os.path.join(os.path.dirname(__file__), "helpers", "two_rank_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "2", port], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, e[-2000:]
+        outs.append(json.loads([ln for ln in o.splitlines() if ln.startswith("{")][-1]))
+    for o in outs:
+        assert o["same"] and o["moved"] > 1e-6 and all(np.isfinite(o["losses"]))
+    assert outs[0]["sum"] == outs[1]["sum"]
+    assert outs[0]["losses"] == outs[1]["losses"]
