@@ -44,8 +44,10 @@ PEAK_HBM_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # cores execute 3 (u8 operand) or 9 bf16 products per fp32 product, so their
 # MFMA ceiling is the bf16 peak / 3 or / 9 in fp32-FLOP units.
 PROFILED = {
-    "conv2_dgrad": ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"),
-    "conv1_wgrad_u8": ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"),
+    "conv2_dgrad": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9, "v_mfma_f32_16x16x32_bf16 x9 (exact split), image-resident"),
+    # u8 pixels are exact in bf16: 3 products per fp32 product
+    "conv1_wgrad_u8": ("mfma", PEAK_BF16_MFMA_TFLOPS / 3, "v_mfma_f32_32x32x16_bf16 x3 (u8 exact), image-resident"),
+    "conv3_dgrad": ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"),
     "conv2_wgrad": ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"),
     "conv2_fwd": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9, "v_mfma_f32_16x16x32_bf16 x9 (exact split)"),
     # conv1 forward: 79,424 B of compulsory HBM traffic per sample (28,224 B u8 in, 51,200 B f32 out)

@@ -540,6 +540,155 @@ struct Conv2Dgrad : C_ {
   }
 };
 
+// conv2 dgrad, image-resident on the bf16 matrix cores (exact split, DESIGN.md
+// §3): the phase-merged GEMM of Conv2Dgrad (n = (phase, ci), k = (tap, co)),
+// one persistent block (8 waves) per CU walking images.  Per image the LDS holds
+// dz2 already split into three bf16 planes, as a zero-padded 12 x 11 pixel grid
+// (dz2 pixel (oy, ox) at (oy + 1, ox + 1)): 2 stages x 50,688 B, the next image
+// in flight into registers, so the k loop has no staging, no barrier and no
+// range tests.  GEMM rows run over the padded grid too: m = 11 yy + xx (xx = 10 is
+// a dummy column, 110 rows in 7 tiles of 16 — the padding 100 rows would need
+// anyway), so row m's tap (ty, tx) is grid pixel m + 12 - (11 ty + tx).
+//   k order: k-step s takes co 8s .. 8s+7 of all four taps, lane group g = tap
+//   (ty, tx) = (g >> 1, g & 1): the A fragment of lane (row i, g) is one 16-B
+//   read per plane, and a 16-lane ds_read_b128 group reads 16 consecutive grid
+//   pixels — conflict-free with chunk c of pixel p stored at c ^ ((p >> 1) & 7)
+//   (128-B pixel rows: slot = 8 (p & 1) + chunk).  W2d [128][(tap, co)] needs no
+//   repacking: lane (n, g) of k-step s reads W2d[n][64 g + 8 s .. +7].
+// Wave w owns n tile w (phase w >> 1, ci 16 (w & 1) + [0, 16)) for all of K,
+// its weight fragments (pre-split planes, 8 k-steps x 3) in 96 VGPRs.
+__global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __restrict__ dz2, int B,
+                                                            const uint16_t* __restrict__ wpl,
+                                                            const float* __restrict__ a1,
+                                                            float* __restrict__ dz1) {
+  constexpr int HO = 9, CO = 64, GW = 11, GP = 12 * GW, ROW = CO, PL = GP * ROW, MT = 7, KS = 8;
+  constexpr int CH = HO * HO * CO / 8, PER = (CH + 511) / 512, WN = 128 * 256;
+  __shared__ __attribute__((aligned(16))) uint16_t S[2][3][PL];
+  __shared__ int etab[16 * MT];   // row m -> output offset yy*1280 + xx*64 (or -1: dummy row)
+  // ReLU mask of a1 (conv1's output) for the image: one byte per element,
+  // staged like dz2 (coalesced 16-B loads one image ahead, in registers)
+  constexpr int MC = 400 * 32 / 4, MPER = (MC + 511) / 512;
+  __shared__ __attribute__((aligned(16))) uint32_t Mk[2][MC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int n = 16 * wave + i16, ph = wave >> 1, ci = 16 * (wave & 1) + i16;
+  bf16x8 bw[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + n * 256 + 64 * g + 8 * s);
+  // zero the pad pixels of both stages (staging only ever writes the 81 real ones)
+  for (int i = tid; i < 2 * 3 * GP * 8; i += 512) {
+    const int c = i % (GP * 8), p = c >> 3, py = p / GW, px = p - GW * py;
+    if (py == 0 || py >= 10 || px == 0 || px == 10)
+      *reinterpret_cast<uint4*>(&S[i / (3 * GP * 8)][(i / (GP * 8)) % 3][8 * c]) = uint4{0, 0, 0, 0};
+  }
+  if (tid < 16 * MT) {
+    const int yy = tid / GW, xx = tid - GW * yy;
+    etab[tid] = (yy < 10 && xx < 10) ? yy * 1280 + xx * 64 : -1;
+  }
+  // byte offset of this lane's A fragment, row tile 0, k-step 0 (tile t adds 16
+  // pixels = 2048 B, k-step s XORs 16 s — both leave the swizzle term unchanged)
+  const int pa = i16 + 12 - (11 * (g >> 1) + (g & 1));
+  const int abase = pa * 128 + 16 * ((pa >> 1) & 7);
+  f32x4 stg[PER][2];
+  f32x4 mst[MPER];
+  auto fetch = [&](int b) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(dz2 + (size_t)b * (HO * HO * CO));
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = tid + 512 * j;
+      if (c < CH) { stg[j][0] = src[2 * c]; stg[j][1] = src[2 * c + 1]; }
+    }
+    const f32x4* ms = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
+#pragma unroll
+    for (int j = 0; j < MPER; ++j) {
+      const int c = tid + 512 * j;
+      if (c < MC) mst[j] = ms[c];
+    }
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < MPER; ++j) {
+      const int c = tid + 512 * j;
+      if (c < MC)
+        Mk[buf][c] = (mst[j][0] > 0.f ? 1u : 0u) | (mst[j][1] > 0.f ? 0x100u : 0u) |
+                     (mst[j][2] > 0.f ? 0x10000u : 0u) | (mst[j][3] > 0.f ? 0x1000000u : 0u);
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int c = tid + 512 * j;
+      if (c < CH) {
+        const int r = c >> 3, oy = r / HO, p = (oy + 1) * GW + (r - HO * oy) + 1;
+        const int off = p * ROW + 8 * ((c & 7) ^ ((p >> 1) & 7));
+        Frag3 f;
+        split8(stg[j][0], stg[j][1], f, false);
+        *reinterpret_cast<bf16x8*>(&S[buf][0][off]) = f.h;
+        *reinterpret_cast<bf16x8*>(&S[buf][1][off]) = f.m;
+        *reinterpret_cast<bf16x8*>(&S[buf][2][off]) = f.l;
+      }
+    }
+  };
+  const int G = gridDim.x;
+  int b = blockIdx.x, cur = 0;
+  if (b < B) {
+    fetch(b);
+    put(0);
+    if (b + G < B) fetch(b + G);
+  }
+  __syncthreads();
+  for (; b < B; b += G) {
+    if (b + G < B) put(cur ^ 1);
+    if (b + 2 * G < B) fetch(b + 2 * G);
+    const char* Sb = reinterpret_cast<const char*>(S[cur][0]);
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = zero4();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const char* As = Sb + (abase ^ (16 * s));
+      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+      // two groups of row tiles (4 + 3: register budget); within a group the
+      // nine part products, smallest first, go round the tiles
+#pragma unroll
+      for (int t0 = 0; t0 < MT; t0 += 4) {
+        constexpr int TG = 4;
+        Frag3 a[TG];
+#pragma unroll
+        for (int u = 0; u < TG; ++u)
+          if (t0 + u < MT) {
+            const char* q = As + 2048 * (t0 + u);
+            a[u].h = *reinterpret_cast<const bf16x8*>(q);
+            a[u].m = *reinterpret_cast<const bf16x8*>(q + 2 * PL);
+            a[u].l = *reinterpret_cast<const bf16x8*>(q + 4 * PL);
+          }
+#define PPO_PART(X, Y)                                                  \
+  _Pragma("unroll") for (int u = 0; u < TG; ++u) if (t0 + u < MT) acc[t0 + u] = mma(a[u].X, w.Y, acc[t0 + u]);
+        PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
+        PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+#undef PPO_PART
+      }
+    }
+    // epilogue: C row 4g + r of tile t is grid row m = 16t + 4g + r; ReLU mask of a1
+    const uint8_t* mk = reinterpret_cast<const uint8_t*>(Mk[cur]);
+    float* dm = dz1 + (size_t)b * 12800;
+    const int cb = (ph >> 1) * 640 + (ph & 1) * 32 + ci;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int4 e = *reinterpret_cast<const int4*>(&etab[16 * t + 4 * g]);
+      const int eo[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (eo[r] >= 0) {
+          const int i = eo[r] + cb;
+          dm[i] = mk[i] ? acc[t][r] : 0.f;
+        }
+    }
+    __syncthreads();   // every wave is done with S[cur]; S[cur ^ 1] is complete
+    cur ^= 1;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Weight-gradient (wgrad) problems: dW[co][kk] = Σ_r dz[r][co] · X(r, kk)
 // over the reduction r = (b, output pixel), split over blockIdx.z into fp32
@@ -699,7 +848,7 @@ enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRA
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
                                          "fc_fwd", "conv2_fwd", "x9"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
-static int g_tune[TK_N] = {0, 3, 3, 1, 1, 0, 0, 1};  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 3, 8, 1, 1, 0, 0, 1};  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   for (int i = 0; i < TK_N; ++i)
@@ -757,6 +906,19 @@ using XP64 = CfgX<128, 64, 4, 1, true, true, false, false, false, true>;    // w
 using XP128 = CfgX<128, 128, 4, 1, true, true, false, false, false, true>;  // waves 32x128
 // x9 = 1: the split-bf16 core where it measured faster (forward GEMMs, fc dgrad); the gather-heavy
 // conv dgrads and the wgrads stay on fp32 MFMA (their split path is VALU-bound); x9 = 2: everywhere
+// compute units of the current device (persistent-kernel grid size)
+static int device_cus() {
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    n_cu = n;
+  }
+  return n_cu;
+}
+
 static inline bool use_x9() { return g_tune[TK_X9] != 0; }
 static inline bool use_x9_all() { return g_tune[TK_X9] == 2; }
 template <class P>
@@ -811,13 +973,7 @@ PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, lo
   p.obs = (const T_*)obs; p.idx = idx; p.row0 = row0; p.C = C; p.M = (int)M; p.w = w1; p.bias = b1; p.out = out
   if (obs_is_u8 && C == 4 && g_tune[tk] != 9) {
     if (B == 0) return 0;
-    static int n_cu = 0;
-    if (!n_cu) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-        n_cu = 256;
-    }
+    const int n_cu = device_cus();
     const int npairs = (B + 1) / 2;
     const unsigned blocks = (unsigned)(npairs < n_cu ? npairs : n_cu);   // persistent, one per CU
     int slot;
@@ -1003,6 +1159,18 @@ PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const flo
 }
 
 PPO_API int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const float* a1, float* dz1, void* stream) {
+  if (g_tune[TK_CONV2_DGRAD] == 8) {
+    if (B <= 0) return 0;
+    const int n_cu = device_cus();
+    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+    int slot;
+    const bool prof = ppo_prof_begin("conv2_dgrad", as_stream(stream), &slot);
+    const uint16_t* wpl = planes_of(w2d, 128 * 256);
+    conv2_dgrad_x9_kernel<<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, a1, dz1);
+    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
+    PPO_LAUNCH_CHECK("conv2_dgrad_x9_kernel");
+    return 0;
+  }
   if (use_x9_all()) {
     Conv2Dgrad<XP128> p;
     p.dy = dz2; p.wd = w2d; p.act = a1; p.dx = dz1; p.M = B * 100;

@@ -766,6 +766,47 @@ def test_packed_weight_planes_exact(gpu):
     assert np.array_equal(w4p, ref)
 
 
+def _packed(gpu, H, seed):
+    Hh = _hip()
+    g = torch.Generator().manual_seed(seed)
+    w = {"w2": torch.randn(64, 32, 4, 4, generator=g) * 0.05, "w3": torch.randn(32, 64, 3, 3, generator=g) * 0.05,
+         "w4": torch.randn(H, 1568, generator=g) * 0.02}
+    d = {k: v.cuda() for k, v in w.items()}
+    packed = torch.zeros(Hh.call("ppo_packed_weights_size", H), device=gpu)
+    offs = torch.zeros(6, dtype=torch.int64)
+    Hh.call("ppo_packed_offsets", H, offs.data_ptr())
+    Hh.call("ppo_pack_weights", d["w2"].data_ptr(), d["w3"].data_ptr(), d["w4"].data_ptr(), H, packed.data_ptr(),
+            _s())
+    return w, packed, [packed.data_ptr() + 4 * int(o) for o in offs]
+
+
+@pytest.mark.parametrize("variant", [3, 8])
+def test_conv2_dgrad_variants_vs_torch(gpu, variant):
+    """conv2 dgrad (phase-merged GEMM, 4x4 stride 2 transposed conv 9x9 -> 20x20
+    with the conv1 ReLU mask), every kernel variant — the fp32 tile GEMM (3) and
+    the image-resident exact split-bf16 kernel (8) — vs torch float64:
+    max |err| <= 1e-5 * max |ref| (fp32 arithmetic, summation order differs).
+    B = 300 images > the persistent grid, so blocks walk several images."""
+    Hh = _hip()
+    B = 300
+    w, packed, pk = _packed(gpu, 64, 11)
+    g = torch.Generator().manual_seed(12)
+    dz2 = torch.randn(B, 9, 9, 64, generator=g)
+    a1 = torch.randn(B, 20, 20, 32, generator=g)
+    dz1 = torch.full((B, 20, 20, 32), float("nan"), device=gpu)
+    dz2_d, a1_d = dz2.cuda(), a1.cuda()
+    Hh.call("ppo_tune_set", b"conv2_dgrad", variant)
+    try:
+        Hh.call("ppo_conv2_dgrad", dz2_d.data_ptr(), B, pk[5], a1_d.data_ptr(), dz1.data_ptr(), _s())
+        torch.cuda.synchronize()
+    finally:
+        Hh.call("ppo_tune_set", b"conv2_dgrad", 8)
+    ref = F.conv_transpose2d(dz2.double().permute(0, 3, 1, 2), w["w2"].double(), stride=2).permute(0, 2, 3, 1)
+    ref = torch.where(a1 > 0, ref, torch.zeros((), dtype=torch.float64))
+    err = (dz1.cpu().double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item(), err
+
+
 def test_two_rank_update_one_gpu():
     """The N>1 protocol end to end on the device (two processes sharing the one
     GPU, gloo collectives on device tensors; RCCL takes the same calls on an
