@@ -540,6 +540,137 @@ struct Conv2Dgrad : C_ {
   }
 };
 
+// conv2 forward, image-resident on the bf16 matrix cores (exact split, DESIGN.md
+// §3): a2[b][m][co] = relu(b2[co] + Σ_k im2col(a1)[m][k] W2p[co][k]), m = (oy, ox)
+// (81 rows in 6 tiles of 16), k = (ky, kx, ci).  One persistent block (8 waves)
+// per CU walks images; the image sits in LDS split into three bf16 planes, the
+// next one in flight into registers (stored between the compute phases).
+//   LDS layout: 16-B units (8 ci) of pixel (y, x) at unit index
+//     c * CS + (y & 1) * 250 + (y >> 1) * 25 + (x & 1) * 10 + (x >> 1)
+//   (c = ci >> 3, CS = 544): with y and x parities split out, the pixel a row
+//   m = 9 oy + ox reads for tap (ky, kx) is oy * 25 + ox + const ≡ m + const
+//   (mod 16), so the 16 rows of a tile hit 16 distinct 16-B slots whatever their
+//   ci chunk — ds_read_b128 without bank conflicts.
+//   Wave w: n tile w & 3 (16 co), taps 8 (w >> 2) .. +7 (ky rows 0-1 / 2-3);
+//   its weight fragments (pre-split planes) in 96 VGPRs.  The two K halves are
+//   summed through LDS (half 1 writes, half 0 adds and stores).
+__global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restrict__ a1, int B,
+                                                          const uint16_t* __restrict__ wpl,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out) {
+  constexpr int CS = 544, PLU = 4 * CS, MT = 6, KS = 8, UNITS = 400 * 4, UPER = (UNITS + 511) / 512;
+  constexpr int WN = 64 * 512;
+  __shared__ __attribute__((aligned(16))) uint16_t S[3 * PLU * 8];   // 3 planes x 4 chunks x CS units x 8 bf16
+  __shared__ __attribute__((aligned(16))) f32x4 R[4][MT][64];        // K-half-1 partial sums
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int nt = wave & 3, kh = wave >> 2, co = 16 * nt + i16;
+  bf16x8 bw[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
+  const float bv = bias[co];
+  // unit index of this lane's A fragment per row tile, tap (0, 0); a tap adds toff
+  int qrow[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int m = 16 * t + i16, oy = m / 9, ox = m - 9 * oy;
+    qrow[t] = g * CS + oy * 25 + ox;
+  }
+  // staging: unit u -> chunk (u >> 3) & 3 of the pixel at LDS-order position
+  // rho = 8 (u >> 5) + (u & 7), rho = 20 y + 10 (x & 1) + (x >> 1): the 8 lanes of a
+  // ds_write_b128 pass store 8 consecutive units (no bank conflicts), and the 4
+  // chunks of a pixel are read by one load instruction (whole 128-B lines)
+  int upx[UPER], uq[UPER];
+#pragma unroll
+  for (int j = 0; j < UPER; ++j) {
+    const int u = tid + 512 * j, rho = 8 * (u >> 5) + (u & 7), c = (u >> 3) & 3;
+    const int y = rho / 20, r = rho - 20 * y, x = r < 10 ? 2 * r : 2 * (r - 10) + 1;
+    upx[j] = (y * 20 + x) * 4 + c;
+    uq[j] = c * CS + (y & 1) * 250 + (y >> 1) * 25 + r;
+  }
+  float4 stg[UPER][2];
+  auto fetch = [&](int b) {
+    const float4* src = reinterpret_cast<const float4*>(a1 + (size_t)b * 12800);
+#pragma unroll
+    for (int j = 0; j < UPER; ++j) {
+      const int u = tid + 512 * j;
+      if (u < UNITS) { stg[j][0] = src[2 * upx[j]]; stg[j][1] = src[2 * upx[j] + 1]; }
+    }
+  };
+  auto put = [&]() {
+#pragma unroll
+    for (int j = 0; j < UPER; ++j) {
+      const int u = tid + 512 * j;
+      if (u < UNITS) {
+        const int q = uq[j];
+        Frag3 f;
+        split8(f32x4{stg[j][0].x, stg[j][0].y, stg[j][0].z, stg[j][0].w},
+               f32x4{stg[j][1].x, stg[j][1].y, stg[j][1].z, stg[j][1].w}, f, false);
+        *reinterpret_cast<bf16x8*>(&S[8 * q]) = f.h;
+        *reinterpret_cast<bf16x8*>(&S[8 * (PLU + q)]) = f.m;
+        *reinterpret_cast<bf16x8*>(&S[8 * (2 * PLU + q)]) = f.l;
+      }
+    }
+  };
+  const int G = gridDim.x;
+  int b = blockIdx.x;
+  if (b < B) {
+    fetch(b);
+    put();
+    if (b + G < B) fetch(b + G);
+  }
+  __syncthreads();
+  for (; b < B; b += G) {
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = zero4();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int tap = 8 * kh + s, ky = tap >> 2, kx = tap & 3;
+      const int toff = (ky & 1) * 250 + (ky >> 1) * 25 + (kx & 1) * 10 + (kx >> 1);
+      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+#pragma unroll
+      for (int t0 = 0; t0 < MT; t0 += 3) {
+        Frag3 a[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const uint16_t* q = S + 8 * (qrow[t0 + u] + toff);
+          a[u].h = *reinterpret_cast<const bf16x8*>(q);
+          a[u].m = *reinterpret_cast<const bf16x8*>(q + 8 * PLU);
+          a[u].l = *reinterpret_cast<const bf16x8*>(q + 16 * PLU);
+        }
+#define PPO_PART(X, Y) \
+  _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(a[u].X, w.Y, acc[t0 + u]);
+        PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
+        PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+#undef PPO_PART
+      }
+    }
+    __syncthreads();   // A: the image is consumed
+    if (kh == 1) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t) R[nt][t][lane] = acc[t];
+    }
+    if (b + G < B) put();
+    if (b + 2 * G < B) fetch(b + 2 * G);
+    __syncthreads();   // B: partials and the next image are in LDS
+    if (kh == 0) {
+      float* o = out + (size_t)b * (81 * 64) + co;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const f32x4 v = acc[t] + R[nt][t][lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * t + 4 * g + r;
+          if (m < 81) o[m * 64] = fmaxf(v[r] + bv, 0.f);
+        }
+      }
+    }
+  }
+}
+
 // conv2 dgrad, image-resident on the bf16 matrix cores (exact split, DESIGN.md
 // §3): the phase-merged GEMM of Conv2Dgrad (n = (phase, ci), k = (tap, co)),
 // one persistent block (8 waves) per CU walking images.  Per image the LDS holds
@@ -848,7 +979,7 @@ enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRA
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
                                          "fc_fwd", "conv2_fwd", "x9"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
-static int g_tune[TK_N] = {0, 3, 8, 1, 1, 0, 0, 1};  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 3, 8, 1, 1, 0, 8, 1};  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   for (int i = 0; i < TK_N; ++i)
@@ -1000,6 +1131,17 @@ PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, lo
 }
 
 PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream) {
+  if (g_tune[TK_CONV2_FWD] == 8) {
+    if (B <= 0) return 0;
+    const int n_cu = device_cus();
+    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+    int slot;
+    const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
+    conv2_fwd_x9_kernel<<<nb, 512, 0, as_stream(stream)>>>(a1, B, planes_of(w2p, 64 * 512), b2, out);
+    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
+    PPO_LAUNCH_CHECK("conv2_fwd_x9_kernel");
+    return 0;
+  }
   if (use_x9()) {
     ConvFwd<20, 32, 4, 2, 9, 64, XP64> p;
     p.in = a1; p.w = w2p; p.bias = b2; p.out = out; p.M = B * 81;

@@ -807,6 +807,32 @@ def test_conv2_dgrad_variants_vs_torch(gpu, variant):
     assert err <= 1e-5 * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("variant", [0, 8])
+def test_conv2_fwd_variants_vs_torch(gpu, variant):
+    """conv2 forward (4x4 stride 2, 20x20x32 -> 9x9x64, bias + ReLU): the split-bf16
+    tile GEMM (0) and the image-resident kernel (8) vs torch float64:
+    max |err| <= 1e-5 * max |ref|.  B = 300 > the persistent grid."""
+    Hh = _hip()
+    B = 300
+    w, packed, pk = _packed(gpu, 64, 21)
+    g = torch.Generator().manual_seed(22)
+    a1 = torch.relu(torch.randn(B, 20, 20, 32, generator=g))
+    b2 = torch.randn(64, generator=g) * 0.1
+    a1_d, b2_d = a1.cuda(), b2.cuda()
+    out = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
+    old = 8   # the default
+    Hh.call("ppo_tune_set", b"conv2_fwd", variant)
+    try:
+        Hh.call("ppo_conv2_fwd", a1_d.data_ptr(), B, pk[0], b2_d.data_ptr(), out.data_ptr(), _s())
+        torch.cuda.synchronize()
+    finally:
+        Hh.call("ppo_tune_set", b"conv2_fwd", old)
+    ref = F.conv2d(a1.double().permute(0, 3, 1, 2), w["w2"].double(), b2.double(), stride=2)
+    ref = torch.relu(ref).permute(0, 2, 3, 1)
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item(), err
+
+
 def test_two_rank_update_one_gpu():
     """The N>1 protocol end to end on the device (two processes sharing the one
     GPU, gloo collectives on device tensors; RCCL takes the same calls on an
