@@ -671,6 +671,182 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restri
   }
 }
 
+// conv2 weight gradient, image-resident on the bf16 matrix cores (exact split,
+// DESIGN.md §3): dW2[co][k] = Σ_pixels dz2[m][co] · a1[2oy+ky][2ox+kx][ci],
+// k = (ky, kx, ci); per image a 64 x 512 x 81 product (reduction padded to 96 =
+// 3 k-steps of 32), accumulated in registers over the block's images and
+// written once as the block's split-K partial (slab [Z][64][512], bias
+// partials [Z][64]; ppo_wgrad_reduce sums the Z partials in a fixed order).
+// Per image the LDS holds, split into bf16 planes (the next image in flight in
+// registers, stored between compute phases):
+//   X  [3][400 px][32 ci]  a1, pixels in parity order Q = 20 y + 10 (x & 1) + (x >> 1)
+//                          (76,800 B): the B fragment (8 reduction slots x 16 ci of
+//                          one tap) comes from two ds_read_b64_tr_b16 per plane —
+//                          4 pixel rows each, gathered by per-lane row addresses;
+//                          8-B unit u of pixel Q at u ^ 4 ((Q >> 3) & 1)
+//   D  [3][64 co][112]     dz2 transposed to [co][reduction slot] (43,008 B; rows of
+//                          14 16-B units: conflict-free ds_read_b128 A fragments)
+// Reduction slot r -> pixel: the 72 pixels with ox < 8 oy-major, then the ox = 8
+// column (no 4-slot tr group straddles an output row; fewer bank conflicts);
+// slots 81..95 have dz = 0 and read pixel 80's finite a1.
+// Wave w: k columns 64 w .. +63 (taps 2w, 2w+1, both ci halves) x all 64 co:
+// 16 accumulator tiles (64 VGPRs).
+__device__ __forceinline__ int c2w_pix(int r) {
+  r = r < 80 ? r : 80;
+  return r < 72 ? (r >> 3) * 9 + (r & 7) : (r - 72) * 9 + 8;
+}
+
+__global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __restrict__ dz2,
+                                                            const float* __restrict__ a1, int B,
+                                                            float* __restrict__ slab,
+                                                            float* __restrict__ slab_bias) {
+  constexpr int XPL = 400 * 32, DR = 112, DPL = 64 * DR;
+  constexpr int XU = 1600, XPER = (XU + 511) / 512, DU = 64 * 12, DPER = (DU + 511) / 512;
+  __shared__ __attribute__((aligned(16))) uint16_t X[3 * XPL];
+  __shared__ __attribute__((aligned(16))) uint16_t D[3 * DPL];
+  __shared__ float bred[512];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int q = i16 >> 2, p = i16 & 3;
+  // tap-(0,0) pixel (parity order) of the row this lane addresses in the tr
+  // reads of k-step s, half h: Q = Qb + 20 ky + 10 (kx & 1) + (kx >> 1)
+  int Qb[3][2];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int m = c2w_pix(32 * s + 8 * g + 4 * h + q), oy = m / 9;
+      Qb[s][h] = 40 * oy + (m - 9 * oy);
+    }
+  // staging maps: X unit u -> (pixel Q = u >> 2, 16-B chunk c = u & 3); D unit
+  // v -> (co = v & 63, slots 8 (v >> 6) .. +7)
+  int xsrc[XPER], xdst[XPER];
+#pragma unroll
+  for (int j = 0; j < XPER; ++j) {
+    const int u = tid + 512 * j, Q = u >> 2, c = u & 3, y = Q / 20, rem = Q - 20 * y;
+    const int x = rem < 10 ? 2 * rem : 2 * (rem - 10) + 1;
+    xsrc[j] = (y * 20 + x) * 32 + 8 * c;
+    xdst[j] = Q * 32 + 8 * (c ^ (((Q >> 3) & 1) * 2));
+  }
+  f32x4 xs[XPER][2];
+  float ds[DPER][8];
+  float bsum = 0.f;   // bias partial of co = tid & 63 (fixed for this thread's D units)
+  auto fetch = [&](int b) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
+#pragma unroll
+    for (int j = 0; j < XPER; ++j)
+      if (tid + 512 * j < XU) { xs[j][0] = src[xsrc[j] / 4]; xs[j][1] = src[xsrc[j] / 4 + 1]; }
+    const float* dsrc = dz2 + (size_t)b * (81 * 64);
+#pragma unroll
+    for (int j = 0; j < DPER; ++j) {
+      const int v = tid + 512 * j;
+      if (v < DU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int r = 8 * (v >> 6) + e;
+          ds[j][e] = r < 81 ? dsrc[c2w_pix(r) * 64 + (v & 63)] : 0.f;
+        }
+      }
+    }
+  };
+  auto put = [&]() {
+#pragma unroll
+    for (int j = 0; j < XPER; ++j)
+      if (tid + 512 * j < XU) {
+        Frag3 f;
+        split8(xs[j][0], xs[j][1], f, false);
+        *reinterpret_cast<bf16x8*>(&X[xdst[j]]) = f.h;
+        *reinterpret_cast<bf16x8*>(&X[XPL + xdst[j]]) = f.m;
+        *reinterpret_cast<bf16x8*>(&X[2 * XPL + xdst[j]]) = f.l;
+      }
+#pragma unroll
+    for (int j = 0; j < DPER; ++j) {
+      const int v = tid + 512 * j;
+      if (v < DU) {
+        Frag3 f;
+        split8(f32x4{ds[j][0], ds[j][1], ds[j][2], ds[j][3]}, f32x4{ds[j][4], ds[j][5], ds[j][6], ds[j][7]}, f,
+               false);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum += ds[j][e];
+        const int off = (v & 63) * DR + 8 * (v >> 6);
+        *reinterpret_cast<bf16x8*>(&D[off]) = f.h;
+        *reinterpret_cast<bf16x8*>(&D[DPL + off]) = f.m;
+        *reinterpret_cast<bf16x8*>(&D[2 * DPL + off]) = f.l;
+      }
+    }
+  };
+  f32x4 acc[4][4];   // [n tile j][co tile mt]
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[j][mt] = zero4();
+  const int Z = gridDim.x;
+  int b = blockIdx.x;
+  if (b < B) {
+    fetch(b);
+    put();
+    if (b + Z < B) fetch(b + Z);
+  }
+  __syncthreads();
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  for (; b < B; b += Z) {
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      Frag3 a[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int off = (16 * mt + i16) * DR + 32 * s + 8 * g;
+        a[mt].h = *reinterpret_cast<const bf16x8*>(&D[off]);
+        a[mt].m = *reinterpret_cast<const bf16x8*>(&D[DPL + off]);
+        a[mt].l = *reinterpret_cast<const bf16x8*>(&D[2 * DPL + off]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int tap = 2 * wave + (j >> 1), ky = tap >> 2, kx = tap & 3, cb = j & 1;
+        const int toff = 20 * ky + 10 * (kx & 1) + (kx >> 1);
+        s16x4 t[3][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int Q = Qb[s][h] + toff, unit = (4 * cb + p) ^ (((Q >> 3) & 1) * 4);
+          const uint16_t* rp = &X[Q * 32 + 4 * unit];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            t[pl][h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(rp + pl * XPL));
+        }
+        Frag3 bf;
+        bf.h = __builtin_bit_cast(bf16x8, __builtin_shufflevector(t[0][0], t[0][1], 0, 1, 2, 3, 4, 5, 6, 7));
+        bf.m = __builtin_bit_cast(bf16x8, __builtin_shufflevector(t[1][0], t[1][1], 0, 1, 2, 3, 4, 5, 6, 7));
+        bf.l = __builtin_bit_cast(bf16x8, __builtin_shufflevector(t[2][0], t[2][1], 0, 1, 2, 3, 4, 5, 6, 7));
+#define PPO_PART(XX, YY) \
+  _Pragma("unroll") for (int mt = 0; mt < 4; ++mt) acc[j][mt] = mma(a[mt].XX, bf.YY, acc[j][mt]);
+        PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
+        PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+#undef PPO_PART
+      }
+    }
+    __syncthreads();   // the image is consumed
+    if (b + Z < B) put();
+    if (b + 2 * Z < B) fetch(b + 2 * Z);
+    __syncthreads();   // the next image is in LDS
+  }
+  // this block's partial: C row 4g + r of co tile mt, column i16 of n tile j
+  float* o = slab + (size_t)blockIdx.x * (64 * 512) + 64 * wave + i16;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[(16 * mt + 4 * g + r) * 512 + 16 * j] = acc[j][mt][r];
+  bred[tid] = bsum;
+  __syncthreads();
+  if (tid < 64) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) t += bred[tid + 64 * w];
+    slab_bias[(size_t)blockIdx.x * 64 + tid] = t;
+  }
+}
+
 // conv2 dgrad, image-resident on the bf16 matrix cores (exact split, DESIGN.md
 // §3): the phase-merged GEMM of Conv2Dgrad (n = (phase, ci), k = (tap, co)),
 // one persistent block (8 waves) per CU walking images.  Per image the LDS holds
@@ -975,11 +1151,11 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
 // ---------------------------------------------------------------------------
 enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_X9,
-       TK_N };
+       TK_CONV2_WGRAD, TK_N };
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
-                                         "fc_fwd", "conv2_fwd", "x9"};
+                                         "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
-static int g_tune[TK_N] = {0, 3, 8, 1, 1, 0, 8, 1};  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 3, 8, 1, 1, 0, 8, 1, 8};  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   for (int i = 0; i < TK_N; ++i)
@@ -1390,6 +1566,15 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
 
 PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, float* slab, float* slab_bias,
                             void* stream) {
+  if (g_tune[TK_CONV2_WGRAD] == 8) {
+    if (B <= 0 || Z <= 0) return 0;
+    int slot;
+    const bool prof = ppo_prof_begin("conv2_wgrad", as_stream(stream), &slot);
+    conv2_wgrad_x9_kernel<<<Z, 512, 0, as_stream(stream)>>>(dz2, a1, B, slab, slab_bias);
+    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
+    PPO_LAUNCH_CHECK("conv2_wgrad_x9_kernel");
+    return 0;
+  }
   if (use_x9_all()) {
     ConvWgrad<20, 32, 4, 2, 9, XW64> p;
     set_wgrad(p, dz2, 64, (long long)B * 81, Z, slab, slab_bias, 512);

@@ -833,6 +833,38 @@ def test_conv2_fwd_variants_vs_torch(gpu, variant):
     assert err <= 1e-5 * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("variant", [0, 8])
+def test_conv2_wgrad_variants_vs_torch(gpu, variant):
+    """conv2 weight + bias gradient (split-K partials + ppo_wgrad_reduce into the
+    torch layout): the fp32 tile GEMM (0) and the image-resident split-bf16 kernel
+    (8) vs torch float64: max |err| <= 1e-5 * max |ref| per tensor.  B = 300."""
+    Hh = _hip()
+    B = 300
+    g = torch.Generator().manual_seed(31)
+    a1 = torch.relu(torch.randn(B, 20, 20, 32, generator=g))
+    dz2 = torch.randn(B, 9, 9, 64, generator=g)
+    a1_d, dz2_d = a1.cuda(), dz2.cuda()
+    Z = Hh.call("ppo_wgrad_splits", B * 81, 4, 2048, 16)
+    slab = torch.empty(Z * 64 * 512, device=gpu)
+    slab_b = torch.empty(Z * 64, device=gpu)
+    gw = torch.empty(64 * 512, device=gpu)
+    gb = torch.empty(64, device=gpu)
+    Hh.call("ppo_tune_set", b"conv2_wgrad", variant)
+    try:
+        Hh.call("ppo_conv2_wgrad", dz2_d.data_ptr(), a1_d.data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), _s())
+        Hh.call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, 64, 512, 1, 4, 32, gw.data_ptr(),
+                gb.data_ptr(), 1.0, 0, _s())
+        torch.cuda.synchronize()
+    finally:
+        Hh.call("ppo_tune_set", b"conv2_wgrad", 8)
+    x, dy = a1.double().permute(0, 3, 1, 2), dz2.double().permute(0, 3, 1, 2)
+    ref_w = torch.nn.grad.conv2d_weight(x, (64, 32, 4, 4), dy, stride=2)
+    ref_b = dy.sum((0, 2, 3))
+    for got, ref in ((gw.cpu().double().view(64, 32, 4, 4), ref_w), (gb.cpu().double(), ref_b)):
+        err = (got - ref).abs().max().item()
+        assert err <= 1e-5 * ref.abs().max().item(), err
+
+
 def test_two_rank_update_one_gpu():
     """The N>1 protocol end to end on the device (two processes sharing the one
     GPU, gloo collectives on device tensors; RCCL takes the same calls on an

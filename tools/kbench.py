@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
     ap.add_argument("--tune", default="", help="key=v[,key=v...] tile variants (ppo_tune_set)")
+    ap.add_argument("--z2", type=int, default=0, help="conv2 wgrad split count (default: ppo_wgrad_splits)")
     a = ap.parse_args()
     for kv in [x for x in a.tune.split(",") if x]:
         k, v = kv.split("=")
@@ -66,6 +67,7 @@ def main():
         return call("ppo_wgrad_splits", R, tiles, 2048, 16)
 
     z1, z2, z3, z4 = zs(B * 400, 1), zs(B * 81, 4), zs(B * 49, 5), zs(B, ((H + 127) // 128) * 13)
+    z2 = a.z2 or z2
     K = {
         "conv1_fwd": (lambda: call("ppo_conv1_fwd", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, w1.data_ptr(),
                                    b1.data_ptr(), a1.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
