@@ -47,7 +47,7 @@ PROFILED = {
     "conv2_dgrad": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9, "v_mfma_f32_16x16x32_bf16 x9 (exact split), image-resident"),
     # u8 pixels are exact in bf16: 3 products per fp32 product
     "conv1_wgrad_u8": ("mfma", PEAK_BF16_MFMA_TFLOPS / 3, "v_mfma_f32_32x32x16_bf16 x3 (u8 exact), image-resident"),
-    "conv3_dgrad": ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"),
+    "conv3_dgrad": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9, "v_mfma_f32_16x16x32_bf16 x9 (exact split), image-resident"),
     "conv2_wgrad": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9,
                     "v_mfma_f32_16x16x32_bf16 x9 (exact split), image-resident, ds_read_b64_tr_b16 im2col"),
     "conv2_fwd": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9, "v_mfma_f32_16x16x32_bf16 x9 (exact split)"),

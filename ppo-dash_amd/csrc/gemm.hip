@@ -847,6 +847,384 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
   }
 }
 
+// conv3 dgrad, image-resident on the bf16 matrix cores (exact split, DESIGN.md
+// §3): dz2[m][ci] = [a2 > 0] Σ_(ky,kx,co) dz3[y-ky][x-kx][co] W3d[ci][(ky,kx,co)],
+// m = (y, x) over the 9 x 9 input (81 rows in 6 tiles of 16), k-step = tap, lane
+// group g = co chunk.  One persistent block (8 waves) per CU walks images; per
+// image the LDS holds dz3 split into three bf16 planes on a zero-padded grid of
+// width 25 (dz3 pixel (oy, ox) at (oy + 2) * 25 + ox + 2; 11 rows), in 16-B units
+// c * 288 + pixel: row m's tap pixel is 25 y + x + const ≡ m + const (mod 16), so
+// the 16 rows of a tile hit distinct slots (conflict-free ds_read_b128), and out-of-
+// range taps read zeros.  Two stages (2 x 55,296 B) plus the a2 ReLU mask as
+// bytes (2 x 5,184 B): the next image is staged before the compute, one barrier
+// per image.  Wave w: ci tile w & 3 (weights, 9 taps x 3 planes, in 108 VGPRs),
+// row tiles 3 (w >> 2) .. +2.
+__global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __restrict__ dz3, int B,
+                                                            const uint16_t* __restrict__ wpl,
+                                                            const float* __restrict__ a2,
+                                                            float* __restrict__ dz2) {
+  constexpr int GW = 25, CS = 288, PLU = 4 * CS, KS = 9, WN = 64 * 288;
+  constexpr int DU = 49 * 4, MC = 81 * 64 / 4, MPER = (MC + 511) / 512;
+  __shared__ __attribute__((aligned(16))) uint16_t S[2][3 * PLU * 8];
+  __shared__ __attribute__((aligned(16))) uint32_t Mk[2][MC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int nt = wave & 3, mh = wave >> 2, ci = 16 * nt + i16;
+  bf16x8 bw[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + ci * 288 + 32 * s + 8 * g);
+  for (int i = tid; i < 2 * 3 * PLU; i += 512) reinterpret_cast<uint4*>(&S[0][0])[i] = uint4{0, 0, 0, 0};
+  // unit index of this lane's A fragment per row tile for tap (0, 0); tap
+  // (ky, kx) subtracts 25 ky + kx
+  int qrow[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int m = min(16 * (3 * mh + t) + i16, 80), y = m / 9, x = m - 9 * y;   // dummy rows: pixel 80
+    qrow[t] = g * CS + (y + 2) * GW + x + 2;
+  }
+  f32x4 stg[2];
+  f32x4 mst[MPER];
+  auto fetch = [&](int b) {
+    if (tid < DU) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(dz3 + (size_t)b * 1568);
+      stg[0] = src[2 * tid];
+      stg[1] = src[2 * tid + 1];
+    }
+    const f32x4* ms = reinterpret_cast<const f32x4*>(a2 + (size_t)b * 5184);
+#pragma unroll
+    for (int j = 0; j < MPER; ++j)
+      if (tid + 512 * j < MC) mst[j] = ms[tid + 512 * j];
+  };
+  auto put = [&](int buf) {
+    if (tid < DU) {   // unit tid: dz3 pixel tid >> 2, co chunk tid & 3
+      const int px = tid >> 2, oy = px / 7, ox = px - 7 * oy;
+      const int q = (tid & 3) * CS + (oy + 2) * GW + ox + 2;
+      Frag3 f;
+      split8(stg[0], stg[1], f, false);
+      *reinterpret_cast<bf16x8*>(&S[buf][8 * q]) = f.h;
+      *reinterpret_cast<bf16x8*>(&S[buf][8 * (PLU + q)]) = f.m;
+      *reinterpret_cast<bf16x8*>(&S[buf][8 * (2 * PLU + q)]) = f.l;
+    }
+#pragma unroll
+    for (int j = 0; j < MPER; ++j) {
+      const int c = tid + 512 * j;
+      if (c < MC)
+        Mk[buf][c] = (mst[j][0] > 0.f ? 1u : 0u) | (mst[j][1] > 0.f ? 0x100u : 0u) |
+                     (mst[j][2] > 0.f ? 0x10000u : 0u) | (mst[j][3] > 0.f ? 0x1000000u : 0u);
+    }
+  };
+  __syncthreads();   // the zeroed pads
+  const int G = gridDim.x;
+  int b = blockIdx.x, cur = 0;
+  if (b < B) {
+    fetch(b);
+    put(0);
+    if (b + G < B) fetch(b + G);
+  }
+  __syncthreads();
+  for (; b < B; b += G) {
+    if (b + G < B) put(cur ^ 1);
+    if (b + 2 * G < B) fetch(b + 2 * G);
+    const uint16_t* Sc = S[cur];
+    f32x4 acc[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) acc[t] = zero4();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int toff = -(GW * (s / 3) + s % 3);
+      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+      Frag3 a[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const uint16_t* q = Sc + 8 * (qrow[u] + toff);
+        a[u].h = *reinterpret_cast<const bf16x8*>(q);
+        a[u].m = *reinterpret_cast<const bf16x8*>(q + 8 * PLU);
+        a[u].l = *reinterpret_cast<const bf16x8*>(q + 16 * PLU);
+      }
+#define PPO_PART(X, Y) \
+  _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[u] = mma(a[u].X, w.Y, acc[u]);
+      PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
+      PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+#undef PPO_PART
+    }
+    // epilogue: C row 4g + r of tile t is input pixel m; ReLU mask of a2
+    const uint8_t* mk = reinterpret_cast<const uint8_t*>(Mk[cur]);
+    float* o = dz2 + (size_t)b * 5184 + ci;
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * (3 * mh + t) + 4 * g + r;
+        if (m < 81) o[m * 64] = mk[m * 64 + ci] ? acc[t][r] : 0.f;
+      }
+    __syncthreads();   // every wave is done with stage cur; stage cur ^ 1 is complete
+    cur ^= 1;
+  }
+}
+
+// conv3 forward, image-resident on the bf16 matrix cores (exact split, DESIGN.md
+// §3): a3[b][(oy, ox)][co] = relu(b3[co] + Σ_(ky,kx,ci) a2[oy+ky][ox+kx][ci] W3p[co][k]).
+// GEMM rows run over the 9-wide input grid, m = 9 oy + ox (ox = 7, 8 dummy: 63 rows
+// in 4 tiles, as many as the 49 real rows need), so row m's tap pixel is m + 9 ky
+// + kx — 16 consecutive pixels per tile, conflict-free ds_read_b128 with chunk c of
+// pixel p at c ^ ((p >> 1) & 7) (128-B pixel rows).  k-step = (tap, ci half), lane
+// group g = 8-ci chunk.  Per image the LDS holds a2 split into three bf16 planes
+// (84 pixel rows, the last 3 zero, reached by dummy rows only): 2 stages x 32,256 B,
+// the next image staged before the compute.  Wave w: co tile w & 1, K half
+// (w >> 1) & 1 (taps 0-4.5 / 4.5-8: 9 k-steps, weights in 108 VGPRs), row tiles
+// 2 (w >> 2) .. +1; K half 1 hands its partial sums over through LDS.
+__global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restrict__ a2, int B,
+                                                          const uint16_t* __restrict__ wpl,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out) {
+  constexpr int NP = 84, PL = NP * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, UPER = (UNITS + 511) / 512;
+  __shared__ __attribute__((aligned(16))) uint16_t S[2][3 * PL];
+  __shared__ __attribute__((aligned(16))) f32x4 R[2][2][2][2][64];   // [stage][co tile][row half][tile][lane]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int nt = wave & 1, kh = (wave >> 1) & 1, mh = wave >> 2, co = 16 * nt + i16;
+  bf16x8 bw[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 576 + (9 * kh + s) * 32 + 8 * g);
+  const float bv = bias[co];
+  for (int i = tid; i < 2 * 3 * PL / 8; i += 512) reinterpret_cast<uint4*>(&S[0][0])[i] = uint4{0, 0, 0, 0};
+  f32x4 stg[UPER][2];
+  auto fetch = [&](int b) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(a2 + (size_t)b * 5184);
+#pragma unroll
+    for (int j = 0; j < UPER; ++j) {
+      const int u = tid + 512 * j;
+      if (u < UNITS) { stg[j][0] = src[2 * u]; stg[j][1] = src[2 * u + 1]; }
+    }
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < UPER; ++j) {
+      const int u = tid + 512 * j;
+      if (u < UNITS) {
+        const int p = u >> 3, off = p * 64 + 8 * ((u & 7) ^ ((p >> 1) & 7));
+        Frag3 f;
+        split8(stg[j][0], stg[j][1], f, false);
+        *reinterpret_cast<bf16x8*>(&S[buf][off]) = f.h;
+        *reinterpret_cast<bf16x8*>(&S[buf][PL + off]) = f.m;
+        *reinterpret_cast<bf16x8*>(&S[buf][2 * PL + off]) = f.l;
+      }
+    }
+  };
+  __syncthreads();   // the zeroed pad rows
+  const int G = gridDim.x;
+  int b = blockIdx.x, cur = 0;
+  if (b < B) {
+    fetch(b);
+    put(0);
+    if (b + G < B) fetch(b + G);
+  }
+  __syncthreads();
+  for (; b < B; b += G) {
+    if (b + G < B) put(cur ^ 1);
+    if (b + 2 * G < B) fetch(b + 2 * G);
+    const uint16_t* Sc = S[cur];
+    f32x4 acc[2] = {zero4(), zero4()};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int ks = 9 * kh + s, tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky, c = 4 * (ks & 1) + g;
+      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+      Frag3 a[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int p = 16 * (2 * mh + u) + i16 + 9 * ky + kx;
+        const uint16_t* q = Sc + p * 64 + 8 * (c ^ ((p >> 1) & 7));
+        a[u].h = *reinterpret_cast<const bf16x8*>(q);
+        a[u].m = *reinterpret_cast<const bf16x8*>(q + PL);
+        a[u].l = *reinterpret_cast<const bf16x8*>(q + 2 * PL);
+      }
+#define PPO_PART(X, Y) \
+  _Pragma("unroll") for (int u = 0; u < 2; ++u) acc[u] = mma(a[u].X, w.Y, acc[u]);
+      PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
+      PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+#undef PPO_PART
+    }
+    if (kh == 1) {
+      R[cur][nt][mh][0][lane] = acc[0];
+      R[cur][nt][mh][1][lane] = acc[1];
+    }
+    __syncthreads();   // stage cur consumed, stage cur ^ 1 complete, partials in R[cur]
+    if (kh == 0) {
+      float* o = out + (size_t)b * (49 * 32) + co;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const f32x4 v = acc[u] + R[cur][nt][mh][u][lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * (2 * mh + u) + 4 * g + r, oy = m / 9, ox = m - 9 * oy;
+          if (ox < 7 && oy < 7) o[(7 * oy + ox) * 32] = fmaxf(v[r] + bv, 0.f);
+        }
+      }
+    }
+    cur ^= 1;
+  }
+}
+
+// conv3 weight gradient, image-resident on the bf16 matrix cores (exact split,
+// DESIGN.md §3): dW3[co][k] = Σ_pixels dz3[m][co] · a2[oy+ky][ox+kx][ci], k = (ky,
+// kx, ci); per image a 32 x 576 x 49 product, accumulated in registers over the
+// block's images and written once as its split-K partial (slab [Z][32][576],
+// bias partials [Z][32]).  Reduction slot r = 8 oy + ox (ox = 7 and oy = 7 are
+// dummy slots, dz = 0): 64 slots = 2 k-steps.  Per image (2 stages) the LDS holds
+//   X [3][9 x 12 px][64 ci]  a2 split into bf16 planes, pixel P = 12 y + x, 128-B
+//                            rows; the B fragment (8 slots x 16 ci of one tap) is two
+//                            ds_read_b64_tr_b16 per plane whose 4-slot row groups
+//                            are 4 consecutive ox and the next oy (P + 12): with
+//                            8-B unit u of pixel P at u ^ 4 ((P >> 1) & 3) every
+//                            32-lane half hits distinct banks
+//   D [3][32 co][112]        dz3 transposed to [co][slot] (224-B rows: conflict-free
+//                            ds_read_b128 A fragments)
+// 12 waves (3 per SIMD), wave w: n tiles 3w .. 3w+2 (both co tiles).
+__global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __restrict__ dz3,
+                                                            const float* __restrict__ a2, int B,
+                                                            float* __restrict__ slab,
+                                                            float* __restrict__ slab_bias) {
+  constexpr int NT = 768, XPL = 108 * 64, DR = 112, DPL = 32 * DR;
+  constexpr int XU = 81 * 8, XPER = (XU + NT - 1) / NT, DU = 32 * 8;
+  __shared__ __attribute__((aligned(16))) uint16_t X[2][3 * XPL];
+  __shared__ __attribute__((aligned(16))) uint16_t D[2][3 * DPL];
+  __shared__ float bred[DU];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int q = i16 >> 2, p = i16 & 3;
+  // tap-(0,0) pixel of the row this lane addresses in the tr reads of k-step s,
+  // half h (dummy slots read pixel (6, 6): finite, times dz = 0)
+  int Pb[2][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = 32 * s + 8 * g + 4 * h + q;
+      int oy = r >> 3, ox = r & 7;
+      if (oy > 6 || ox > 6) { oy = 6; ox = 6; }
+      Pb[s][h] = 12 * oy + ox;
+    }
+  f32x4 xs[XPER][2];
+  float ds[7];
+  float bsum = 0.f;   // bias partial of co = tid & 31 (threads < 256: slots of row oy = tid >> 5)
+  auto fetch = [&](int b) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(a2 + (size_t)b * 5184);
+#pragma unroll
+    for (int j = 0; j < XPER; ++j) {
+      const int u = tid + NT * j;
+      if (u < XU) { xs[j][0] = src[2 * u]; xs[j][1] = src[2 * u + 1]; }
+    }
+    if (tid < DU) {
+      const float* d = dz3 + (size_t)b * 1568 + (tid >> 5) * 7 * 32 + (tid & 31);
+      if ((tid >> 5) < 7) {
+#pragma unroll
+        for (int e = 0; e < 7; ++e) ds[e] = d[e * 32];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 7; ++e) ds[e] = 0.f;
+      }
+    }
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < XPER; ++j) {
+      const int u = tid + NT * j;
+      if (u < XU) {
+        const int px = u >> 3, c = u & 7, y = px / 9, P = 12 * y + (px - 9 * y);
+        const int off = P * 64 + 8 * (c ^ (2 * ((P >> 1) & 3)));
+        Frag3 f;
+        split8(xs[j][0], xs[j][1], f, false);
+        *reinterpret_cast<bf16x8*>(&X[buf][off]) = f.h;
+        *reinterpret_cast<bf16x8*>(&X[buf][XPL + off]) = f.m;
+        *reinterpret_cast<bf16x8*>(&X[buf][2 * XPL + off]) = f.l;
+      }
+    }
+    if (tid < DU) {
+      Frag3 f;
+      split8(f32x4{ds[0], ds[1], ds[2], ds[3]}, f32x4{ds[4], ds[5], ds[6], 0.f}, f, false);
+#pragma unroll
+      for (int e = 0; e < 7; ++e) bsum += ds[e];
+      const int off = (tid & 31) * DR + 8 * (tid >> 5);
+      *reinterpret_cast<bf16x8*>(&D[buf][off]) = f.h;
+      *reinterpret_cast<bf16x8*>(&D[buf][DPL + off]) = f.m;
+      *reinterpret_cast<bf16x8*>(&D[buf][2 * DPL + off]) = f.l;
+    }
+  };
+  f32x4 acc[3][2];   // [n tile][co tile]
+#pragma unroll
+  for (int j = 0; j < 3; ++j) acc[j][0] = acc[j][1] = zero4();
+  const int Z = gridDim.x;
+  int b = blockIdx.x, cur = 0;
+  if (b < B) {
+    fetch(b);
+    put(0);
+    if (b + Z < B) fetch(b + Z);
+  }
+  __syncthreads();
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  for (; b < B; b += Z) {
+    if (b + Z < B) put(cur ^ 1);
+    if (b + 2 * Z < B) fetch(b + 2 * Z);
+    const uint16_t* Xc = X[cur];
+    const uint16_t* Dc = D[cur];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      Frag3 a[2];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int off = (16 * mt + i16) * DR + 32 * s + 8 * g;
+        a[mt].h = *reinterpret_cast<const bf16x8*>(&Dc[off]);
+        a[mt].m = *reinterpret_cast<const bf16x8*>(&Dc[DPL + off]);
+        a[mt].l = *reinterpret_cast<const bf16x8*>(&Dc[2 * DPL + off]);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int n = 3 * wave + j, tap = n >> 2, ky = tap / 3, kx = tap - 3 * ky, cb = n & 3;
+        s16x4 t[3][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int P = Pb[s][h] + 12 * ky + kx, unit = (4 * cb + p) ^ (4 * ((P >> 1) & 3));
+          const uint16_t* rp = &Xc[P * 64 + 4 * unit];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            t[pl][h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(rp + pl * XPL));
+        }
+        Frag3 bf;
+        bf.h = __builtin_bit_cast(bf16x8, __builtin_shufflevector(t[0][0], t[0][1], 0, 1, 2, 3, 4, 5, 6, 7));
+        bf.m = __builtin_bit_cast(bf16x8, __builtin_shufflevector(t[1][0], t[1][1], 0, 1, 2, 3, 4, 5, 6, 7));
+        bf.l = __builtin_bit_cast(bf16x8, __builtin_shufflevector(t[2][0], t[2][1], 0, 1, 2, 3, 4, 5, 6, 7));
+#define PPO_PART(XX, YY) \
+  _Pragma("unroll") for (int mt = 0; mt < 2; ++mt) acc[j][mt] = mma(a[mt].XX, bf.YY, acc[j][mt]);
+        PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
+        PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+#undef PPO_PART
+      }
+    }
+    __syncthreads();   // stage cur consumed; stage cur ^ 1 complete
+    cur ^= 1;
+  }
+  // this block's partial: C row 4g + r of co tile mt, column i16 of n tile 3w + j
+  float* o = slab + (size_t)blockIdx.x * (32 * 576) + 48 * wave + i16;
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[(16 * mt + 4 * g + r) * 576 + 16 * j] = acc[j][mt][r];
+  if (tid < DU) bred[tid] = bsum;
+  __syncthreads();
+  if (tid < 32) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) t += bred[tid + 32 * w];
+    slab_bias[(size_t)blockIdx.x * 32 + tid] = t;
+  }
+}
+
 // conv2 dgrad, image-resident on the bf16 matrix cores (exact split, DESIGN.md
 // §3): the phase-merged GEMM of Conv2Dgrad (n = (phase, ci), k = (tap, co)),
 // one persistent block (8 waves) per CU walking images.  Per image the LDS holds
@@ -1151,11 +1529,11 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
 // ---------------------------------------------------------------------------
 enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_X9,
-       TK_CONV2_WGRAD, TK_N };
+       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_N };
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
-                                         "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad"};
+                                         "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
-static int g_tune[TK_N] = {0, 3, 8, 1, 1, 0, 8, 1, 8};  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 8, 8, 8, 1, 0, 8, 1, 8, 8};  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   for (int i = 0; i < TK_N; ++i)
@@ -1332,6 +1710,17 @@ PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float*
 }
 
 PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream) {
+  if (g_tune[TK_CONV3_FWD] == 8) {
+    if (B <= 0) return 0;
+    const int n_cu = device_cus();
+    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+    int slot;
+    const bool prof = ppo_prof_begin("conv3_fwd", as_stream(stream), &slot);
+    conv3_fwd_x9_kernel<<<nb, 512, 0, as_stream(stream)>>>(a2, B, planes_of(w3p, 32 * 576), b3, out);
+    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
+    PPO_LAUNCH_CHECK("conv3_fwd_x9_kernel");
+    return 0;
+  }
   if (use_x9()) {
     ConvFwd<9, 64, 3, 1, 7, 32, XP32> p;
     p.in = a2; p.w = w3p; p.bias = b3; p.out = out; p.M = B * 49;
@@ -1463,6 +1852,17 @@ PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt
 }
 
 PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream) {
+  if (g_tune[TK_CONV3_DGRAD] == 8) {
+    if (B <= 0) return 0;
+    const int n_cu = device_cus();
+    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+    int slot;
+    const bool prof = ppo_prof_begin("conv3_dgrad", as_stream(stream), &slot);
+    conv3_dgrad_x9_kernel<<<nb, 512, 0, as_stream(stream)>>>(dz3, B, planes_of(w3d, 64 * 288), a2, dz2);
+    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
+    PPO_LAUNCH_CHECK("conv3_dgrad_x9_kernel");
+    return 0;
+  }
   if (use_x9_all()) {
     ConvDgradS1<9, 64, 3, 7, 32, XP64> p;
     p.dy = dz3; p.wd = w3d; p.act = a2; p.dx = dz2; p.M = B * 81;
@@ -1589,6 +1989,15 @@ PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, flo
 
 PPO_API int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, float* slab, float* slab_bias,
                             void* stream) {
+  if (g_tune[TK_CONV3_WGRAD] == 8) {
+    if (B <= 0 || Z <= 0) return 0;
+    int slot;
+    const bool prof = ppo_prof_begin("conv3_wgrad", as_stream(stream), &slot);
+    conv3_wgrad_x9_kernel<<<Z, 768, 0, as_stream(stream)>>>(dz3, a2, B, slab, slab_bias);
+    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
+    PPO_LAUNCH_CHECK("conv3_wgrad_x9_kernel");
+    return 0;
+  }
   if (use_x9_all()) {
     ConvWgrad<9, 64, 3, 1, 7, XW32> p;
     set_wgrad(p, dz3, 32, (long long)B * 49, Z, slab, slab_bias, 576);

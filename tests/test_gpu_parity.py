@@ -898,3 +898,84 @@ def test_two_rank_update_one_gpu():
         assert o["same"] and o["moved"] > 1e-6 and all(np.isfinite(o["losses"]))
     assert outs[0]["sum"] == outs[1]["sum"]
     assert outs[0]["losses"] == outs[1]["losses"]
+
+
+@pytest.mark.parametrize("variant", [1, 8])
+def test_conv3_dgrad_variants_vs_torch(gpu, variant):
+    """conv3 dgrad (3x3 stride 1, 7x7x32 -> 9x9x64, a2 ReLU mask): the fp32 tile
+    GEMM (1) and the image-resident split-bf16 kernel (8) vs torch float64:
+    max |err| <= 1e-5 * max |ref|.  B = 300 > the persistent grid."""
+    Hh = _hip()
+    B = 300
+    w, packed, pk = _packed(gpu, 64, 41)
+    g = torch.Generator().manual_seed(42)
+    dz3 = torch.randn(B, 7, 7, 32, generator=g)
+    a2 = torch.randn(B, 9, 9, 64, generator=g)
+    dz3_d, a2_d = dz3.cuda(), a2.cuda()
+    dz2 = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
+    Hh.call("ppo_tune_set", b"conv3_dgrad", variant)
+    try:
+        Hh.call("ppo_conv3_dgrad", dz3_d.data_ptr(), B, pk[4], a2_d.data_ptr(), dz2.data_ptr(), _s())
+        torch.cuda.synchronize()
+    finally:
+        Hh.call("ppo_tune_set", b"conv3_dgrad", 8)
+    ref = F.conv_transpose2d(dz3.double().permute(0, 3, 1, 2), w["w3"].double()).permute(0, 2, 3, 1)
+    ref = torch.where(a2 > 0, ref, torch.zeros((), dtype=torch.float64))
+    err = (dz2.cpu().double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("variant", [3, 8])
+def test_conv3_fwd_variants_vs_torch(gpu, variant):
+    """conv3 forward (3x3 stride 1, 9x9x64 -> 7x7x32, bias + ReLU): the split-bf16
+    tile GEMM (3) and the image-resident kernel (8) vs torch float64:
+    max |err| <= 1e-5 * max |ref|.  B = 300 > the persistent grid."""
+    Hh = _hip()
+    B = 300
+    w, packed, pk = _packed(gpu, 64, 51)
+    g = torch.Generator().manual_seed(52)
+    a2 = torch.relu(torch.randn(B, 9, 9, 64, generator=g))
+    b3 = torch.randn(32, generator=g) * 0.1
+    a2_d, b3_d = a2.cuda(), b3.cuda()
+    out = torch.full((B, 7, 7, 32), float("nan"), device=gpu)
+    Hh.call("ppo_tune_set", b"conv3_fwd", variant)
+    try:
+        Hh.call("ppo_conv3_fwd", a2_d.data_ptr(), B, pk[1], b3_d.data_ptr(), out.data_ptr(), _s())
+        torch.cuda.synchronize()
+    finally:
+        Hh.call("ppo_tune_set", b"conv3_fwd", 8)
+    ref = torch.relu(F.conv2d(a2.double().permute(0, 3, 1, 2), w["w3"].double(), b3.double())).permute(0, 2, 3, 1)
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("variant", [0, 8])
+def test_conv3_wgrad_variants_vs_torch(gpu, variant):
+    """conv3 weight + bias gradient (partials + ppo_wgrad_reduce into the torch
+    layout): the fp32 tile GEMM (0) and the image-resident split-bf16 kernel (8)
+    vs torch float64: max |err| <= 1e-5 * max |ref| per tensor.  B = 300."""
+    Hh = _hip()
+    B = 300
+    g = torch.Generator().manual_seed(61)
+    a2 = torch.relu(torch.randn(B, 9, 9, 64, generator=g))
+    dz3 = torch.randn(B, 7, 7, 32, generator=g)
+    a2_d, dz3_d = a2.cuda(), dz3.cuda()
+    Z = Hh.call("ppo_wgrad_splits", B * 49, 5, 2048, 16)
+    slab = torch.empty(Z * 32 * 576, device=gpu)
+    slab_b = torch.empty(Z * 32, device=gpu)
+    gw = torch.empty(32 * 576, device=gpu)
+    gb = torch.empty(32, device=gpu)
+    Hh.call("ppo_tune_set", b"conv3_wgrad", variant)
+    try:
+        Hh.call("ppo_conv3_wgrad", dz3_d.data_ptr(), a2_d.data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), _s())
+        Hh.call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, 32, 576, 1, 3, 64, gw.data_ptr(),
+                gb.data_ptr(), 1.0, 0, _s())
+        torch.cuda.synchronize()
+    finally:
+        Hh.call("ppo_tune_set", b"conv3_wgrad", 8)
+    x, dy = a2.double().permute(0, 3, 1, 2), dz3.double().permute(0, 3, 1, 2)
+    ref_w = torch.nn.grad.conv2d_weight(x, (32, 64, 3, 3), dy)
+    ref_b = dy.sum((0, 2, 3))
+    for got, ref in ((gw.cpu().double().view(32, 64, 3, 3), ref_w), (gb.cpu().double(), ref_b)):
+        err = (got - ref).abs().max().item()
+        assert err <= 1e-5 * ref.abs().max().item(), err
