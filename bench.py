@@ -40,21 +40,31 @@ PEAK_HBM_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 # The kernels timed with HIP events inside the timed region, and the roofline
 # that bounds each one.  "work" is algorithmic fp32 FLOP per
-# launch (2·M·N·K of the layer); for the exact-split bf16 kernels the matrix
-# cores execute 3 (u8 operand) or 9 bf16 products per fp32 product, so their
-# MFMA ceiling is the bf16 peak / 3 or / 9 in fp32-FLOP units.
-PROFILED = {
-    "conv2_dgrad": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9, "v_mfma_f32_16x16x32_bf16 x9 (exact split), image-resident"),
-    # u8 pixels are exact in bf16: 3 products per fp32 product
-    "conv1_wgrad_u8": ("mfma", PEAK_BF16_MFMA_TFLOPS / 3, "v_mfma_f32_32x32x16_bf16 x3 (u8 exact), image-resident"),
-    "conv3_dgrad": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9, "v_mfma_f32_16x16x32_bf16 x9 (exact split), image-resident"),
-    "conv2_wgrad": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9,
-                    "v_mfma_f32_16x16x32_bf16 x9 (exact split), image-resident, ds_read_b64_tr_b16 im2col"),
-    "conv2_fwd": ("mfma", PEAK_BF16_MFMA_TFLOPS / 9, "v_mfma_f32_16x16x32_bf16 x9 (exact split)"),
-    # conv1 forward: 79,424 B of compulsory HBM traffic per sample (28,224 B u8 in, 51,200 B f32 out)
-    # against 6.55 MFLOP at bf16/3 -> HBM-bound
-    "conv1_fwd_u8": ("hbm", PEAK_HBM_GBPS, "v_mfma_f32_16x16x32_bf16 x3 (u8 exact), image-resident"),
-}
+# launch (2·M·N·K of the layer).  The split-bf16 kernels execute P bf16 part
+# products per fp32 product on the matrix cores — 3 with a u8 operand (exact in
+# bf16), 6 (default) or 9 (ppo_tune_set("products")) with two fp32 operands — so
+# their MFMA ceiling is the dense bf16 peak / P in fp32-FLOP units.
+def profiled(products):
+    split = (f"v_mfma_f32_16x16x32_bf16 x{products} "
+             + ("(exact split)" if products == 9 else "(split, 6 products: fp32-accurate)"))
+    pk = PEAK_BF16_MFMA_TFLOPS / products
+    return {
+        "conv2_fwd": ("mfma", pk, split + ", image-resident"),
+        "conv2_dgrad": ("mfma", pk, split + ", image-resident"),
+        "conv2_wgrad": ("mfma", pk, split + ", image-resident, ds_read_b64_tr_b16 im2col"),
+        "conv3_fwd": ("mfma", pk, split + ", image-resident"),
+        "conv3_dgrad": ("mfma", pk, split + ", image-resident"),
+        "conv3_wgrad": ("mfma", pk, split + ", image-resident, ds_read_b64_tr_b16 im2col"),
+        # u8 pixels are exact in bf16: 3 products per fp32 product
+        "conv1_wgrad_u8": ("mfma", PEAK_BF16_MFMA_TFLOPS / 3,
+                           "v_mfma_f32_32x32x16_bf16 x3 (u8 exact), image-resident"),
+        # conv1 forward: 79,424 B of compulsory HBM traffic per sample (28,224 B u8 in, 51,200 B f32 out)
+        # against 6.55 MFLOP at bf16/3 -> HBM-bound
+        "conv1_fwd_u8": ("hbm", PEAK_HBM_GBPS, "v_mfma_f32_16x16x32_bf16 x3 (u8 exact), image-resident"),
+    }
+
+
+PROFILED = profiled(6)
 CONV1_FWD_BYTES_PER_FLOP = 79424.0 / (2.0 * 400 * 32 * 256)
 
 
@@ -72,6 +82,8 @@ def parse():
     p.add_argument("--vec-len", type=int, default=14, help="vector obs length with --recurrent (OTC v7: 14)")
     p.add_argument("--profile-kernels", default=",".join(PROFILED),
                    help="kernels timed with HIP events; the one with the most time is the roofline kernel")
+    p.add_argument("--products", type=int, default=6, choices=(6, 9),
+                   help="part products per fp32 product in the split-bf16 GEMMs (9 = every product exact)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-envs", type=int, default=32)
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -166,6 +178,7 @@ def main():
     from a2c_ppo_acktr.storage import RolloutStorage
     from a2c_ppo_acktr.synthetic import SyntheticVecEnv
 
+    _hip.call("ppo_tune_set", b"products", args.products)
     N, T, E, M = args.envs, args.num_steps, args.ppo_epoch, args.num_mini_batch
     H = args.hidden or (256 if args.recurrent else 512)
     V = args.vec_len if args.recurrent else 0
@@ -240,7 +253,7 @@ def main():
     for name, (launches, ms_total, flops) in per_kernel.items():
         if launches <= 0 or ms_total <= 0:
             continue
-        bound, peak, how = PROFILED.get(name, ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"))
+        bound, peak, how = profiled(args.products).get(name, ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"))
         tflops = flops / (ms_total * 1e-3) / 1e12
         if bound == "hbm":
             achieved, unit = flops * CONV1_FWD_BYTES_PER_FLOP / (ms_total * 1e-3) / 1e9, "GB/s"
@@ -267,7 +280,7 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "split_products": args.products,
         "data": "synthetic: counter-hash u8 4x84x84 obs, U[0,1) rewards, Bernoulli(0.01) dones; random-init weights",
         "config": {"workload": workload,
                    "envs_per_gpu": N, "num_steps": T, "ppo_epoch": E, "num_mini_batch": M, "hidden": H,

@@ -135,8 +135,12 @@ int ppo_wgrad_reduce(const float* slab, const float* slab_bias, int Z, int M, in
 /* deterministic column sums out[c] = scale·Σ_r src[r*ld + c] (split-partial reduces) */
 int ppo_colsum(const float* src, long long ld, int rows, long long cols, float* out, float scale, int accumulate,
                void* stream);
-/* tile-configuration variant of a GEMM family (development A/B knob; 0 = default) */
+/* tile-configuration variant of a GEMM family (development A/B knob; 0 = default).
+ * key "products": part products per operand pair of the split-bf16 fp32 GEMMs,
+ * 6 (default: dropped terms < 2^-26 |a·b|) or 9 (every product exact) */
 int ppo_tune_set(const char* key, int value);
+/* current value of a tune key (-1 if unknown) */
+int ppo_tune_get(const char* key);
 
 /* ---------------- GRU (model.py:89-95, 111-166) ---------------------------- */
 /* one step h' = GRU(gi, h_prev·mask) with the cell fused into the W_hh GEMM;

@@ -57,6 +57,7 @@ SIGNATURES = {
     "ppo_wgrad_reduce": [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_f, c_int, c_p],
     "ppo_colsum": [c_p, c_ll, c_int, c_ll, c_p, c_f, c_int, c_p],
     "ppo_tune_set": [ctypes.c_char_p, c_int],
+    "ppo_tune_get": [ctypes.c_char_p],
     # heads.hip
     "ppo_heads_act": [c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_ull, c_ull, c_int, c_p, c_p, c_p,
                       c_p, c_p, c_p],

@@ -554,6 +554,7 @@ struct Conv2Dgrad : C_ {
 //   Wave w: n tile w & 3 (16 co), taps 8 (w >> 2) .. +7 (ky rows 0-1 / 2-3);
 //   its weight fragments (pre-split planes) in 96 VGPRs.  The two K halves are
 //   summed through LDS (half 1 writes, half 0 adds and stores).
+template <int NP>
 __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restrict__ a1, int B,
                                                           const uint16_t* __restrict__ wpl,
                                                           const float* __restrict__ bias,
@@ -643,8 +644,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restri
         }
 #define PPO_PART(X, Y) \
   _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(a[u].X, w.Y, acc[t0 + u]);
-        PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
-        PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+        PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       }
     }
@@ -696,6 +696,7 @@ __device__ __forceinline__ int c2w_pix(int r) {
   return r < 72 ? (r >> 3) * 9 + (r & 7) : (r - 72) * 9 + 8;
 }
 
+template <int NP>
 __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __restrict__ dz2,
                                                             const float* __restrict__ a1, int B,
                                                             float* __restrict__ slab,
@@ -819,8 +820,7 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
         bf.l = __builtin_bit_cast(bf16x8, __builtin_shufflevector(t[2][0], t[2][1], 0, 1, 2, 3, 4, 5, 6, 7));
 #define PPO_PART(XX, YY) \
   _Pragma("unroll") for (int mt = 0; mt < 4; ++mt) acc[j][mt] = mma(a[mt].XX, bf.YY, acc[j][mt]);
-        PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
-        PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+        PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       }
     }
@@ -859,6 +859,7 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
 // bytes (2 x 5,184 B): the next image is staged before the compute, one barrier
 // per image.  Wave w: ci tile w & 3 (weights, 9 taps x 3 planes, in 108 VGPRs),
 // row tiles 3 (w >> 2) .. +2.
+template <int NP>
 __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __restrict__ dz3, int B,
                                                             const uint16_t* __restrict__ wpl,
                                                             const float* __restrict__ a2,
@@ -945,8 +946,7 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
       }
 #define PPO_PART(X, Y) \
   _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[u] = mma(a[u].X, w.Y, acc[u]);
-      PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
-      PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+      PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
     }
     // epilogue: C row 4g + r of tile t is input pixel m; ReLU mask of a2
@@ -975,11 +975,12 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
 // the next image staged before the compute.  Wave w: co tile w & 1, K half
 // (w >> 1) & 1 (taps 0-4.5 / 4.5-8: 9 k-steps, weights in 108 VGPRs), row tiles
 // 2 (w >> 2) .. +1; K half 1 hands its partial sums over through LDS.
+template <int NP>
 __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restrict__ a2, int B,
                                                           const uint16_t* __restrict__ wpl,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ out) {
-  constexpr int NP = 84, PL = NP * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, UPER = (UNITS + 511) / 512;
+  constexpr int NPX = 84, PL = NPX * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, UPER = (UNITS + 511) / 512;
   __shared__ __attribute__((aligned(16))) uint16_t S[2][3 * PL];
   __shared__ __attribute__((aligned(16))) f32x4 R[2][2][2][2][64];   // [stage][co tile][row half][tile][lane]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
@@ -1044,8 +1045,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
       }
 #define PPO_PART(X, Y) \
   _Pragma("unroll") for (int u = 0; u < 2; ++u) acc[u] = mma(a[u].X, w.Y, acc[u]);
-      PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
-      PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+      PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
     }
     if (kh == 1) {
@@ -1084,6 +1084,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
 //   D [3][32 co][112]        dz3 transposed to [co][slot] (224-B rows: conflict-free
 //                            ds_read_b128 A fragments)
 // 12 waves (3 per SIMD), wave w: n tiles 3w .. 3w+2 (both co tiles).
+template <int NP>
 __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __restrict__ dz3,
                                                             const float* __restrict__ a2, int B,
                                                             float* __restrict__ slab,
@@ -1199,8 +1200,7 @@ __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __rest
         bf.l = __builtin_bit_cast(bf16x8, __builtin_shufflevector(t[2][0], t[2][1], 0, 1, 2, 3, 4, 5, 6, 7));
 #define PPO_PART(XX, YY) \
   _Pragma("unroll") for (int mt = 0; mt < 2; ++mt) acc[j][mt] = mma(a[mt].XX, bf.YY, acc[j][mt]);
-        PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
-        PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+        PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       }
     }
@@ -1242,6 +1242,7 @@ __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __rest
 //   repacking: lane (n, g) of k-step s reads W2d[n][64 g + 8 s .. +7].
 // Wave w owns n tile w (phase w >> 1, ci 16 (w & 1) + [0, 16)) for all of K,
 // its weight fragments (pre-split planes, 8 k-steps x 3) in 96 VGPRs.
+template <int NP>
 __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __restrict__ dz2, int B,
                                                             const uint16_t* __restrict__ wpl,
                                                             const float* __restrict__ a1,
@@ -1349,8 +1350,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
           }
 #define PPO_PART(X, Y)                                                  \
   _Pragma("unroll") for (int u = 0; u < TG; ++u) if (t0 + u < MT) acc[t0 + u] = mma(a[u].X, w.Y, acc[t0 + u]);
-        PPO_PART(l, l) PPO_PART(l, m) PPO_PART(m, l) PPO_PART(m, m) PPO_PART(l, h)
-        PPO_PART(m, h) PPO_PART(h, l) PPO_PART(h, m) PPO_PART(h, h)
+        PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       }
     }
@@ -1536,6 +1536,11 @@ static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad"
 static int g_tune[TK_N] = {0, 8, 8, 8, 1, 0, 8, 1, 8, 8};  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
+  if (strcmp(key, "products") == 0) {
+    PPO_REQUIRE(value == 6 || value == 9, "ppo_tune_set: products must be 6 or 9, got %d", value);
+    g_products = value;
+    return 0;
+  }
   for (int i = 0; i < TK_N; ++i)
     if (strcmp(key, g_tune_names[i]) == 0) {
       g_tune[i] = value;
@@ -1543,6 +1548,13 @@ PPO_API int ppo_tune_set(const char* key, int value) {
     }
   ppo_set_error("ppo_tune_set: unknown key %s", key);
   return PPO_EARG;
+}
+
+PPO_API int ppo_tune_get(const char* key) {
+  if (strcmp(key, "products") == 0) return g_products;
+  for (int i = 0; i < TK_N; ++i)
+    if (strcmp(key, g_tune_names[i]) == 0) return g_tune[i];
+  return -1;
 }
 
 // N = 32 output-channel problems (conv1/conv3 fwd, conv2 dgrad)
@@ -1691,7 +1703,7 @@ PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float*
     const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
     int slot;
     const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
-    conv2_fwd_x9_kernel<<<nb, 512, 0, as_stream(stream)>>>(a1, B, planes_of(w2p, 64 * 512), b2, out);
+    PPO_LAUNCH_NP(conv2_fwd_x9_kernel, nb, 512, as_stream(stream), a1, B, planes_of(w2p, 64 * 512), b2, out);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
     PPO_LAUNCH_CHECK("conv2_fwd_x9_kernel");
     return 0;
@@ -1716,7 +1728,7 @@ PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float*
     const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
     int slot;
     const bool prof = ppo_prof_begin("conv3_fwd", as_stream(stream), &slot);
-    conv3_fwd_x9_kernel<<<nb, 512, 0, as_stream(stream)>>>(a2, B, planes_of(w3p, 32 * 576), b3, out);
+    PPO_LAUNCH_NP(conv3_fwd_x9_kernel, nb, 512, as_stream(stream), a2, B, planes_of(w3p, 32 * 576), b3, out);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
     PPO_LAUNCH_CHECK("conv3_fwd_x9_kernel");
     return 0;
@@ -1858,7 +1870,7 @@ PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const flo
     const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
     int slot;
     const bool prof = ppo_prof_begin("conv3_dgrad", as_stream(stream), &slot);
-    conv3_dgrad_x9_kernel<<<nb, 512, 0, as_stream(stream)>>>(dz3, B, planes_of(w3d, 64 * 288), a2, dz2);
+    PPO_LAUNCH_NP(conv3_dgrad_x9_kernel, nb, 512, as_stream(stream), dz3, B, planes_of(w3d, 64 * 288), a2, dz2);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
     PPO_LAUNCH_CHECK("conv3_dgrad_x9_kernel");
     return 0;
@@ -1884,7 +1896,7 @@ PPO_API int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const flo
     int slot;
     const bool prof = ppo_prof_begin("conv2_dgrad", as_stream(stream), &slot);
     const uint16_t* wpl = planes_of(w2d, 128 * 256);
-    conv2_dgrad_x9_kernel<<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, a1, dz1);
+    PPO_LAUNCH_NP(conv2_dgrad_x9_kernel, nb, 512, as_stream(stream), dz2, B, wpl, a1, dz1);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
     PPO_LAUNCH_CHECK("conv2_dgrad_x9_kernel");
     return 0;
@@ -1970,7 +1982,7 @@ PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, flo
     if (B <= 0 || Z <= 0) return 0;
     int slot;
     const bool prof = ppo_prof_begin("conv2_wgrad", as_stream(stream), &slot);
-    conv2_wgrad_x9_kernel<<<Z, 512, 0, as_stream(stream)>>>(dz2, a1, B, slab, slab_bias);
+    PPO_LAUNCH_NP(conv2_wgrad_x9_kernel, Z, 512, as_stream(stream), dz2, a1, B, slab, slab_bias);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
     PPO_LAUNCH_CHECK("conv2_wgrad_x9_kernel");
     return 0;
@@ -1993,7 +2005,7 @@ PPO_API int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, flo
     if (B <= 0 || Z <= 0) return 0;
     int slot;
     const bool prof = ppo_prof_begin("conv3_wgrad", as_stream(stream), &slot);
-    conv3_wgrad_x9_kernel<<<Z, 768, 0, as_stream(stream)>>>(dz3, a2, B, slab, slab_bias);
+    PPO_LAUNCH_NP(conv3_wgrad_x9_kernel, Z, 768, as_stream(stream), dz3, a2, B, slab, slab_bias);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
     PPO_LAUNCH_CHECK("conv3_wgrad_x9_kernel");
     return 0;

@@ -61,13 +61,31 @@ __device__ __forceinline__ f32x4 mma(const bf16x8& a, const bf16x8& b, const f32
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Part products per operand pair: NP = 9 sums all nine (exact
+// products); NP = 6 (default) drops l·l, l·m and m·l, whose sum is below
+// 2^-26 |a·b| — a quarter of the rounding unit of one fp32 product, so the GEMM
+// keeps fp32 accuracy (the six-pass fp32 emulation, "bf16_6x").  Smallest first.
+#define PPO_PRODUCTS(NP, PART)                  \
+  if constexpr (NP == 9) { PART(l, l) PART(l, m) PART(m, l) } \
+  PART(m, m) PART(l, h) PART(m, h) PART(h, l) PART(h, m) PART(h, h)
+
+// split-product count of the launches below (ppo_tune_set("products", 6 | 9))
+static int g_products = 6;
+#define PPO_LAUNCH_NP(KERNEL, GRID, BLOCK, ST, ...)                   \
+  do {                                                                \
+    if (g_products == 9) KERNEL<9><<<GRID, BLOCK, 0, ST>>>(__VA_ARGS__); \
+    else KERNEL<6><<<GRID, BLOCK, 0, ST>>>(__VA_ARGS__);              \
+  } while (0)
+
 // c += Σ over the part pairs (smallest first); exact operands have hi only
-template <bool AX, bool BX>
+template <bool AX, bool BX, int NP>
 __device__ __forceinline__ f32x4 mma9(const Frag3& a, const Frag3& b, f32x4 c) {
   if constexpr (!AX && !BX) {
-    c = mma(a.l, b.l, c);
-    c = mma(a.l, b.m, c);
-    c = mma(a.m, b.l, c);
+    if constexpr (NP == 9) {
+      c = mma(a.l, b.l, c);
+      c = mma(a.l, b.m, c);
+      c = mma(a.m, b.l, c);
+    }
     c = mma(a.m, b.m, c);
   }
   if constexpr (!AX) {
@@ -118,7 +136,7 @@ __device__ __forceinline__ int pl_off(int row, int q) {   // bf16 element offset
   return row * 32 + 8 * (q ^ ((H4 >> (4 * ((row >> 2) & 3))) & 3));
 }
 
-template <class P>
+template <class P, int NP>
 __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
   constexpr int BM = P::BM, BN = P::BN, NT = P::NT, WM = P::WM, WN = P::WN, BK = 32;
   constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
@@ -299,7 +317,7 @@ __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
         fb.m = *reinterpret_cast<const bf16x8*>(Bp + BN * 32 + o);
         fb.l = *reinterpret_cast<const bf16x8*>(Bp + 2 * BN * 32 + o);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) acc[i][j] = mma9<P::A_EXACT, false>(fa[i], fb, acc[i][j]);
+        for (int i = 0; i < TM; ++i) acc[i][j] = mma9<P::A_EXACT, false, NP>(fa[i], fb, acc[i][j]);
       }
     } else {
       Frag3 fb[TN];
@@ -310,7 +328,7 @@ __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
         Frag3 fa;
         frag(As, (wm * TM + i) * 16 + fr, fa, P::A_EXACT);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mma9<P::A_EXACT, P::B_EXACT>(fa, fb[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mma9<P::A_EXACT, P::B_EXACT, NP>(fa, fb[j], acc[i][j]);
       }
     }
     if (kt + 1 < nk) sstore(buf ^ 1);
@@ -350,7 +368,8 @@ int launch_x9(const P& p, long long M, int N, int Z, hipStream_t st, const char*
   dim3 grid((unsigned)gx, (unsigned)((N + P::BN - 1) / P::BN), (unsigned)Z);
   int slot;
   const bool prof = ppo_prof_begin(name, st, &slot);
-  igemm_x9_kernel<P><<<grid, P::NT, 0, st>>>(p);
+  if (g_products == 9) igemm_x9_kernel<P, 9><<<grid, P::NT, 0, st>>>(p);
+  else igemm_x9_kernel<P, 6><<<grid, P::NT, 0, st>>>(p);
   if (prof) ppo_prof_end(slot, st, flops);
   PPO_LAUNCH_CHECK(name);
   return 0;

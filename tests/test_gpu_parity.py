@@ -979,3 +979,71 @@ def test_conv3_wgrad_variants_vs_torch(gpu, variant):
     for got, ref in ((gw.cpu().double().view(32, 64, 3, 3), ref_w), (gb.cpu().double(), ref_b)):
         err = (got - ref).abs().max().item()
         assert err <= 1e-5 * ref.abs().max().item(), err
+
+
+def _conv_ops(gpu, B, seed):
+    """The six image-resident split kernels on one random problem each; returns
+    {name: (gpu fp32 result, float64 reference, torch CPU fp32 result)}."""
+    Hh = _hip()
+    w, packed, pk = _packed(gpu, 64, seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    a1 = torch.relu(torch.randn(B, 20, 20, 32, generator=g))
+    a2 = torch.relu(torch.randn(B, 9, 9, 64, generator=g))
+    dz2 = torch.randn(B, 9, 9, 64, generator=g)
+    dz3 = torch.randn(B, 7, 7, 32, generator=g)
+    b2, b3 = torch.randn(64, generator=g) * 0.1, torch.randn(32, generator=g) * 0.1
+    d = {k: v.cuda() for k, v in dict(a1=a1, a2=a2, dz2=dz2, dz3=dz3, b2=b2, b3=b3).items()}
+    s = _s()
+    out = {}
+    o = torch.empty(B, 9, 9, 64, device=gpu)
+    Hh.call("ppo_conv2_fwd", d["a1"].data_ptr(), B, pk[0], d["b2"].data_ptr(), o.data_ptr(), s)
+    nchw = lambda t: t.permute(0, 3, 1, 2)
+    f = lambda x, w_, b_, st: torch.relu(F.conv2d(nchw(x), w_, b_, stride=st)).permute(0, 2, 3, 1)
+    out["conv2_fwd"] = (o, f(a1.double(), w["w2"].double(), b2.double(), 2), f(a1, w["w2"], b2, 2))
+    o = torch.empty(B, 7, 7, 32, device=gpu)
+    Hh.call("ppo_conv3_fwd", d["a2"].data_ptr(), B, pk[1], d["b3"].data_ptr(), o.data_ptr(), s)
+    out["conv3_fwd"] = (o, f(a2.double(), w["w3"].double(), b3.double(), 1), f(a2, w["w3"], b3, 1))
+    ct = lambda dz, w_, mask, st: torch.where(mask > 0, F.conv_transpose2d(nchw(dz), w_, stride=st).permute(0, 2, 3, 1),
+                                              torch.zeros((), dtype=dz.dtype))
+    o = torch.empty(B, 20, 20, 32, device=gpu)
+    Hh.call("ppo_conv2_dgrad", d["dz2"].data_ptr(), B, pk[5], d["a1"].data_ptr(), o.data_ptr(), s)
+    out["conv2_dgrad"] = (o, ct(dz2.double(), w["w2"].double(), a1, 2), ct(dz2, w["w2"], a1, 2))
+    o = torch.empty(B, 9, 9, 64, device=gpu)
+    Hh.call("ppo_conv3_dgrad", d["dz3"].data_ptr(), B, pk[4], d["a2"].data_ptr(), o.data_ptr(), s)
+    out["conv3_dgrad"] = (o, ct(dz3.double(), w["w3"].double(), a2, 1), ct(dz3, w["w3"], a2, 1))
+    for name, x, dz, co, K, ks, st, tap in (("conv2_wgrad", "a1", "dz2", 64, 512, 4, 2, 81),
+                                            ("conv3_wgrad", "a2", "dz3", 32, 576, 3, 1, 49)):
+        Z = Hh.call("ppo_wgrad_splits", B * tap, 4 if ks == 4 else 5, 2048, 16)
+        slab, slab_b = torch.empty(Z * co * K, device=gpu), torch.empty(Z * co, device=gpu)
+        gw, gb = torch.empty(co * K, device=gpu), torch.empty(co, device=gpu)
+        Hh.call("ppo_" + name, d[dz].data_ptr(), d[x].data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), s)
+        Hh.call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, co, K, 1, ks, K // (ks * ks),
+                gw.data_ptr(), gb.data_ptr(), 1.0, 0, s)
+        xs, dzs = dict(a1=a1, a2=a2)[x], dict(dz2=dz2, dz3=dz3)[dz]
+        cw = lambda xx, dd: torch.nn.grad.conv2d_weight(nchw(xx), (co, K // (ks * ks), ks, ks), nchw(dd), stride=st)
+        out[name] = (gw.view(co, K // (ks * ks), ks, ks), cw(xs.double(), dzs.double()), cw(xs, dzs))
+    torch.cuda.synchronize()
+    return out
+
+
+def test_split_products_fp32_accuracy(gpu):
+    """Six part products per operand pair (the default) keep fp32 accuracy: on
+    every image-resident split kernel, the error vs float64 (max |err| / max |ref|)
+    stays within 2x that of the exact nine-product path and within 4x that of
+    torch's own CPU fp32 convolution on the same inputs; both below 1e-6."""
+    Hh = _hip()
+    B = 300
+    res = {}
+    for np_ in (9, 6):
+        Hh.call("ppo_tune_set", b"products", np_)
+        try:
+            res[np_] = _conv_ops(gpu, B, 70)
+        finally:
+            Hh.call("ppo_tune_set", b"products", 6)
+    rel = lambda got, ref: ((got.cpu().double() - ref).abs().max() / ref.abs().max()).item()
+    for name in res[6]:
+        e6 = rel(res[6][name][0], res[6][name][1])
+        e9 = rel(res[9][name][0], res[9][name][1])
+        ecpu = rel(res[6][name][2], res[6][name][1])
+        print(f"{name}: x6 {e6:.3e}  x9 {e9:.3e}  torch-cpu-fp32 {ecpu:.3e}")
+        assert e6 <= 2 * e9 + 1e-9 and e6 <= 4 * ecpu + 1e-9 and e6 < 1e-6, (name, e6, e9, ecpu)
