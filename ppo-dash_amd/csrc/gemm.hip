@@ -1533,7 +1533,7 @@ enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRA
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
                                          "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
-static int g_tune[TK_N] = {0, 8, 8, 8, 1, 0, 8, 1, 8, 8};  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 8, 8, 8, 1, 0, 8, 1, 8, 8};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   if (strcmp(key, "products") == 0) {
@@ -1601,6 +1601,7 @@ using XW128 = CfgX<128, 128, 2, 2, false, false, true>; // wgrad, >= 128 output 
 using XP32 = CfgX<128, 32, 4, 1, true, true, false, false, false, true>;    // B from planes, waves 32x32
 using XP64 = CfgX<128, 64, 4, 1, true, true, false, false, false, true>;    // waves 32x64
 using XP128 = CfgX<128, 128, 4, 1, true, true, false, false, false, true>;  // waves 32x128
+using XP64s = CfgX<64, 64, 2, 1, true, true, false, false, false, true>;    // 2 waves of 32x64
 // x9 = 1: the split-bf16 core where it measured faster (forward GEMMs, fc dgrad); the gather-heavy
 // conv dgrads and the wgrads stay on fp32 MFMA (their split path is VALU-bound); x9 = 2: everywhere
 // compute units of the current device (persistent-kernel grid size)
@@ -1753,10 +1754,24 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
   PPO_REQUIRE(H > 0 && H % 8 == 0 && ldo >= H, "ppo_fc_fwd: H=%d ldo=%d", H, ldo);
   const int K = 1568;
   if (use_x9()) {
-    DenseReluFwd<XP128> p;
-    p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1;
-    set_planes(p, w4p, (long long)H * K, H, K);
-    return launch_x9(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);
+    // rollout-sized M (4096 rows) fills a quarter of the chip with 128 x 128
+    // tiles: narrower tiles there (fc_fwd tune: 0 auto, 1 128x128, 2 128x64, 3 64x64)
+    int v = g_tune[TK_FC_FWD];
+    if (v == 0) {
+      const long long t128 = ((M + 127LL) / 128) * ((H + 127) / 128);
+      v = t128 >= 2LL * device_cus() ? 1 : 2;   // measured: 128x64 best at M = 4096
+    }
+#define PPO_FC(CFG)                                                                                  \
+  {                                                                                                  \
+    DenseReluFwd<CFG> p;                                                                             \
+    p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1; \
+    set_planes(p, w4p, (long long)H * K, H, K);                                                      \
+    return launch_x9(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);                      \
+  }
+    if (v == 2) PPO_FC(XP64)
+    if (v == 3) PPO_FC(XP64s)
+    PPO_FC(XP128)
+#undef PPO_FC
   }
   DenseReluFwd<CfgN128> p;
   p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1;
@@ -2026,7 +2041,9 @@ PPO_API int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, flo
 PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int K, int Z, float* slab,
                              float* slab_bias, void* stream) {
   PPO_REQUIRE(N % 4 == 0 && K % 4 == 0, "ppo_linear_wgrad: N=%d K=%d must be multiples of 4", N, K);
-  if (use_x9_all()) {
+  // split path: the fc layer (N >= 128) whenever the split core is on (0.82 vs
+  // 1.03 ms at the c3 minibatch); the narrow GRU/MLP layers only with x9 = 2
+  if (use_x9_all() || (use_x9() && N >= 128)) {
     if (N <= 64) {
       DenseWgrad<XW64> p;
       set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);

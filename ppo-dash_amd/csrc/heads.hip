@@ -370,7 +370,8 @@ int launch_act(const float* feat, const float* feat_v, int N, int H, const float
                const float* ba,
                int A, const float* noise, unsigned long long seed, unsigned long long counter, int det,
                const int64_t* given, float* v, int64_t* act, float* lp, float* ent, hipStream_t st) {
-  const int rpw = 8;
+  // ~2048 waves in flight (8 per CU): a rollout batch of 4096 rows takes 2 per wave
+  const int rpw = (int)std::min<long long>(8, std::max<long long>(1, ceil_div(N, 2048)));
   const unsigned blocks = ceil_div(N, HW * rpw);
   heads_act_kernel<HC, AMAX><<<blocks, 64 * HW, 0, st>>>(feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter,
                                                         det,
