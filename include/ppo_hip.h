@@ -142,6 +142,23 @@ int ppo_tune_set(const char* key, int value);
 /* current value of a tune key (-1 if unknown) */
 int ppo_tune_get(const char* key);
 
+/* ---------------- observation boundary ------------ */
+/* NormalizeWrapper (ppo-dash-study/013_…/sohojoe_wrappers.py:872-884) +
+ * FrameStackMono(k=2) (:425-501) + TransposeImage (pytorch_wrappers.py:170-203)
+ * + VecPyTorch .float() (:105-160), fused: src u8 [N][S][S][3] RGB frames (env
+ * stride src_stride bytes) -> dst fp32 [N][3 (+1 mono)][S][S] (env stride
+ * dst_stride floats).  mode 0: raw values, 1: u8/255, 2: (u8 - mean[S][S][3]) / std
+ * (float64 arithmetic, as numpy, then rounded to fp32).  mono: append the
+ * reference's (transposed) cv2 RGB2GRAY channel. */
+int ppo_obs_preprocess(const uint8_t* src, long long src_stride, int N, int S, int mode, const double* mean,
+                       double stdv, int mono, float* dst, long long dst_stride, void* stream);
+/* VecPyTorchFrameStack.step_wait / reset (pytorch_wrappers.py:58-102) on
+ * stacked [N][nstack][frame_elems]: shift one frame left, zero envs with done[n]
+ * (u8, nullable), write obs [N][frame_elems] into the last slot; reset = 1 zeroes
+ * every slot first */
+int ppo_frame_stack(float* stacked, int N, int nstack, long long frame_elems, const float* obs,
+                    const uint8_t* done, int reset, void* stream);
+
 /* ---------------- GRU (model.py:89-95, 111-166) ---------------------------- */
 /* one step h' = GRU(gi, h_prev·mask) with the cell fused into the W_hh GEMM;
  * save_* (all or none) keep r, z, n, W_hn·h+b_hn, h_in for the backward */

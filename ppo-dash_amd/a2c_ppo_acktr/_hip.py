@@ -75,6 +75,9 @@ SIGNATURES = {
     "ppo_rec_indices": [c_p, c_int, c_int, c_int, c_p, c_p],
     "ppo_heads_reduce": [c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_d, c_f, c_int, c_p],
     "ppo_mean_f32": [c_p, c_ll, c_p, c_p],
+    # obs.hip
+    "ppo_obs_preprocess": [c_p, c_ll, c_int, c_int, c_int, c_p, c_d, c_int, c_p, c_ll, c_p],
+    "ppo_frame_stack": [c_p, c_int, c_int, c_ll, c_p, c_p, c_int, c_p],
     # optim.hip
     "ppo_grad_partials_count": [c_ll],
     "ppo_grad_sumsq": [c_p, c_ll, c_f, c_p, c_p],

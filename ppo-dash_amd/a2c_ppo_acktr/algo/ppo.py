@@ -49,6 +49,7 @@ class FlatAdam(object):
         if self.exp_avg is None or self.exp_avg.numel() != n or self.exp_avg.device != eng.device:
             self.exp_avg = torch.zeros(n, device=eng.device)
             self.exp_avg_sq = torch.zeros(n, device=eng.device)
+        if self._partials is None or self._partials.device != eng.device:   # also after load_state_dict
             self._partials = torch.empty(call("ppo_grad_partials_count", n), dtype=torch.float64, device=eng.device)
             self._norm = torch.zeros(1, dtype=torch.float64, device=eng.device)
         scale = _dist.allreduce_grads(eng.grad)

@@ -55,6 +55,9 @@ class Policy(nn.Module):
                 base = MLPBase
             else:
                 raise NotImplementedError
+        # constructor arguments, for checkpoint.save_checkpoint (state_dict-based files)
+        self._ctor = {"obs_shape": tuple(obs_shape), "action_space": action_space, "base_kwargs": dict(base_kwargs),
+                      "vector_obs_len": vector_obs_len}
         self.base = base(obs_shape[0], vector_obs_len, **base_kwargs)
         if action_space.__class__.__name__ == "Discrete":
             num_outputs = action_space.n

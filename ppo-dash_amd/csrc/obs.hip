@@ -1,0 +1,121 @@
+// Observation boundary on the GPU: the env-side
+// wrappers that turn a raw u8 RGB frame into the policy input, fused into one
+// pass over the frame, and the device-side frame stack.
+//
+// Reference (ppo-dash-study/013_…/, the "norm_obs" variants; T/ has the same
+// classes with the `if self.mean:` bug that raises on an ndarray):
+//   NormalizeWrapper.observation   sohojoe_wrappers.py:872-884
+//       x = (u8 - mean[y][x][c]) / std   (float64; mean/std from ObtRetro-v6_*.txt)
+//       or x = u8 / 255                  (float64, no normaliser file)
+//   FrameStackMono(k=2)._add_ob/_get_ob  sohojoe_wrappers.py:425-501
+//       channels = R, G, B of the current frame + mono_frames[1], the current
+//       frame's cv2 RGB2GRAY of x.astype(float32); np.array(frames).T transposes
+//       the (H, W) mono image against the (W, H) colour planes, so the mono
+//       channel at (y, x) is gray(frame[x][y]) — reproduced here (H == W).
+//   TransposeImage op=[2,0,1]      pytorch_wrappers.py:170-203   HWC -> CHW
+//   VecPyTorch.step_wait .float()  pytorch_wrappers.py:105-160   float64 -> fp32
+//   VecPyTorchFrameStack           pytorch_wrappers.py:58-102
+//       stacked[:, :-C] = stacked[:, C:]; stacked[i] = 0 where done; stacked[:, -C:] = obs
+//
+// Both kernels are HBM-bound streams (u8 in, fp32 out); one thread per pixel.
+#include "common.h"
+
+namespace {
+
+constexpr int OBS_THREADS = 256;
+
+// cv2 cvtColor(COLOR_RGB2GRAY) on float32: R*0.299f + G*0.587f + B*0.114f, summed
+// left to right (OpenCV's RGB2Gray<float> scalar loop); this file is built with
+// -ffp-contract=off (Makefile): hipcc's default contraction would fuse the last add
+__device__ __forceinline__ float gray_f32(float r, float g, float b) {
+  return __fadd_rn(__fadd_rn(__fmul_rn(r, 0.299f), __fmul_rn(g, 0.587f)), __fmul_rn(b, 0.114f));
+}
+
+// NormalizeWrapper value of byte u at element e of the (y, x, c) frame, float64
+__device__ __forceinline__ double norm_value(uint32_t u, int mode, const double* __restrict__ mean, double inv_or_std,
+                                             long long e) {
+  if (mode == 2) return ((double)u - mean[e]) / inv_or_std;
+  if (mode == 1) return (double)u / 255.0;
+  return (double)u;
+}
+
+__global__ __launch_bounds__(OBS_THREADS) void obs_preprocess_kernel(
+    const uint8_t* __restrict__ src, long long src_stride, int N, int S, int mode, const double* __restrict__ mean,
+    double stdv, int mono, float* __restrict__ dst, long long dst_stride) {
+  const long long px = (long long)S * S;
+  const long long total = (long long)N * px;
+  for (long long i = (long long)blockIdx.x * OBS_THREADS + threadIdx.x; i < total;
+       i += (long long)gridDim.x * OBS_THREADS) {
+    const int n = (int)(i / px);
+    const int p = (int)(i - (long long)n * px);
+    const int y = p / S, x = p - y * S;
+    const uint8_t* f = src + (size_t)n * src_stride;
+    float* o = dst + (size_t)n * dst_stride;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const long long e = (long long)p * 3 + c;
+      o[(size_t)c * px + p] = (float)norm_value(f[e], mode, mean, stdv, e);
+    }
+    if (mono) {
+      const long long q = (long long)x * S + y;   // transposed pixel (see header)
+      float v[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c] = (float)norm_value(f[q * 3 + c], mode, mean, stdv, q * 3 + c);
+      float gm = gray_f32(v[0], v[1], v[2]);
+      if (mode == 0) gm = (float)(uint8_t)gm;   // mono.astype(uint8) when the frame is still u8
+      o[3 * px + p] = gm;
+    }
+  }
+}
+
+// one thread per (env, element of one frame): walk the nstack slots upward
+// (slot s reads slot s+1 before slot s+1 is written: no race, in place)
+__global__ __launch_bounds__(OBS_THREADS) void frame_stack_kernel(float* __restrict__ stacked, int N, int nstack,
+                                                                  long long fe, const float* __restrict__ obs,
+                                                                  const uint8_t* __restrict__ done, int reset) {
+  const long long total = (long long)N * fe;
+  for (long long i = (long long)blockIdx.x * OBS_THREADS + threadIdx.x; i < total;
+       i += (long long)gridDim.x * OBS_THREADS) {
+    const int n = (int)(i / fe);
+    const long long e = i - (long long)n * fe;
+    float* st = stacked + (size_t)n * nstack * fe + e;
+    const bool zero = reset || (done && done[n]);
+    for (int s = 0; s + 1 < nstack; ++s) st[(size_t)s * fe] = zero ? 0.f : st[(size_t)(s + 1) * fe];
+    st[(size_t)(nstack - 1) * fe] = obs[(size_t)n * fe + e];
+  }
+}
+
+unsigned grid_for(long long total) {
+  const long long b = (total + OBS_THREADS - 1) / OBS_THREADS;
+  return (unsigned)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+}  // namespace
+
+PPO_API int ppo_obs_preprocess(const uint8_t* src, long long src_stride, int N, int S, int mode, const double* mean,
+                               double stdv, int mono, float* dst, long long dst_stride, void* stream) {
+  PPO_REQUIRE(N >= 0 && S > 0 && mode >= 0 && mode <= 2, "ppo_obs_preprocess: N=%d S=%d mode=%d", N, S, mode);
+  PPO_REQUIRE(mode != 2 || (mean != nullptr && stdv != 0.0), "ppo_obs_preprocess: mode 2 needs mean and std != 0");
+  PPO_REQUIRE(src_stride >= 3LL * S * S && dst_stride >= (3LL + (mono ? 1 : 0)) * S * S,
+              "ppo_obs_preprocess: strides %lld / %lld too small for %dx%dx3", src_stride, dst_stride, S, S);
+  if (N == 0) return 0;
+  int slot;
+  const bool prof = ppo_prof_begin("obs_preprocess", as_stream(stream), &slot);
+  obs_preprocess_kernel<<<grid_for((long long)N * S * S), OBS_THREADS, 0, as_stream(stream)>>>(
+      src, src_stride, N, S, mode, mean, stdv, mono, dst, dst_stride);
+  // algorithmic bytes: 3 u8 in + (3 + mono) f32 out per pixel
+  if (prof) ppo_prof_end(slot, as_stream(stream), (double)N * S * S * (3.0 + 4.0 * (3 + (mono ? 1 : 0))));
+  PPO_LAUNCH_CHECK("obs_preprocess_kernel");
+  return 0;
+}
+
+PPO_API int ppo_frame_stack(float* stacked, int N, int nstack, long long frame_elems, const float* obs,
+                            const uint8_t* done, int reset, void* stream) {
+  PPO_REQUIRE(N >= 0 && nstack >= 1 && frame_elems > 0, "ppo_frame_stack: N=%d nstack=%d frame=%lld", N, nstack,
+              frame_elems);
+  if (N == 0) return 0;
+  frame_stack_kernel<<<grid_for((long long)N * frame_elems), OBS_THREADS, 0, as_stream(stream)>>>(
+      stacked, N, nstack, frame_elems, obs, done, reset);
+  PPO_LAUNCH_CHECK("frame_stack_kernel");
+  return 0;
+}
