@@ -88,6 +88,7 @@ def parse():
     p.add_argument("--cpu-envs", type=int, default=32)
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-gae-roofline", action="store_true")
+    p.add_argument("--no-boundary", action="store_true", help="skip the observation-boundary measurement")
     p.add_argument("--gae-lanes", type=int, default=1 << 20)
     return p.parse_args()
 
@@ -124,6 +125,59 @@ def gae_roofline(device, lanes, T=128, reps=10):
             "frac": round(gbps / PEAK_HBM_GBPS, 4), "traffic": None,
             "config": f"T={T} x {lanes} lanes (fp32 planes, {nbytes / 1e9:.2f} GB algorithmic per launch)",
             "ms_per_launch": round(ms, 4)}
+
+
+def boundary_roofline(device, frames=16384, reps=5, cpu_frames=64):
+    """Observation boundary: the fused NormalizeWrapper +
+    FrameStackMono(2) + TransposeImage + .float() kernel on `frames` raw u8 RGB
+    frames (algorithmic bytes per frame: 84*84*3 u8 in + 84*84*4 fp32 out), the
+    pinned host->device rate of one rollout step of u8 frames (4096 envs), and
+    the oracle's numpy restatement of the reference's per-env chain on the host."""
+    from a2c_ppo_acktr.vec_env import ObsPreprocess
+    S = 84
+    g = torch.Generator(device=device).manual_seed(0)
+    fr = torch.randint(0, 256, (frames, S, S, 3), dtype=torch.uint8, device=device, generator=g)
+    mean = np.random.default_rng(0).uniform(20, 80, (S, S, 3))
+    pre = ObsPreprocess(S, "norm", mean, 36.3, device=device)
+    out = torch.empty(frames, 4, S, S, device=device)
+    pre(fr, out=out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        pre(fr, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    per = S * S * (3 + 16)
+    gbps = frames * per / (ms * 1e-3) / 1e9
+    del fr, out
+    host = torch.randint(0, 256, (4096, S, S, 3), dtype=torch.uint8).pin_memory()
+    dev = torch.empty_like(host, device=device)
+    dev.copy_(host, non_blocking=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        dev.copy_(host, non_blocking=True)
+    e1.record()
+    torch.cuda.synchronize()
+    h2d_ms = e0.elapsed_time(e1) / reps
+    del host, dev
+    torch.cuda.empty_cache()
+    from oracle import obs_oracle as OO
+    cf = np.random.default_rng(1).integers(0, 256, (cpu_frames, S, S, 3), dtype=np.uint8)
+    t0 = time.perf_counter()
+    OO.preprocess_batch(cf, mean=mean, std=36.3)
+    cpu_s = time.perf_counter() - t0
+    return {"bound": "hbm", "achieved": round(gbps, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+            "frac": round(gbps / PEAK_HBM_GBPS, 4), "kernel": "obs_preprocess (norm + grey + transpose + fp32)",
+            "config": f"{frames} raw 84x84x3 u8 frames, {per} B algorithmic per frame",
+            "frames_per_s": round(frames / (ms * 1e-3), 1), "ms_per_launch": round(ms, 4),
+            "h2d_u8_step_ms": round(h2d_ms, 4),
+            "h2d_u8_env_steps_per_s": round(4096 / (h2d_ms * 1e-3), 1),
+            "cpu_baseline": {"value": round(cpu_frames / cpu_s, 1), "unit": "frames/s", "cores": 1, "kind": "port",
+                             "sample": f"oracle numpy restatement of NormalizeWrapper + FrameStackMono(2) + "
+                                       f"TransposeImage + .float() (013 chain), {cpu_frames} frames"}}
 
 
 def pmc_traffic(kernel, workload):
@@ -217,6 +271,9 @@ def main():
     gae = None
     if rank == 0 and not args.no_gae_roofline:
         gae = gae_roofline(device, args.gae_lanes)
+    boundary = None
+    if rank == 0 and not args.no_boundary:
+        boundary = boundary_roofline(device)
 
     cap = args.steps * (T + 2 * E * M + 8) + 16
     names = [k for k in args.profile_kernels.split(",") if k]
@@ -285,7 +342,8 @@ def main():
         "config": {"workload": workload,
                    "envs_per_gpu": N, "num_steps": T, "ppo_epoch": E, "num_mini_batch": M, "hidden": H,
                    "global_batch": N * T * world, "parallelism": f"dp{world}"},
-        "roofline": roof, "cpu_baseline": cpu, "gae_roofline": gae, "kernel_rooflines": kernels,
+        "roofline": roof, "cpu_baseline": cpu, "gae_roofline": gae, "boundary_roofline": boundary,
+        "kernel_rooflines": kernels,
         "losses": [round(x, 6) for x in losses],
     }
     print(json.dumps(out))

@@ -39,31 +39,48 @@ __device__ __forceinline__ double norm_value(uint32_t u, int mode, const double*
   return (double)u;
 }
 
+// One block per frame (blocks walk frames): the frame's bytes are staged in LDS
+// with coalesced dword loads, every pixel is normalised once (3 float64 divides),
+// the colour planes are written straight out and the grey value goes to LDS, from
+// where the transposed mono plane is written (coalesced on the output side).
+// Dynamic LDS: S*S*3 bytes (frame, rounded to dwords) + S*S floats (grey).
 __global__ __launch_bounds__(OBS_THREADS) void obs_preprocess_kernel(
     const uint8_t* __restrict__ src, long long src_stride, int N, int S, int mode, const double* __restrict__ mean,
-    double stdv, int mono, float* __restrict__ dst, long long dst_stride) {
-  const long long px = (long long)S * S;
-  const long long total = (long long)N * px;
-  for (long long i = (long long)blockIdx.x * OBS_THREADS + threadIdx.x; i < total;
-       i += (long long)gridDim.x * OBS_THREADS) {
-    const int n = (int)(i / px);
-    const int p = (int)(i - (long long)n * px);
-    const int y = p / S, x = p - y * S;
+    double stdv, int mono, float* __restrict__ dst, long long dst_stride, int aligned) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int px = S * S, nb = px * 3, nw = (nb + 3) / 4;
+  uint32_t* fw = reinterpret_cast<uint32_t*>(lds);
+  float* gray = reinterpret_cast<float*>(lds + 4 * nw);
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
     const uint8_t* f = src + (size_t)n * src_stride;
     float* o = dst + (size_t)n * dst_stride;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const long long e = (long long)p * 3 + c;
-      o[(size_t)c * px + p] = (float)norm_value(f[e], mode, mean, stdv, e);
+    __syncthreads();   // the previous frame's LDS reads are done
+    if (aligned) {
+      const uint32_t* fs = reinterpret_cast<const uint32_t*>(f);
+      for (int w = threadIdx.x; w < nw; w += OBS_THREADS) fw[w] = fs[w];   // nb % 4 == 0 when aligned
+    } else {
+      for (int b = threadIdx.x; b < nb; b += OBS_THREADS) lds[b] = f[b];
     }
-    if (mono) {
-      const long long q = (long long)x * S + y;   // transposed pixel (see header)
+    __syncthreads();
+    for (int p = threadIdx.x; p < px; p += OBS_THREADS) {
       float v[3];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) v[c] = (float)norm_value(f[q * 3 + c], mode, mean, stdv, q * 3 + c);
-      float gm = gray_f32(v[0], v[1], v[2]);
-      if (mode == 0) gm = (float)(uint8_t)gm;   // mono.astype(uint8) when the frame is still u8
-      o[3 * px + p] = gm;
+      for (int c = 0; c < 3; ++c) {
+        v[c] = (float)norm_value(lds[3 * p + c], mode, mean, stdv, 3LL * p + c);
+        o[(size_t)c * px + p] = v[c];
+      }
+      if (mono) {
+        float gm = gray_f32(v[0], v[1], v[2]);
+        if (mode == 0) gm = (float)(uint8_t)gm;   // mono.astype(uint8) when the frame is still u8
+        gray[p] = gm;
+      }
+    }
+    if (mono) {
+      __syncthreads();
+      for (int p = threadIdx.x; p < px; p += OBS_THREADS) {
+        const int y = p / S, x = p - y * S;
+        o[(size_t)3 * px + p] = gray[x * S + y];   // transposed pixel (see header)
+      }
     }
   }
 }
@@ -98,11 +115,14 @@ PPO_API int ppo_obs_preprocess(const uint8_t* src, long long src_stride, int N, 
   PPO_REQUIRE(mode != 2 || (mean != nullptr && stdv != 0.0), "ppo_obs_preprocess: mode 2 needs mean and std != 0");
   PPO_REQUIRE(src_stride >= 3LL * S * S && dst_stride >= (3LL + (mono ? 1 : 0)) * S * S,
               "ppo_obs_preprocess: strides %lld / %lld too small for %dx%dx3", src_stride, dst_stride, S, S);
+  const long long lds_bytes = 4LL * ((3LL * S * S + 3) / 4) + 4LL * S * S;
+  PPO_REQUIRE(lds_bytes <= 160 * 1024, "ppo_obs_preprocess: %dx%d frames exceed the LDS (%lld B)", S, S, lds_bytes);
   if (N == 0) return 0;
+  const int aligned = ((uintptr_t)src % 4 == 0) && (src_stride % 4 == 0) && ((3 * S * S) % 4 == 0);
   int slot;
   const bool prof = ppo_prof_begin("obs_preprocess", as_stream(stream), &slot);
-  obs_preprocess_kernel<<<grid_for((long long)N * S * S), OBS_THREADS, 0, as_stream(stream)>>>(
-      src, src_stride, N, S, mode, mean, stdv, mono, dst, dst_stride);
+  obs_preprocess_kernel<<<(unsigned)(N < 4096 ? N : 4096), OBS_THREADS, (size_t)lds_bytes, as_stream(stream)>>>(
+      src, src_stride, N, S, mode, mean, stdv, mono, dst, dst_stride, aligned);
   // algorithmic bytes: 3 u8 in + (3 + mono) f32 out per pixel
   if (prof) ppo_prof_end(slot, as_stream(stream), (double)N * S * S * (3.0 + 4.0 * (3 + (mono ? 1 : 0))));
   PPO_LAUNCH_CHECK("obs_preprocess_kernel");
