@@ -180,6 +180,52 @@ def boundary_roofline(device, frames=16384, reps=5, cpu_frames=64):
                                        f"TransposeImage + .float() (013 chain), {cpu_frames} frames"}}
 
 
+def eval_latency(device, H=256, V=14, steps=200, cpu_steps=20):
+    """Evaluation path (SURVEY §8f f4, T/run_evaluation.py:25-122): one env,
+    deterministic act with the GRU (H=256) + 14 vector obs of the OTC policy.
+    Wall time per act, eager vs replayed from a HIP graph, synchronised each step
+    (as the env loop needs the action), next to the oracle's float64 forward of
+    one sample on the host."""
+    from a2c_ppo_acktr.evaluation import GraphedActor
+    from a2c_ppo_acktr.model import CNNBase, Policy
+    from a2c_ppo_acktr.synthetic import Discrete
+    torch.manual_seed(1)
+    pol = Policy((4, 84, 84), Discrete(8), base=CNNBase, base_kwargs={"recurrent": True, "hidden_size": H},
+                 vector_obs_len=V)
+    flat = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy().astype(np.float64)
+    pol.to(device)
+    obs = torch.rand(1, 4, 84, 84, device=device)
+    vec = torch.rand(1, V, device=device)
+    hx = torch.zeros(1, H, device=device)
+    m = torch.ones(1, 1, device=device)
+    ga = GraphedActor(pol)
+    res = {}
+    for name, fn in (("eager", lambda h: pol.act(obs, vec, h, m, deterministic=True)),
+                     ("graph", lambda h: ga.act(obs, vec, h, m))):
+        h = hx
+        for _ in range(10):
+            h = fn(h)[3]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            with torch.no_grad():
+                _, a, _, h = fn(h)
+            a.item()   # the env step needs the action on the host
+        res[name] = (time.perf_counter() - t0) / steps * 1e3
+    from oracle import ppo_oracle as O
+    p = O.unflatten(flat, O.cnn_param_shapes(H, recurrent=True, vector_obs_len=V))
+    o, v, h0 = np.random.rand(1, 4, 84, 84), np.random.rand(1, V), np.zeros((1, H))
+    t0 = time.perf_counter()
+    for _ in range(cpu_steps):
+        O.recurrent_forward(p, o, v, h0, np.ones((1, 1)))
+    cpu_ms = (time.perf_counter() - t0) / cpu_steps * 1e3
+    return {"config": f"1 env, CNNBase+GRU H={H} + {V} vector obs, deterministic act, synchronised per step",
+            "eager_ms_per_act": round(res["eager"], 4), "graph_ms_per_act": round(res["graph"], 4),
+            "graph_acts_per_s": round(1e3 / res["graph"], 1),
+            "cpu_baseline": {"value": round(cpu_ms, 3), "unit": "ms/act", "cores": 1, "kind": "port",
+                             "sample": f"oracle float64 numpy forward of one sample, {cpu_steps} acts"}}
+
+
 def pmc_traffic(kernel, workload):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
     (profiles/roofline_traffic.json, written by tools/pmc_traffic.py) — only when
@@ -274,6 +320,9 @@ def main():
     boundary = None
     if rank == 0 and not args.no_boundary:
         boundary = boundary_roofline(device)
+    evalp = None
+    if rank == 0 and not args.no_boundary:
+        evalp = eval_latency(device)
 
     cap = args.steps * (T + 2 * E * M + 8) + 16
     names = [k for k in args.profile_kernels.split(",") if k]
@@ -342,7 +391,7 @@ def main():
         "config": {"workload": workload,
                    "envs_per_gpu": N, "num_steps": T, "ppo_epoch": E, "num_mini_batch": M, "hidden": H,
                    "global_batch": N * T * world, "parallelism": f"dp{world}"},
-        "roofline": roof, "cpu_baseline": cpu, "gae_roofline": gae, "boundary_roofline": boundary,
+        "roofline": roof, "cpu_baseline": cpu, "gae_roofline": gae, "boundary_roofline": boundary, "eval_latency": evalp,
         "kernel_rooflines": kernels,
         "losses": [round(x, 6) for x in losses],
     }

@@ -1,0 +1,65 @@
+"""Evaluation path: T/run_evaluation.py:25-122 steps one
+env with Policy.act(obs, vector_obs, hxs, masks, deterministic) — batch 1, GRU
+state carried across steps, masks zeroed on done.  At batch 1 every act is a
+chain of ~10 tiny kernels, so launch overhead, not arithmetic, sets the step
+latency.  GraphedActor records that chain once into a HIP graph (torch.cuda.graph
+drives hipStreamBeginCapture on the current stream, which is where every
+libppo_hip.so launch goes) and replays it per step: inputs are copied into
+static buffers, one graph launch runs the whole forward.
+
+The graph holds pointers to the engine's flat parameters and packed weights,
+so it stays valid while the policy trains in place: before each replay the
+packed planes are refreshed if the parameters changed since the last pack.
+Only deterministic acting is graphed (the stochastic sampler's RNG counter is
+a launch argument and would freeze inside a graph).
+"""
+import torch
+
+
+class GraphedActor(object):
+    def __init__(self, policy, num_envs=1, obs_dtype=torch.float32, device=None, warmup=2):
+        eng = policy.hip_engine(device)
+        self.policy, self.eng, self.device = policy, eng, eng.device
+        base = policy.base
+        C = base.main[0].weight.shape[1]
+        V = getattr(base, "vector_obs_len", 0)
+        Hh = policy.recurrent_hidden_state_size
+        dev = self.device
+        self.obs = torch.zeros(num_envs, C, 84, 84, dtype=obs_dtype, device=dev)
+        self.vec = torch.zeros(num_envs, V, device=dev)
+        self.hxs = torch.zeros(num_envs, Hh, device=dev)
+        self.masks = torch.ones(num_envs, 1, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):   # warm-up: workspaces, packed weights, device attributes
+            for _ in range(warmup):
+                self._act()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = self._act()
+        self._key = self._pack_key()
+
+    def _act(self):
+        with torch.no_grad():
+            return self.policy.act(self.obs, self.vec, self.hxs, self.masks, deterministic=True)
+
+    def _pack_key(self):
+        return (sum(p._version for p in self.eng.params), self.eng.epoch)
+
+    def act(self, visual_inputs, vector_inputs, rnn_hxs, masks, deterministic=True):
+        """Policy.act (model.py:54-66) for the captured batch -> (value, action, log_prob, rnn_hxs)"""
+        if not deterministic:
+            raise NotImplementedError("GraphedActor replays deterministic acting only; use Policy.act to sample")
+        self.eng.ensure_bound()
+        if self._pack_key() != self._key:   # parameters were updated in place: refresh the packed planes
+            self.eng.pack(force=True)
+            self._key = self._pack_key()
+        for dst, src in ((self.obs, visual_inputs), (self.vec, vector_inputs), (self.hxs, rnn_hxs),
+                         (self.masks, masks)):
+            if dst.numel() and src is not dst:
+                dst.copy_(src.reshape(dst.shape), non_blocking=True)
+        self.graph.replay()
+        # the graph's output buffers, overwritten by the next act (as torch.cuda.graphs
+        # outputs are); the hidden state fed back in is copied before that happens
+        return self.out
