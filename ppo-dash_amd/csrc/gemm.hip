@@ -280,7 +280,10 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
 //                           elements for every (c, ky, kx); the 8 kx rows of
 //                           one (c, y) take 81 dwords (odd: the staging stores
 //                           of 32 lanes hit 32 banks)                   108,864 B
-//   dzT[co][404]       f32   dz1 transposed (row padded: conflict-free reads) 51,712 B
+//   dzT[co][416]       f32   dz1 transposed; the 16-B chunk k of row co sits at
+//                           chunk k ^ SW(co) (a searched 3-bit table): the staging
+//                           ds_write_b128 of 8 lanes (rows 4cq + q) and the fragment
+//                           ds_read_b128 of each 16-lane group both conflict-free 53,248 B
 // and the next image is in flight into registers.  The reduction runs over
 // pixels in natural order: k-step s covers pixels 16s .. 16s+15, lane half h the
 // 8 pixels 16s + 8h .. +7 (two output-row quads 4Q .. 4Q+3).  Wave w: n tiles
@@ -295,7 +298,13 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
                                                                  int B, float* __restrict__ slab,
                                                                  float* __restrict__ slab_bias) {
   static_assert(C == 4, "LDS budget sized for 4 input channels");
-  constexpr int EROW = 162, NE = C * IMG * EROW, DZL = 404, NPX = 400, KS = 25, NT = 512;
+  constexpr int EROW = 162, NE = C * IMG * EROW, DZL = 416, NPX = 400, KS = 25, NT = 512;
+  // float offset of pixel px (multiple of 4) in dzT row co: chunk px/4 XOR SW(co)
+  auto dzo = [](int co, int px) {
+    constexpr unsigned long long SWLO = 0x312423067232146ull, SWHI = 0x1601706435575475ull;
+    const int sw = (int)(((co < 16 ? SWLO >> (4 * co) : SWHI >> (4 * (co - 16)))) & 7);
+    return co * DZL + 4 * ((px >> 2) ^ sw);
+  };
   __shared__ __attribute__((aligned(16))) uint16_t E[NE];
   __shared__ __attribute__((aligned(16))) float dzT[32 * DZL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -344,7 +353,7 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const f32x4 v = f32x4{dzr[i][0][q], dzr[i][1][q], dzr[i][2][q], dzr[i][3][q]};
-          *reinterpret_cast<f32x4*>(dzT + (4 * cq + q) * DZL + 4 * p4) = v;
+          *reinterpret_cast<f32x4*>(dzT + dzo(4 * cq + q, 4 * p4)) = v;
           bsum[q] += (v[0] + v[1]) + (v[2] + v[3]);
         }
       }
@@ -365,8 +374,8 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
   };
   auto rd = [&](int st, f32x4& x0, f32x4& x1, bf16x8 (&bb)[4]) {
     const int px = 16 * st + 8 * h;   // this lane half's 8 pixels: quads px/4, px/4 + 1
-    x0 = *reinterpret_cast<const f32x4*>(dzT + l32 * DZL + px);
-    x1 = *reinterpret_cast<const f32x4*>(dzT + l32 * DZL + px + 4);
+    x0 = *reinterpret_cast<const f32x4*>(dzT + dzo(l32, px));
+    x1 = *reinterpret_cast<const f32x4*>(dzT + dzo(l32, px + 4));
     const int q1 = px >> 2, q2 = q1 + 1;
     const int e1 = (q1 / 5) * (4 * EROW) + 4 * (q1 % 5), e2 = (q2 / 5) * (4 * EROW) + 4 * (q2 % 5);
 #pragma unroll
@@ -572,6 +581,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restri
     for (int p = 0; p < 3; ++p)
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
   const float bv = bias[co];
+  wait_vm0();
   // unit index of this lane's A fragment per row tile, tap (0, 0); a tap adds toff
   int qrow[MT];
 #pragma unroll
@@ -876,6 +886,7 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
 #pragma unroll
     for (int p = 0; p < 3; ++p)
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + ci * 288 + 32 * s + 8 * g);
+  wait_vm0();
   for (int i = tid; i < 2 * 3 * PLU; i += 512) reinterpret_cast<uint4*>(&S[0][0])[i] = uint4{0, 0, 0, 0};
   // unit index of this lane's A fragment per row tile for tap (0, 0); tap
   // (ky, kx) subtracts 25 ky + kx
@@ -992,6 +1003,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
     for (int p = 0; p < 3; ++p)
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 576 + (9 * kh + s) * 32 + 8 * g);
   const float bv = bias[co];
+  wait_vm0();
   for (int i = tid; i < 2 * 3 * PL / 8; i += 512) reinterpret_cast<uint4*>(&S[0][0])[i] = uint4{0, 0, 0, 0};
   f32x4 stg[UPER][2];
   auto fetch = [&](int b) {
@@ -999,7 +1011,9 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < UPER; ++j) {
       const int u = tid + 512 * j;
-      if (u < UNITS) { stg[j][0] = src[2 * u]; stg[j][1] = src[2 * u + 1]; }
+      const int uu = u < UNITS ? u : 0;   // unconditional loads: no exec branch around them
+      stg[j][0] = src[2 * uu];
+      stg[j][1] = src[2 * uu + 1];
     }
   };
   auto put = [&](int buf) {
@@ -1263,6 +1277,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
 #pragma unroll
     for (int p = 0; p < 3; ++p)
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + n * 256 + 64 * g + 8 * s);
+  wait_vm0();
   // zero the pad pixels of both stages (staging only ever writes the 81 real ones)
   for (int i = tid; i < 2 * 3 * GP * 8; i += 512) {
     const int c = i % (GP * 8), p = c >> 3, py = p / GW, px = p - GW * py;
@@ -1284,7 +1299,9 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int c = tid + 512 * j;
-      if (c < CH) { stg[j][0] = src[2 * c]; stg[j][1] = src[2 * c + 1]; }
+      const int cc = c < CH ? c : 0;   // unconditional loads: no exec branch around them
+      stg[j][0] = src[2 * cc];
+      stg[j][1] = src[2 * cc + 1];
     }
     const f32x4* ms = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
 #pragma unroll

@@ -57,6 +57,12 @@ __device__ __forceinline__ void split8(const f32x4& x0, const f32x4& x1, Frag3& 
   }
 }
 
+// s_waitcnt vmcnt(0) as a real S_WAITCNT (the waitcnt pass sees it, unlike inline
+// asm).  Issued once after a persistent kernel's prologue loads (weights, bias):
+// otherwise the pass carries those loads as pending into the image loop and its
+// conservative vmcnt(N) waits there also drain the next image's prefetch.
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 __device__ __forceinline__ f32x4 mma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
