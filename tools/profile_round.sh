@@ -10,7 +10,7 @@ BENCH_ARGS="${BENCH_ARGS:-}"
 step() { echo "== $1"; shift; "$@"; rc=$?; echo "rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 step bench timeout -k 10 900 python bench.py $BENCH_ARGS > gpurun_out/bench_full.log 2>&1
 grep '^{' gpurun_out/bench_full.log
-step stats timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-gae-roofline $BENCH_ARGS
-step fetch timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcb -o fetch -- python3 bench.py --no-cpu-baseline --no-gae-roofline $BENCH_ARGS
-step write timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcb -o write -- python3 bench.py --no-cpu-baseline --no-gae-roofline $BENCH_ARGS
+step stats timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-gae-roofline --no-boundary $BENCH_ARGS
+step fetch timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcb -o fetch -- python3 bench.py --no-cpu-baseline --no-gae-roofline --no-boundary $BENCH_ARGS
+step write timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcb -o write -- python3 bench.py --no-cpu-baseline --no-gae-roofline --no-boundary $BENCH_ARGS
 echo done
