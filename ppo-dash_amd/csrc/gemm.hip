@@ -1546,11 +1546,11 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
 // ---------------------------------------------------------------------------
 enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_X9,
-       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_N };
+       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_FC_DGRAD, TK_FC_WGRAD, TK_N };
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
-                                         "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad"};
+                                         "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad", "fc_dgrad", "fc_wgrad"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
-static int g_tune[TK_N] = {0, 8, 8, 8, 1, 0, 8, 1, 8, 8};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 8, 8, 8, 1, 0, 8, 1, 8, 8, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   if (strcmp(key, "products") == 0) {
@@ -1615,10 +1615,20 @@ using X128 = CfgX<128, 128, 2, 2, true, true>;        // N >= 128: waves of 64x6
 using XW32 = CfgX<32, 128, 1, 4, false, false, true>;   // wgrad, 32 output channels
 using XW64 = CfgX<64, 128, 2, 2, false, false, true>;   // wgrad, 64 output channels
 using XW128 = CfgX<128, 128, 2, 2, false, false, true>; // wgrad, >= 128 output channels
+using XW128w8a = CfgX<128, 128, 4, 2, false, false, true>;  // 8 waves of 32x64
+using XW128w8b = CfgX<128, 128, 2, 4, false, false, true>;  // 8 waves of 64x32
+using XW256x128 = CfgX<256, 128, 4, 2, false, false, true>; // 8 waves of 64x64
 using XP32 = CfgX<128, 32, 4, 1, true, true, false, false, false, true>;    // B from planes, waves 32x32
 using XP64 = CfgX<128, 64, 4, 1, true, true, false, false, false, true>;    // waves 32x64
 using XP128 = CfgX<128, 128, 4, 1, true, true, false, false, false, true>;  // waves 32x128
 using XP64s = CfgX<64, 64, 2, 1, true, true, false, false, false, true>;    // 2 waves of 32x64
+using XP256x128w8 = CfgX<256, 128, 8, 1, true, true, false, false, false, true>;  // 8 waves of 32x128
+using XP128w8 = CfgX<128, 128, 8, 1, true, true, false, false, false, true>;      // 8 waves of 16x128
+using XP256x64w8 = CfgX<256, 64, 8, 1, true, true, false, false, false, true>;    // 8 waves of 32x64
+using XP128x256 = CfgX<128, 256, 4, 1, true, true, false, false, false, true>;    // 4 waves of 32x256
+using XP64x128w4 = CfgX<64, 128, 4, 1, true, true, false, false, false, true>;    // 4 waves of 16x128 (2 blocks/CU)
+using XP128x64w8 = CfgX<128, 64, 8, 1, true, true, false, false, false, true>;    // 8 waves of 16x64 (2 blocks/CU)
+using XP256x128w16 = CfgX<256, 128, 16, 1, true, true, false, false, false, true>; // 16 waves of 16x128
 // x9 = 1: the split-bf16 core where it measured faster (forward GEMMs, fc dgrad); the gather-heavy
 // conv dgrads and the wgrads stay on fp32 MFMA (their split path is VALU-bound); x9 = 2: everywhere
 // compute units of the current device (persistent-kernel grid size)
@@ -1776,7 +1786,7 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
     int v = g_tune[TK_FC_FWD];
     if (v == 0) {
       const long long t128 = ((M + 127LL) / 128) * ((H + 127) / 128);
-      v = t128 >= 2LL * device_cus() ? 1 : 2;   // measured: 128x64 best at M = 4096
+      v = t128 >= 2LL * device_cus() ? 1 : 5;   // measured at M = 4096: 8 waves of 16x64 0.060 ms, 128x64 0.070
     }
 #define PPO_FC(CFG)                                                                                  \
   {                                                                                                  \
@@ -1787,6 +1797,8 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
   }
     if (v == 2) PPO_FC(XP64)
     if (v == 3) PPO_FC(XP64s)
+    if (v == 4) PPO_FC(XP128w8)
+    if (v == 5) PPO_FC(XP128x64w8)
     PPO_FC(XP128)
 #undef PPO_FC
   }
@@ -1885,10 +1897,24 @@ PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 4", K);
   if (use_x9()) {   // wt = the packed W4T segment [1568][H] (planes follow)
     PPO_REQUIRE(K % 8 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 8", K);
-    DenseDgradMask<XP128> p;
-    p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;
-    set_planes(p, wt, (long long)N * K, N, K);
-    return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);
+#define PPO_FCD(CFG)                                                                \
+  {                                                                                 \
+    DenseDgradMask<CFG> p;                                                          \
+    p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;        \
+    set_planes(p, wt, (long long)N * K, N, K);                                      \
+    return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K); \
+  }
+    switch (g_tune[TK_FC_DGRAD]) {   // tile variants (kbench A/B)
+      case 1: PPO_FCD(XP256x128w8)
+      case 2: PPO_FCD(XP128)
+      case 3: PPO_FCD(XP256x64w8)
+      case 4: PPO_FCD(XP128x256)
+      case 5: PPO_FCD(XP64x128w4)
+      case 6: PPO_FCD(XP128x64w8)
+      case 7: PPO_FCD(XP256x128w16)
+      default: PPO_FCD(XP128w8)   // measured: 0.75 vs 0.87 ms (XP128) at the c3 minibatch
+    }
+#undef PPO_FCD
   }
   DenseDgradMask<CfgN128> p;
   p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;
@@ -2067,10 +2093,20 @@ PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int 
       p.x = x; p.K = K;
       return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K);
     }
-    DenseWgrad<XW128> p;
-    set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);
-    p.x = x; p.K = K;
-    return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K);
+#define PPO_FCW(CFG)                                                                \
+  {                                                                                 \
+    DenseWgrad<CFG> p;                                                              \
+    set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);                                  \
+    p.x = x; p.K = K;                                                               \
+    return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K); \
+  }
+    switch (g_tune[TK_FC_WGRAD]) {   // tile variants (kbench A/B)
+      case 1: PPO_FCW(XW128w8a)
+      case 2: PPO_FCW(XW128w8b)
+      case 3: PPO_FCW(XW128)
+      default: PPO_FCW(XW256x128)   // measured: 0.79 vs 0.83 ms (XW128) at the c3 minibatch
+    }
+#undef PPO_FCW
   }
   DenseWgrad<CfgWfc> p;
   set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);
