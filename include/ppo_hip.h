@@ -173,6 +173,9 @@ int ppo_gru_cell_bwd(const float* dout, const float* carry, const float* r, cons
 int ppo_gru_step_bwd(const float* dgh, const float* whhT, const float* dhz, const float* masks,
                      const int64_t* mask_idx, float* carry, int M, int H, void* stream);
 /* W_ih -> zero-padded [3H][Ip], W_ih[:, :H]ᵀ [H][3H], W_hhᵀ [H][3H] */
+/* step-kernel variant (A/B knob): 0 register-tiled 16x16x4 f32 MFMA kernels
+ * (H in {64,128,256,512}), 1 the tile-GEMM steps */
+int ppo_gru_variant_set(int v);
 int ppo_gru_pack(const float* wih, const float* whh, int H, int I, int Ip, float* wih_pad, float* wihT, float* whhT,
                  void* stream);
 /* model.py:195 torch.cat((x, vector_inputs)): dst[r][col0 + c] = src[idx(r)][c], zero pad */

@@ -185,6 +185,182 @@ __global__ __launch_bounds__(256) void rec_indices_kernel(const int64_t* __restr
 using CfgGru = Cfg<32, 96, 1, 1, true, true>;     // one wave: 32 rows x (r,z,n) x 32 units
 using CfgGruB = Cfg<64, 64, 2, 2, true, true>;
 
+// ---------------------------------------------------------------------------
+// Register-tiled step kernels.  A minibatch step has only n_env = 512 rows, so
+// the tile GEMM above fills 128 waves (half the chip, one wave per CU) and each
+// step is latency-bound (~40 us).  Here a block of 4 waves owns 32 rows x 16
+// hidden units and splits K four ways; every operand goes global -> registers
+// once per launch (no LDS staging, no k-loop barrier), one
+// v_mfma_f32_16x16x4_f32 (exact fp32) per 16x16 tile per k-step, and the four
+// K-quarter partials meet in LDS for the fused epilogue.  512 rows x 256 units
+// -> 256 blocks.  K order: lane group g of wave q owns the KW consecutive k
+// starting at q*4*KW + g*KW, the same k for the A and B operands.
+// MFMA maps (16x16x4 f32): A[l&15][k=l>>4], B[k=l>>4][l&15], D col=l&15, row=4(l>>4)+r.
+
+// forward: gh = h_in · W_hhᵀ for the (r, z, n) rows of the block's 16 units, then
+// the GRU cell (as GruStep::store_tile)
+template <int H>
+__global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict__ hprev,
+                                                         const float* __restrict__ masks,
+                                                         const int64_t* __restrict__ mask_idx,
+                                                         const float* __restrict__ whh, const float* __restrict__ bhh,
+                                                         const float* __restrict__ gi, int M, float* __restrict__ hout,
+                                                         float* __restrict__ sr, float* __restrict__ sz,
+                                                         float* __restrict__ sn, float* __restrict__ sghn,
+                                                         float* __restrict__ shin) {
+  constexpr int KW = H / 16;   // k per lane group and wave (4 groups x 4 waves x KW = H)
+  __shared__ f32x4 P[4][6][64];
+  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
+  const int k0 = q * 4 * KW + g * KW;
+  float a[2][KW], b[3][KW];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int m = m0 + 16 * rt + c;
+    const bool ok = m < M;
+    const float mk = ok && masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
+    const float* src = hprev + (size_t)(ok ? m : 0) * H + k0;
+#pragma unroll
+    for (int s = 0; s < KW; s += 4) {
+      const f32x4 v = ok ? *reinterpret_cast<const f32x4*>(src + s) * mk : zero4();
+      a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
+    }
+  }
+#pragma unroll
+  for (int gt = 0; gt < 3; ++gt) {
+    const float* src = whh + ((size_t)gt * H + j0 + c) * H + k0;
+#pragma unroll
+    for (int s = 0; s < KW; s += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + s);
+      b[gt][s] = v[0]; b[gt][s + 1] = v[1]; b[gt][s + 2] = v[2]; b[gt][s + 3] = v[3];
+    }
+  }
+  f32x4 acc[2][3];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int gt = 0; gt < 3; ++gt) acc[rt][gt] = zero4();
+#pragma unroll
+  for (int s = 0; s < KW; ++s)
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int gt = 0; gt < 3; ++gt)
+        acc[rt][gt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], b[gt][s], acc[rt][gt], 0, 0, 0);
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int gt = 0; gt < 3; ++gt) P[q][rt * 3 + gt][lane] = acc[rt][gt];
+  __syncthreads();
+  // epilogue: thread -> (row, unit) pairs; the K quarters summed in a fixed order
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int p = tid + 256 * e, ml = p >> 4, jl = p & 15, m = m0 + ml, j = j0 + jl;
+    if (m >= M) continue;
+    const int rt = ml >> 4, ir = ml & 15, ln = jl + 16 * (ir >> 2), rg = ir & 3;
+    float v[3];
+#pragma unroll
+    for (int gt = 0; gt < 3; ++gt)
+      v[gt] = ((P[0][rt * 3 + gt][ln][rg] + P[1][rt * 3 + gt][ln][rg]) + P[2][rt * 3 + gt][ln][rg]) +
+              P[3][rt * 3 + gt][ln][rg];
+    const float* gr = gi + (size_t)m * 3 * H;
+    const float ghr = v[0] + bhh[j], ghz = v[1] + bhh[H + j], ghn = v[2] + bhh[2 * H + j];
+    const float r = sigm(gr[j] + ghr);
+    const float z = sigm(gr[H + j] + ghz);
+    const float n = tanhf(gr[2 * H + j] + r * ghn);
+    const float mk = masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
+    const float hin = hprev[(size_t)m * H + j] * mk;
+    const size_t o = (size_t)m * H + j;
+    hout[o] = (1.0f - z) * n + z * hin;
+    if (sr) {
+      sr[o] = r;
+      sz[o] = z;
+      sn[o] = n;
+      sghn[o] = ghn;
+      shin[o] = hin;
+    }
+  }
+}
+
+// backward: carry = (dgh · W_hh + dh'·z) · m(t) for the block's 32 rows x 16 units
+// (B = W_hhᵀ packed [H][3H]: unit j's column of W_hh is row j, contiguous)
+template <int H>
+__global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __restrict__ dgh,
+                                                             const float* __restrict__ whhT,
+                                                             const float* __restrict__ dhz,
+                                                             const float* __restrict__ masks,
+                                                             const int64_t* __restrict__ mask_idx,
+                                                             float* __restrict__ carry, int M) {
+  constexpr int KW = 3 * H / 16;
+  constexpr int NH = KW % 8 == 0 ? 2 : 1, KH = KW / NH;   // K halves keep the operand registers small
+  __shared__ f32x4 P[4][2][64];
+  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
+  const int k0 = q * 4 * KW + g * KW;
+  f32x4 acc[2] = {zero4(), zero4()};
+#pragma unroll
+  for (int half = 0; half < NH; ++half) {
+    float a[2][KH], b[KH];
+    const int kb = k0 + half * KH;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int m = m0 + 16 * rt + c;
+      const bool ok = m < M;
+      const float* src = dgh + (size_t)(ok ? m : 0) * 3 * H + kb;
+#pragma unroll
+      for (int s = 0; s < KH; s += 4) {
+        const f32x4 v = ok ? *reinterpret_cast<const f32x4*>(src + s) : zero4();
+        a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
+      }
+    }
+    const float* bs = whhT + (size_t)(j0 + c) * 3 * H + kb;
+#pragma unroll
+    for (int s = 0; s < KH; s += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(bs + s);
+      b[s] = v[0]; b[s + 1] = v[1]; b[s + 2] = v[2]; b[s + 3] = v[3];
+    }
+#pragma unroll
+    for (int s = 0; s < KH; ++s)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], b[s], acc[rt], 0, 0, 0);
+  }
+  P[q][0][lane] = acc[0];
+  P[q][1][lane] = acc[1];
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int p = tid + 256 * e, ml = p >> 4, jl = p & 15, m = m0 + ml, j = j0 + jl;
+    if (m >= M) continue;
+    const int rt = ml >> 4, ir = ml & 15, ln = jl + 16 * (ir >> 2), rg = ir & 3;
+    const float v = ((P[0][rt][ln][rg] + P[1][rt][ln][rg]) + P[2][rt][ln][rg]) + P[3][rt][ln][rg];
+    const float mk = masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
+    const size_t o = (size_t)m * H + j;
+    carry[o] = (v + dhz[o]) * mk;
+  }
+}
+
+// 0: register-tiled step kernels where H allows; 1: the tile-GEMM steps (A/B)
+static int g_gru_variant = 0;
+
+template <int H>
+int launch_step16(const float* hprev, const float* masks, const int64_t* mask_idx, const float* whh,
+                  const float* bhh, const float* gi, int M, float* hout, float* sr, float* sz, float* sn,
+                  float* sghn, float* shin, hipStream_t st) {
+  dim3 grid((unsigned)ceil_div(M, 32), H / 16);
+  gru_step16_kernel<H><<<grid, 256, 0, st>>>(hprev, masks, mask_idx, whh, bhh, gi, M, hout, sr, sz, sn, sghn, shin);
+  PPO_LAUNCH_CHECK("gru_step16_kernel");
+  return 0;
+}
+
+template <int H>
+int launch_step_bwd16(const float* dgh, const float* whhT, const float* dhz, const float* masks,
+                      const int64_t* mask_idx, float* carry, int M, hipStream_t st) {
+  dim3 grid((unsigned)ceil_div(M, 32), H / 16);
+  gru_step_bwd16_kernel<H><<<grid, 256, 0, st>>>(dgh, whhT, dhz, masks, mask_idx, carry, M);
+  PPO_LAUNCH_CHECK("gru_step_bwd16_kernel");
+  return 0;
+}
+
 static unsigned grid_for(long long total) {
   long long b = (total + 255) / 256;
   return (unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096);
@@ -197,6 +373,20 @@ PPO_API int ppo_gru_step_fwd(const float* hprev, const float* masks, const int64
                              const float* bhh, const float* gi, int M, int H, float* hout, float* save_r, float* save_z,
                              float* save_n, float* save_ghn, float* save_hin, void* stream) {
   PPO_REQUIRE(M >= 0 && H > 0 && H % 32 == 0, "ppo_gru_step_fwd: M=%d H=%d (H multiple of 32)", M, H);
+  if (M == 0) return 0;
+  if (g_gru_variant == 0) {
+    hipStream_t st = as_stream(stream);
+    switch (H) {
+      case 64: return launch_step16<64>(hprev, masks, mask_idx, whh, bhh, gi, M, hout, save_r, save_z, save_n,
+                                        save_ghn, save_hin, st);
+      case 128: return launch_step16<128>(hprev, masks, mask_idx, whh, bhh, gi, M, hout, save_r, save_z, save_n,
+                                          save_ghn, save_hin, st);
+      case 256: return launch_step16<256>(hprev, masks, mask_idx, whh, bhh, gi, M, hout, save_r, save_z, save_n,
+                                          save_ghn, save_hin, st);
+      case 512: return launch_step16<512>(hprev, masks, mask_idx, whh, bhh, gi, M, hout, save_r, save_z, save_n,
+                                          save_ghn, save_hin, st);
+    }
+  }
   GruStep<CfgGru> p;
   p.hprev = hprev; p.masks = masks; p.mask_idx = mask_idx; p.whh = whh; p.bhh = bhh; p.gi = gi; p.hout = hout;
   p.sr = save_r; p.sz = save_z; p.sn = save_n; p.sghn = save_ghn; p.shin = save_hin; p.M = M; p.H = H;
@@ -217,9 +407,26 @@ PPO_API int ppo_gru_cell_bwd(const float* dout, const float* carry, const float*
 PPO_API int ppo_gru_step_bwd(const float* dgh, const float* whhT, const float* dhz, const float* masks,
                              const int64_t* mask_idx, float* carry, int M, int H, void* stream) {
   PPO_REQUIRE(M >= 0 && H > 0 && H % 4 == 0, "ppo_gru_step_bwd: M=%d H=%d", M, H);
+  if (M == 0) return 0;
+  if (g_gru_variant == 0) {
+    hipStream_t st = as_stream(stream);
+    switch (H) {
+      case 64: return launch_step_bwd16<64>(dgh, whhT, dhz, masks, mask_idx, carry, M, st);
+      case 128: return launch_step_bwd16<128>(dgh, whhT, dhz, masks, mask_idx, carry, M, st);
+      case 256: return launch_step_bwd16<256>(dgh, whhT, dhz, masks, mask_idx, carry, M, st);
+      case 512: return launch_step_bwd16<512>(dgh, whhT, dhz, masks, mask_idx, carry, M, st);
+    }
+  }
   GruBwdStep<CfgGruB> p;
   p.dgh = dgh; p.whhT = whhT; p.dhz = dhz; p.masks = masks; p.mask_idx = mask_idx; p.carry = carry; p.M = M; p.H = H;
   return launch(p, M, H, 1, as_stream(stream), "gru_step_bwd", 2.0 * M * 3 * H * H);
+}
+
+// A/B switch for the step kernels (0 register-tiled, 1 tile GEMM)
+PPO_API int ppo_gru_variant_set(int v) {
+  PPO_REQUIRE(v == 0 || v == 1, "ppo_gru_variant_set: %d", v);
+  g_gru_variant = v;
+  return 0;
 }
 
 PPO_API int ppo_gru_pack(const float* wih, const float* whh, int H, int I, int Ip, float* wih_pad, float* wihT,

@@ -1047,3 +1047,45 @@ def test_split_products_fp32_accuracy(gpu):
         ecpu = rel(res[6][name][2], res[6][name][1])
         print(f"{name}: x6 {e6:.3e}  x9 {e9:.3e}  torch-cpu-fp32 {ecpu:.3e}")
         assert e6 <= 2 * e9 + 1e-9 and e6 <= 4 * ecpu + 1e-9 and e6 < 1e-6, (name, e6, e9, ecpu)
+
+
+@pytest.mark.parametrize("M,H", [(37, 64), (512, 256), (100, 128)])
+def test_gru_step_kernels_vs_float64(gpu, M, H):
+    """The register-tiled GRU step kernels (default) and the tile-GEMM steps
+    (ppo_gru_variant_set(1)) vs a float64 restatement of the cell
+    (model.py:112-115 with h_in = h·mask): forward outputs, every saved gate, and
+    the backward carry (dh_in + dh'·z)·m, within 2e-5 of max|ref|."""
+    Hh = _hip()
+    g = torch.Generator().manual_seed(M + H)
+    hprev = torch.randn(M, H, generator=g)
+    masks = (torch.rand(M, generator=g) > 0.2).float()
+    whh = torch.randn(3 * H, H, generator=g) / H ** 0.5
+    bhh = torch.randn(3 * H, generator=g) * 0.1
+    gi = torch.randn(M, 3 * H, generator=g)
+    dgh = torch.randn(M, 3 * H, generator=g)
+    dhz = torch.randn(M, H, generator=g)
+    d = {k: v.cuda() for k, v in dict(hprev=hprev, masks=masks, whh=whh, bhh=bhh, gi=gi, dgh=dgh, dhz=dhz).items()}
+    whhT = d["whh"].t().contiguous()
+    hin = hprev.double() * masks.double()[:, None]
+    gh = hin @ whh.double().t() + bhh.double()
+    gd = gi.double()
+    r = torch.sigmoid(gd[:, :H] + gh[:, :H])
+    z = torch.sigmoid(gd[:, H:2 * H] + gh[:, H:2 * H])
+    n = torch.tanh(gd[:, 2 * H:] + r * gh[:, 2 * H:])
+    ref = {"hout": (1 - z) * n + z * hin, "r": r, "z": z, "n": n, "ghn": gh[:, 2 * H:], "hin": hin,
+           "carry": (dgh.double() @ whh.double() + dhz.double()) * masks.double()[:, None]}
+    for variant in (0, 1):
+        out = {k: torch.full((M, H), float("nan"), device=gpu) for k in ref}
+        Hh.call("ppo_gru_variant_set", variant)
+        try:
+            Hh.call("ppo_gru_step_fwd", d["hprev"].data_ptr(), d["masks"].data_ptr(), None, d["whh"].data_ptr(),
+                    d["bhh"].data_ptr(), d["gi"].data_ptr(), M, H, out["hout"].data_ptr(), out["r"].data_ptr(),
+                    out["z"].data_ptr(), out["n"].data_ptr(), out["ghn"].data_ptr(), out["hin"].data_ptr(), _s())
+            Hh.call("ppo_gru_step_bwd", d["dgh"].data_ptr(), whhT.data_ptr(), d["dhz"].data_ptr(),
+                    d["masks"].data_ptr(), None, out["carry"].data_ptr(), M, H, _s())
+            torch.cuda.synchronize()
+        finally:
+            Hh.call("ppo_gru_variant_set", 0)
+        for k, v in ref.items():
+            err = (out[k].cpu().double() - v).abs().max().item()
+            assert err <= 2e-5 * max(v.abs().max().item(), 1.0), (variant, k, err)
