@@ -90,6 +90,8 @@ def parse():
     p.add_argument("--no-gae-roofline", action="store_true")
     p.add_argument("--no-boundary", action="store_true", help="skip the observation-boundary measurement")
     p.add_argument("--gae-lanes", type=int, default=1 << 20)
+    p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                   help="collectives backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     return p.parse_args()
 
 
@@ -267,10 +269,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; modulo the visible count only so a gloo rehearsal of the
+    # N > 1 path can run several ranks on a one-GPU box (--dist-backend gloo)
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)   # RCCL over xGMI
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from a2c_ppo_acktr import _hip
     from a2c_ppo_acktr.algo import PPO
