@@ -681,6 +681,145 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restri
   }
 }
 
+// conv2 forward, LDS-DMA staged variant of conv2_fwd_x9_kernel (same layout,
+// same math, bit-identical results).  The register-staged kernel loses ~45 % of
+// its time in the per-image staging phase: the next image's global loads sit
+// at the VGPR cap (254) and the allocator's register shuffles wait on them
+// right after issue, so every image pays an HBM round trip with the MFMAs
+// idle.  Here the next image goes global -> LDS by global_load_lds_dwordx4
+// (no VGPRs; in flight during the whole compute phase) into a raw fp32 buffer
+// (51,200 B, lane-linear in source order), and the split reads it from LDS.
+// LDS (one array): S planes 104,448 B | RAW 51,200 B; the K-half partials
+// alias S once the image is consumed.  Per image: compute -> vmcnt(0) +
+// barrier -> partials -> barrier -> epilogue -> barrier -> split RAW into S ->
+// barrier -> issue the DMA of the image after next.
+// Measured (kbench, c3 minibatch): 2.00 ms vs 1.98 ms for the register-staged
+// kernel — neutral: what remains of the staging phase is the split VALU and
+// the barriers, which no staging path can overlap with the MFMAs while one
+// split image fills two thirds of the LDS.  Kept as ppo_tune_set("conv2_fwd", 10).
+template <int NP>
+__global__ __launch_bounds__(512) void conv2_fwd_dma_kernel(const float* __restrict__ a1, int B,
+                                                           const uint16_t* __restrict__ wpl,
+                                                           const float* __restrict__ bias,
+                                                           float* __restrict__ out) {
+  constexpr int CS = 544, PLU = 4 * CS, MT = 6, KS = 8, UNITS = 400 * 4, UPER = (UNITS + 511) / 512;
+  constexpr int WN = 64 * 512, SBYTES = 3 * PLU * 8 * 2, RAWU = 400 * 8;   // RAW: 3,200 16-B units
+  __shared__ __attribute__((aligned(16))) uint8_t L[SBYTES + RAWU * 16];
+  uint16_t* S = reinterpret_cast<uint16_t*>(L);
+  f32x4* RAW = reinterpret_cast<f32x4*>(L + SBYTES);
+  f32x4(*R)[MT][64] = reinterpret_cast<f32x4(*)[MT][64]>(L);   // [4][MT][64], aliases S
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int nt = wave & 3, kh = wave >> 2, co = 16 * nt + i16;
+  bf16x8 bw[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
+  const float bv = bias[co];
+  wait_vm0();
+  int qrow[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int m = 16 * t + i16, oy = m / 9, ox = m - 9 * oy;
+    qrow[t] = g * CS + oy * 25 + ox;
+  }
+  int upx[UPER], uq[UPER];
+#pragma unroll
+  for (int j = 0; j < UPER; ++j) {
+    const int u = tid + 512 * j, rho = 8 * (u >> 5) + (u & 7), c = (u >> 3) & 3;
+    const int y = rho / 20, r = rho - 20 * y, x = r < 10 ? 2 * r : 2 * (r - 10) + 1;
+    upx[j] = (y * 20 + x) * 4 + c;
+    uq[j] = c * CS + (y & 1) * 250 + (y >> 1) * 25 + r;
+  }
+  // DMA of image b into RAW: wave w's instruction i moves units (8 i + w) * 64 + lane
+  auto dma = [&](int b) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
+#pragma unroll
+    for (int i = 0; i < (RAWU + 511) / 512; ++i) {
+      const int base = (8 * i + wave) * 64;   // wave-uniform
+      if (base < RAWU)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + base + lane),
+                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                             reinterpret_cast<uintptr_t>(RAW + base)),
+                                         16, 0, 0);
+    }
+  };
+  auto put = [&]() {
+#pragma unroll
+    for (int j = 0; j < UPER; ++j) {
+      const int u = tid + 512 * j;
+      if (u < UNITS) {
+        const int q = uq[j];
+        Frag3 f;
+        split8(RAW[2 * upx[j]], RAW[2 * upx[j] + 1], f, false);
+        *reinterpret_cast<bf16x8*>(&S[8 * q]) = f.h;
+        *reinterpret_cast<bf16x8*>(&S[8 * (PLU + q)]) = f.m;
+        *reinterpret_cast<bf16x8*>(&S[8 * (2 * PLU + q)]) = f.l;
+      }
+    }
+  };
+  const int G = gridDim.x;
+  int b = blockIdx.x;
+  if (b < B) {
+    dma(b);
+    wait_vm0();
+    __syncthreads();
+    put();
+    __syncthreads();
+    if (b + G < B) dma(b + G);
+  }
+  for (; b < B; b += G) {
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = zero4();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int tap = 8 * kh + s, ky = tap >> 2, kx = tap & 3;
+      const int toff = (ky & 1) * 250 + (ky >> 1) * 25 + (kx & 1) * 10 + (kx >> 1);
+      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+#pragma unroll
+      for (int t0 = 0; t0 < MT; t0 += 3) {
+        Frag3 a[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const uint16_t* q = S + 8 * (qrow[t0 + u] + toff);
+          a[u].h = *reinterpret_cast<const bf16x8*>(q);
+          a[u].m = *reinterpret_cast<const bf16x8*>(q + 8 * PLU);
+          a[u].l = *reinterpret_cast<const bf16x8*>(q + 16 * PLU);
+        }
+#define PPO_PART(X, Y) \
+  _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(a[u].X, w.Y, acc[t0 + u]);
+        PPO_PRODUCTS(NP, PPO_PART)
+#undef PPO_PART
+      }
+    }
+    wait_vm0();        // this wave's part of the next image has landed in RAW
+    __syncthreads();   // A: the image is consumed, RAW complete
+    if (kh == 1) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t) R[nt][t][lane] = acc[t];
+    }
+    __syncthreads();   // B: partials visible
+    if (kh == 0) {
+      float* o = out + (size_t)b * (81 * 64) + co;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const f32x4 v = acc[t] + R[nt][t][lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * t + 4 * g + r;
+          if (m < 81) o[m * 64] = fmaxf(v[r] + bv, 0.f);
+        }
+      }
+    }
+    __syncthreads();   // C: partials consumed
+    if (b + G < B) put();
+    __syncthreads();   // D: next image in S, RAW free
+    if (b + 2 * G < B) dma(b + 2 * G);
+  }
+}
+
 // conv2 weight gradient, image-resident on the bf16 matrix cores (exact split,
 // DESIGN.md §3): dW2[co][k] = Σ_pixels dz2[m][co] · a1[2oy+ky][2ox+kx][ci],
 // k = (ky, kx, ci); per image a 64 x 512 x 81 product (reduction padded to 96 =
@@ -1725,6 +1864,17 @@ PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, lo
 }
 
 PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream) {
+  if (g_tune[TK_CONV2_FWD] == 10) {   // LDS-DMA staged
+    if (B <= 0) return 0;
+    const int n_cu = device_cus();
+    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+    int slot;
+    const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
+    PPO_LAUNCH_NP(conv2_fwd_dma_kernel, nb, 512, as_stream(stream), a1, B, planes_of(w2p, 64 * 512), b2, out);
+    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
+    PPO_LAUNCH_CHECK("conv2_fwd_dma_kernel");
+    return 0;
+  }
   if (g_tune[TK_CONV2_FWD] == 8) {
     if (B <= 0) return 0;
     const int n_cu = device_cus();

@@ -807,7 +807,7 @@ def test_conv2_dgrad_variants_vs_torch(gpu, variant):
     assert err <= 1e-5 * ref.abs().max().item(), err
 
 
-@pytest.mark.parametrize("variant", [0, 8])
+@pytest.mark.parametrize("variant", [0, 8, 10])
 def test_conv2_fwd_variants_vs_torch(gpu, variant):
     """conv2 forward (4x4 stride 2, 20x20x32 -> 9x9x64, bias + ReLU): the split-bf16
     tile GEMM (0) and the image-resident kernel (8) vs torch float64:
