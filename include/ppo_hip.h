@@ -176,6 +176,24 @@ int ppo_gru_step_bwd(const float* dgh, const float* whhT, const float* dhz, cons
 /* step-kernel variant (A/B knob): 0 register-tiled 16x16x4 f32 MFMA kernels
  * (H in {64,128,256,512}), 1 the tile-GEMM steps */
 int ppo_gru_variant_set(int v);
+int ppo_gru_variant_get(void);
+/* the BPTT loop body in one launch: step t's carry = (dgh(t)·W_hh + dhz)·m(t)
+ * (ppo_gru_step_bwd) fused with step t-1's gate backward from that carry
+ * (ppo_gru_cell_bwd with dout(t-1) and the saves of t-1; writes dgi/dgh of t-1
+ * and overwrites dhz with t-1's).  H in {64, 128, 256, 512}, variant 0 only. */
+/* whole-sequence forward / backward through time (one call per minibatch; the
+ * per-step kernels above, launched from C): model.py:116-165 */
+int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* idx, const float* whh, const float* bhh,
+                    const float* gi, int T, int n, int H, float* hout, float* save_r, float* save_z, float* save_n,
+                    float* save_ghn, float* save_hin, void* stream);
+int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float* save_z, const float* save_n,
+                    const float* save_ghn, const float* save_hin, const float* masks, const int64_t* idx,
+                    const float* whhT, int T, int n, int H, float* dgi, float* dgh, float* dhz, float* carry,
+                    void* stream);
+int ppo_gru_step_bwd_cell(const float* dgh, const float* whhT, float* dhz, const float* masks,
+                          const int64_t* mask_idx, float* carry, int M, int H, const float* dout_prev,
+                          const float* r, const float* z, const float* n, const float* ghn, const float* hin,
+                          float* dgi_prev, float* dgh_prev, void* stream);
 int ppo_gru_pack(const float* wih, const float* whh, int H, int I, int Ip, float* wih_pad, float* wihT, float* whhT,
                  void* stream);
 /* model.py:195 torch.cat((x, vector_inputs)): dst[r][col0 + c] = src[idx(r)][c], zero pad */

@@ -358,11 +358,8 @@ class RecurrentEngine(CNNEngine):
         m = masks.to(self.device, torch.float32).reshape(R).contiguous()
         hout = torch.empty(R, self.H, device=self.device)
         H, s = self.H, stream()
-        for t in range(T):
-            hprev = hxs.data_ptr() if t == 0 else hout.data_ptr() + 4 * (t - 1) * N * H
-            call("ppo_gru_step_fwd", hprev, m.data_ptr() + 4 * t * N, None, self.pv(self.GHH), self.pv(self.GBH),
-                 gi.data_ptr() + 4 * t * N * 3 * H, N, H, hout.data_ptr() + 4 * t * N * H, None, None, None, None,
-                 None, s)
+        call("ppo_gru_seq_fwd", hxs.data_ptr(), m.data_ptr(), None, self.pv(self.GHH), self.pv(self.GBH),
+             gi.data_ptr(), T, N, H, hout.data_ptr(), None, None, None, None, None, s)
         value, _, logp, ent = self._heads(hout, R, given=action.to(self.device, torch.int64), want_entropy=True)
         return value, logp, ent, hout[(T - 1) * N:]
 
@@ -385,13 +382,9 @@ class RecurrentEngine(CNNEngine):
         hout = ws.get("hout", R * H, device=dev)
         sv = {k: ws.get("s_" + k, R * H, device=dev) for k in ("r", "z", "n", "ghn", "hin")}
         masks = storage.masks
-        for t in range(T):
-            o = 4 * t * n * H
-            hprev = h0.data_ptr() if t == 0 else hout.data_ptr() + o - 4 * n * H
-            call("ppo_gru_step_fwd", hprev, masks.data_ptr(), idx.data_ptr() + 8 * t * n, self.pv(self.GHH),
-                 self.pv(self.GBH), gi.data_ptr() + 3 * o, n, H, hout.data_ptr() + o, sv["r"].data_ptr() + o,
-                 sv["z"].data_ptr() + o, sv["n"].data_ptr() + o, sv["ghn"].data_ptr() + o, sv["hin"].data_ptr() + o,
-                 s)
+        call("ppo_gru_seq_fwd", h0.data_ptr(), masks.data_ptr(), idx.data_ptr(), self.pv(self.GHH), self.pv(self.GBH),
+             gi.data_ptr(), T, n, H, hout.data_ptr(), sv["r"].data_ptr(), sv["z"].data_ptr(), sv["n"].data_ptr(),
+             sv["ghn"].data_ptr(), sv["hin"].data_ptr(), s)
         dout = ws.get("dout", R * H, device=dev)
         self._heads_train(storage, adv, idx, hout, R, hp, loss_acc, dout, feat_act=0)
         # backward through time
@@ -399,14 +392,9 @@ class RecurrentEngine(CNNEngine):
         dgh = ws.get("dgh", R * 3 * H, device=dev)
         dhz = ws.get("dhz", n * H, device=dev)
         carry = ws.get("carry", n * H, device=dev)
-        for t in range(T - 1, -1, -1):
-            o = 4 * t * n * H
-            call("ppo_gru_cell_bwd", dout.data_ptr() + o, carry.data_ptr(), sv["r"].data_ptr() + o,
-                 sv["z"].data_ptr() + o, sv["n"].data_ptr() + o, sv["ghn"].data_ptr() + o, sv["hin"].data_ptr() + o,
-                 dgi.data_ptr() + 3 * o, dgh.data_ptr() + 3 * o, dhz.data_ptr(), n, H, int(t < T - 1), s)
-            if t > 0:
-                call("ppo_gru_step_bwd", dgh.data_ptr() + 3 * o, self.whhT, dhz.data_ptr(), masks.data_ptr(),
-                     idx.data_ptr() + 8 * t * n, carry.data_ptr(), n, H, s)
+        call("ppo_gru_seq_bwd", dout.data_ptr(), sv["r"].data_ptr(), sv["z"].data_ptr(), sv["n"].data_ptr(),
+             sv["ghn"].data_ptr(), sv["hin"].data_ptr(), masks.data_ptr(), idx.data_ptr(), self.whhT, T, n, H,
+             dgi.data_ptr(), dgh.data_ptr(), dhz.data_ptr(), carry.data_ptr(), s)
         self._dense_wgrad(dgh, sv["hin"], R, 3 * H, H, 0, 0, self.GHH, self.GBH)
         self._dense_wgrad(dgi, x, R, 3 * H, self.Ip, 3, self.I, self.GIH, self.GBI)
         dh = ws.get("dh", R * H, device=dev)

@@ -71,6 +71,10 @@ SIGNATURES = {
     "ppo_gru_cell_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p],
     "ppo_gru_step_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p],
     "ppo_gru_variant_set": [c_int],
+    "ppo_gru_variant_get": [],
+    "ppo_gru_seq_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    "ppo_gru_seq_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
+    "ppo_gru_step_bwd_cell": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "ppo_gru_pack": [c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p],
     "ppo_concat_cols": [c_p, c_p, c_ll, c_int, c_p, c_int, c_int, c_int, c_p],
     "ppo_rec_indices": [c_p, c_int, c_int, c_int, c_p, c_p],

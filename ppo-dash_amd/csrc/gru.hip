@@ -110,6 +110,24 @@ struct GruBwdStep : C_ {
 //   dn = dh'(1-z), dz = dh'(h_in - n), da_n = dn(1-n²), dr = da_n·ghn,
 //   da_r = dr·r(1-r), da_z = dz·z(1-z);  dgi = [da_r, da_z, da_n],
 //   dgh = [da_r, da_z, da_n·r];  dhz = dh'·z
+__device__ __forceinline__ void gru_cell_bwd_elem(float dh, float rr, float zz, float nn, float ghn, float hin,
+                                                  size_t i, size_t g, int H, float* __restrict__ dgi,
+                                                  float* __restrict__ dgh, float* __restrict__ dhz) {
+  const float dn = dh * (1.0f - zz);
+  const float dz = dh * (hin - nn);
+  const float dan = dn * (1.0f - nn * nn);
+  const float dr = dan * ghn;
+  const float dar = dr * rr * (1.0f - rr);
+  const float daz = dz * zz * (1.0f - zz);
+  dgi[g] = dar;
+  dgi[g + H] = daz;
+  dgi[g + 2 * H] = dan;
+  dgh[g] = dar;
+  dgh[g + H] = daz;
+  dgh[g + 2 * H] = dan * rr;
+  dhz[i] = dh * zz;
+}
+
 __global__ __launch_bounds__(256) void gru_cell_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ carry,
                                                            const float* __restrict__ r, const float* __restrict__ z,
                                                            const float* __restrict__ n, const float* __restrict__ ghn,
@@ -120,21 +138,7 @@ __global__ __launch_bounds__(256) void gru_cell_bwd_kernel(const float* __restri
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const int m = (int)(i / H), j = (int)(i - (long long)m * H);
     const float dh = dout[i] + (has_carry ? carry[i] : 0.f);
-    const float zz = z[i], nn = n[i], rr = r[i];
-    const float dn = dh * (1.0f - zz);
-    const float dz = dh * (hin[i] - nn);
-    const float dan = dn * (1.0f - nn * nn);
-    const float dr = dan * ghn[i];
-    const float dar = dr * rr * (1.0f - rr);
-    const float daz = dz * zz * (1.0f - zz);
-    const size_t g = (size_t)m * 3 * H + j;
-    dgi[g] = dar;
-    dgi[g + H] = daz;
-    dgi[g + 2 * H] = dan;
-    dgh[g] = dar;
-    dgh[g + H] = daz;
-    dgh[g + 2 * H] = dan * rr;
-    dhz[i] = dh * zz;
+    gru_cell_bwd_elem(dh, r[i], z[i], n[i], ghn[i], hin[i], (size_t)i, (size_t)m * 3 * H + j, H, dgi, dgh, dhz);
   }
 }
 
@@ -282,6 +286,14 @@ __global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict
   }
 }
 
+// step t-1's cell-backward inputs/outputs, fused into step t's carry epilogue
+// (dout NULL: no fusion).  dhz is read for step t and rewritten for t-1 by the
+// same thread, element by element.
+struct CellPrev {
+  const float *dout, *r, *z, *n, *ghn, *hin;
+  float *dgi, *dgh;
+};
+
 // backward: carry = (dgh · W_hh + dh'·z) · m(t) for the block's 32 rows x 16 units
 // (B = W_hhᵀ packed [H][3H]: unit j's column of W_hh is row j, contiguous)
 template <int H>
@@ -290,7 +302,8 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
                                                              const float* __restrict__ dhz,
                                                              const float* __restrict__ masks,
                                                              const int64_t* __restrict__ mask_idx,
-                                                             float* __restrict__ carry, int M) {
+                                                             float* __restrict__ carry, int M,
+                                                             const CellPrev cp) {
   constexpr int KW = 3 * H / 16;
   constexpr int NH = KW % 8 == 0 ? 2 : 1, KH = KW / NH;   // K halves keep the operand registers small
   __shared__ f32x4 P[4][2][64];
@@ -335,7 +348,11 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
     const float v = ((P[0][rt][ln][rg] + P[1][rt][ln][rg]) + P[2][rt][ln][rg]) + P[3][rt][ln][rg];
     const float mk = masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
     const size_t o = (size_t)m * H + j;
-    carry[o] = (v + dhz[o]) * mk;
+    const float cv = (v + dhz[o]) * mk;
+    carry[o] = cv;
+    if (cp.dout)   // the previous step's cell backward for this element (gru_cell_bwd_kernel, fused)
+      gru_cell_bwd_elem(cp.dout[o] + cv, cp.r[o], cp.z[o], cp.n[o], cp.ghn[o], cp.hin[o], o,
+                        (size_t)m * 3 * H + j, H, cp.dgi, cp.dgh, const_cast<float*>(dhz));
   }
 }
 
@@ -354,9 +371,9 @@ int launch_step16(const float* hprev, const float* masks, const int64_t* mask_id
 
 template <int H>
 int launch_step_bwd16(const float* dgh, const float* whhT, const float* dhz, const float* masks,
-                      const int64_t* mask_idx, float* carry, int M, hipStream_t st) {
+                      const int64_t* mask_idx, float* carry, int M, hipStream_t st, const CellPrev& cp = CellPrev{}) {
   dim3 grid((unsigned)ceil_div(M, 32), H / 16);
-  gru_step_bwd16_kernel<H><<<grid, 256, 0, st>>>(dgh, whhT, dhz, masks, mask_idx, carry, M);
+  gru_step_bwd16_kernel<H><<<grid, 256, 0, st>>>(dgh, whhT, dhz, masks, mask_idx, carry, M, cp);
   PPO_LAUNCH_CHECK("gru_step_bwd16_kernel");
   return 0;
 }
@@ -420,6 +437,75 @@ PPO_API int ppo_gru_step_bwd(const float* dgh, const float* whhT, const float* d
   GruBwdStep<CfgGruB> p;
   p.dgh = dgh; p.whhT = whhT; p.dhz = dhz; p.masks = masks; p.mask_idx = mask_idx; p.carry = carry; p.M = M; p.H = H;
   return launch(p, M, H, 1, as_stream(stream), "gru_step_bwd", 2.0 * M * 3 * H * H);
+}
+
+// step t's carry GEMM fused with step t-1's cell backward (the BPTT loop body:
+// ppo_gru_step_bwd(t) then ppo_gru_cell_bwd(t-1, carry) in one launch)
+PPO_API int ppo_gru_step_bwd_cell(const float* dgh, const float* whhT, float* dhz, const float* masks,
+                                  const int64_t* mask_idx, float* carry, int M, int H, const float* dout_prev,
+                                  const float* r, const float* z, const float* n, const float* ghn, const float* hin,
+                                  float* dgi_prev, float* dgh_prev, void* stream) {
+  PPO_REQUIRE(M >= 0 && (H == 64 || H == 128 || H == 256 || H == 512) && g_gru_variant == 0,
+              "ppo_gru_step_bwd_cell: M=%d H=%d (H in 64/128/256/512, register-tiled variant)", M, H);
+  if (M == 0) return 0;
+  const CellPrev cp{dout_prev, r, z, n, ghn, hin, dgi_prev, dgh_prev};
+  hipStream_t st = as_stream(stream);
+  switch (H) {
+    case 64: return launch_step_bwd16<64>(dgh, whhT, dhz, masks, mask_idx, carry, M, st, cp);
+    case 128: return launch_step_bwd16<128>(dgh, whhT, dhz, masks, mask_idx, carry, M, st, cp);
+    case 256: return launch_step_bwd16<256>(dgh, whhT, dhz, masks, mask_idx, carry, M, st, cp);
+    default: return launch_step_bwd16<512>(dgh, whhT, dhz, masks, mask_idx, carry, M, st, cp);
+  }
+}
+
+PPO_API int ppo_gru_variant_get(void) { return g_gru_variant; }
+
+// Whole-sequence loops (model.py:116-165 forward; its backward through time) run
+// from C: one ABI call per minibatch instead of T (or 2T) Python->ctypes calls,
+// which at ~10 us per step kernel were the critical path of the recurrent update.
+// Rows of step t are t*n .. t*n + n - 1; mask of row j at step t: masks[idx[t*n + j]]
+// (idx NULL: masks[t*n + j]).
+PPO_API int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* idx, const float* whh,
+                            const float* bhh, const float* gi, int T, int n, int H, float* hout, float* save_r,
+                            float* save_z, float* save_n, float* save_ghn, float* save_hin, void* stream) {
+  PPO_REQUIRE(T >= 0 && n >= 0 && H > 0 && H % 32 == 0, "ppo_gru_seq_fwd: T=%d n=%d H=%d", T, n, H);
+  const bool sv = save_r != nullptr;
+  for (int t = 0; t < T; ++t) {
+    const size_t o = (size_t)t * n * H;
+    // with idx the mask plane is indexed through it; without, masks is [T][n]
+    const float* mk = masks && !idx ? masks + (size_t)t * n : masks;
+    const int rc = ppo_gru_step_fwd(t == 0 ? h0 : hout + o - (size_t)n * H, mk, idx ? idx + (size_t)t * n : nullptr,
+                                    whh, bhh, gi + 3 * o, n, H, hout + o, sv ? save_r + o : nullptr,
+                                    sv ? save_z + o : nullptr, sv ? save_n + o : nullptr, sv ? save_ghn + o : nullptr,
+                                    sv ? save_hin + o : nullptr, stream);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+PPO_API int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float* save_z, const float* save_n,
+                            const float* save_ghn, const float* save_hin, const float* masks, const int64_t* idx,
+                            const float* whhT, int T, int n, int H, float* dgi, float* dgh, float* dhz, float* carry,
+                            void* stream) {
+  PPO_REQUIRE(T >= 0 && n >= 0 && H > 0 && H % 4 == 0, "ppo_gru_seq_bwd: T=%d n=%d H=%d", T, n, H);
+  const bool fused = (H == 64 || H == 128 || H == 256 || H == 512) && g_gru_variant == 0;
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t o = (size_t)t * n * H, op = o - (size_t)n * H;
+    int rc = 0;
+    if (!fused || t == T - 1)
+      rc = ppo_gru_cell_bwd(dout + o, carry, save_r + o, save_z + o, save_n + o, save_ghn + o, save_hin + o,
+                            dgi + 3 * o, dgh + 3 * o, dhz, n, H, t < T - 1, stream);
+    if (!rc && t > 0) {
+      const int64_t* mi = idx ? idx + (size_t)t * n : nullptr;
+      const float* mk = masks && !idx ? masks + (size_t)t * n : masks;
+      rc = fused ? ppo_gru_step_bwd_cell(dgh + 3 * o, whhT, dhz, mk, mi, carry, n, H, dout + op, save_r + op,
+                                         save_z + op, save_n + op, save_ghn + op, save_hin + op, dgi + 3 * op,
+                                         dgh + 3 * op, stream)
+                 : ppo_gru_step_bwd(dgh + 3 * o, whhT, dhz, mk, mi, carry, n, H, stream);
+    }
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 // A/B switch for the step kernels (0 register-tiled, 1 tile GEMM)
