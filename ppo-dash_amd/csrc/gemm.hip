@@ -1029,10 +1029,17 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
   for (int i = tid; i < 2 * 3 * PLU; i += 512) reinterpret_cast<uint4*>(&S[0][0])[i] = uint4{0, 0, 0, 0};
   // unit index of this lane's A fragment per row tile for tap (0, 0); tap
   // (ky, kx) subtracts 25 ky + kx
-  int qrow[3];
+  // Row tiles and the taps they need: a tap whose source pixel is off the 7 x 7
+  // grid for all 16 rows of a tile is skipped (tile 0: ky <= 1, tile 4: ky >= 1,
+  // tile 5 = pixel 80 alone: tap (2, 2) only) — 40 of the 54 tile-taps.  Wave
+  // halves take tiles {1, 2, 5} (19 tile-taps) and {0, 3, 4} (21).
+  constexpr unsigned TILES = 0x430521u;   // nibbles: tiles of half 0 (1, 2, 5), half 1 (0, 3, 4)
+  // tap masks per tile (bit 3 ky + kx): {0x03F, 0x1FF, 0x1FF, 0x1FF, 0x1F8, 0x100}
+  int qrow[3], tl[3];
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
-    const int m = min(16 * (3 * mh + t) + i16, 80), y = m / 9, x = m - 9 * y;   // dummy rows: pixel 80
+    tl[t] = (TILES >> (4 * (3 * mh + t))) & 15;
+    const int m = min(16 * tl[t] + i16, 80), y = m / 9, x = m - 9 * y;   // dummy rows: pixel 80
     qrow[t] = g * CS + (y + 2) * GW + x + 2;
   }
   f32x4 stg[2];
@@ -1082,23 +1089,36 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
     f32x4 acc[3];
 #pragma unroll
     for (int t = 0; t < 3; ++t) acc[t] = zero4();
+    // the tap masks are compile-time in each of the two instantiations, so the
+    // skipped (tile, tap) pairs vanish from the unrolled schedule
+    auto compute = [&](auto M0, auto M1, auto M2) {
+      constexpr unsigned msk[3] = {decltype(M0)::value, decltype(M1)::value, decltype(M2)::value};
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int toff = -(GW * (s / 3) + s % 3);
-      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
-      Frag3 a[3];
+      for (int s = 0; s < KS; ++s) {
+        const int toff = -(GW * (s / 3) + s % 3);
+        const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+        Frag3 a[3];
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const uint16_t* q = Sc + 8 * (qrow[u] + toff);
-        a[u].h = *reinterpret_cast<const bf16x8*>(q);
-        a[u].m = *reinterpret_cast<const bf16x8*>(q + 8 * PLU);
-        a[u].l = *reinterpret_cast<const bf16x8*>(q + 16 * PLU);
-      }
+        for (int u = 0; u < 3; ++u) {
+          if (!((msk[u] >> s) & 1u)) continue;
+          const uint16_t* q = Sc + 8 * (qrow[u] + toff);
+          a[u].h = *reinterpret_cast<const bf16x8*>(q);
+          a[u].m = *reinterpret_cast<const bf16x8*>(q + 8 * PLU);
+          a[u].l = *reinterpret_cast<const bf16x8*>(q + 16 * PLU);
+        }
 #define PPO_PART(X, Y) \
-  _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[u] = mma(a[u].X, w.Y, acc[u]);
-      PPO_PRODUCTS(NP, PPO_PART)
+  _Pragma("unroll") for (int u = 0; u < 3; ++u) if ((msk[u] >> s) & 1u) acc[u] = mma(a[u].X, w.Y, acc[u]);
+        PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
-    }
+      }
+    };
+    using std::integral_constant;
+    if (mh == 0)
+      compute(integral_constant<unsigned, 0x1FF>{}, integral_constant<unsigned, 0x1FF>{},
+              integral_constant<unsigned, 0x100>{});
+    else
+      compute(integral_constant<unsigned, 0x03F>{}, integral_constant<unsigned, 0x1FF>{},
+              integral_constant<unsigned, 0x1F8>{});
     // epilogue: C row 4g + r of tile t is input pixel m; ReLU mask of a2
     const uint8_t* mk = reinterpret_cast<const uint8_t*>(Mk[cur]);
     float* o = dz2 + (size_t)b * 5184 + ci;
@@ -1106,7 +1126,7 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
     for (int t = 0; t < 3; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = 16 * (3 * mh + t) + 4 * g + r;
+        const int m = 16 * tl[t] + 4 * g + r;
         if (m < 81) o[m * 64] = mk[m * 64 + ci] ? acc[t][r] : 0.f;
       }
     __syncthreads();   // every wave is done with stage cur; stage cur ^ 1 is complete
