@@ -1089,3 +1089,39 @@ def test_gru_step_kernels_vs_float64(gpu, M, H):
         for k, v in ref.items():
             err = (out[k].cpu().double() - v).abs().max().item()
             assert err <= 2e-5 * max(v.abs().max().item(), 1.0), (variant, k, err)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_conv1_wgrad_variants_vs_torch(gpu, variant):
+    """conv1 weight + bias gradient from u8 observations gathered by index (the
+    minibatch path): the 8-wave kernel (1, default) and the one-k-group-per-wave
+    kernel (2) vs torch float64 on (u8 / 255): max |err| <= 1e-5 * max |ref|.
+    B = 300 images, rows gathered out of order."""
+    Hh = _hip()
+    B, rows = 300, 420
+    g = torch.Generator().manual_seed(81)
+    obs = torch.randint(0, 256, (rows, 4, 84, 84), dtype=torch.uint8, generator=g)
+    idx = torch.randperm(rows, generator=g)[:B].contiguous()
+    dz1 = torch.randn(B, 20, 20, 32, generator=g)
+    obs_d, idx_d, dz1_d = obs.cuda(), idx.cuda(), dz1.cuda()
+    Z = Hh.call("ppo_wgrad_splits", B * 400, 1, 2048, 16)
+    slab = torch.empty(Z * 32 * 256, device=gpu)
+    slab_b = torch.empty(Z * 32, device=gpu)
+    gw = torch.empty(32 * 256, device=gpu)
+    gb = torch.empty(32, device=gpu)
+    Hh.call("ppo_tune_set", b"conv1_wgrad", variant)
+    try:
+        Hh.call("ppo_conv1_wgrad", dz1_d.data_ptr(), obs_d.data_ptr(), 1, idx_d.data_ptr(), 0, 4, B, Z,
+                slab.data_ptr(), slab_b.data_ptr(), _s())
+        Hh.call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, 32, 256, 0, 0, 0, gw.data_ptr(),
+                gb.data_ptr(), 1.0 / 255, 0, _s())
+        torch.cuda.synchronize()
+    finally:
+        Hh.call("ppo_tune_set", b"conv1_wgrad", 1)
+    x = obs[idx].double() / 255.0
+    dy = dz1.double().permute(0, 3, 1, 2)
+    ref_w = torch.nn.grad.conv2d_weight(x, (32, 4, 8, 8), dy, stride=4)
+    ref_b = dy.sum((0, 2, 3))
+    for got, ref in ((gw.cpu().double().view(32, 4, 8, 8), ref_w), (gb.cpu().double(), ref_b)):
+        err = (got - ref).abs().max().item()
+        assert err <= 1e-5 * ref.abs().max().item(), err
