@@ -242,6 +242,31 @@ def pmc_traffic(kernel, workload):
     return d.get("traffic_bytes_per_launch"), f"profiles/{d.get('tag', '?')}_traffic.json"
 
 
+# bench kernel name -> the kernel symbol in the rocprofv3 PMC summaries
+PMC_SYMBOL = {"conv2_fwd": "conv2_fwd_x9_kernel<", "conv2_dgrad": "conv2_dgrad_x9_kernel<",
+              "conv2_wgrad": "conv2_wgrad_x9_kernel<", "conv3_fwd": "conv3_fwd_x9_kernel<",
+              "conv3_dgrad": "conv3_dgrad_x9_kernel<", "conv3_wgrad": "conv3_wgrad_x9_kernel<",
+              "conv1_wgrad_u8": "conv1_wgrad_bf16x3_kernel<", "conv1_fwd_u8": "conv1_fwd_bf16x3_kernel<"}
+
+
+def pmc_mfma(workload):
+    """Measured MFMA pipeline utilisation per bench kernel (SQ_VALU_MFMA_BUSY_CYCLES
+    over SIMD-cycles, tools/profile_round.sh 'mfma' pass) — same workload only."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "roofline_traffic.json")))
+        m = json.load(open(os.path.join(ROOT, d["mfma_util_file"])))
+    except (OSError, ValueError, KeyError):
+        return {}, None
+    if m.get("workload") != workload:
+        return {}, None
+    out = {}
+    for name, sym in PMC_SYMBOL.items():
+        for k, v in m["kernels"].items():
+            if k.startswith(sym):
+                out[name] = v["mfma_util"]
+    return out, d["mfma_util_file"]
+
+
 def cpu_baseline(envs, T, E, M, hidden, threads):
     """The oracle's numpy (fp32) restatement of the reference CPU path, timed on a
     bounded sample: `envs` lanes x T steps, E x M minibatches."""
@@ -377,6 +402,10 @@ def main():
                          "frac": round(achieved / peak, 4), "ms_total": round(ms_total, 2),
                          "launches": int(launches), "avg_launch_ms": round(ms_total / launches, 4),
                          "fp32_tflops": round(tflops, 2), "instructions": how}
+    util, util_src = pmc_mfma(workload)
+    for name, u in util.items():
+        if name in kernels:
+            kernels[name]["mfma_util_pmc"] = u
     roof = None
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
@@ -386,6 +415,7 @@ def main():
                 "frac": kd["frac"], "traffic": round(traffic) if traffic else None,
                 "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tsrc, "kernel": dom,
                 "launches": kd["launches"], "avg_launch_ms": kd["avg_launch_ms"],
+                "mfma_util_pmc": kd.get("mfma_util_pmc"), "mfma_util_source": util_src,
                 "flop_per_launch": round(per_kernel[dom][2] / per_kernel[dom][0])}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

@@ -26,6 +26,32 @@ def per_launch(path, counter, sub):
     return (sum(vals) / len(vals) if vals else None), len(vals)
 
 
+def mfma_util(path):
+    """per kernel name: average MFMA pipeline utilisation over its launches"""
+    if not os.path.exists(path):
+        return None
+    per = {}
+    for r in csv.DictReader(open(path)):
+        key = (r["Kernel_Name"], r.get("Dispatch_Id") or r.get("Correlation_Id"))
+        per.setdefault(key, {})[r["Counter_Name"]] = float(r["Counter_Value"])
+    agg = {}
+    for (name, _), c in per.items():
+        if "GRBM_GUI_ACTIVE" not in c or "SQ_VALU_MFMA_BUSY_CYCLES" not in c or c["GRBM_GUI_ACTIVE"] <= 0:
+            continue
+        short = name.split("(")[0].replace("(anonymous namespace)::", "").replace("void ", "")[:80]
+        a = agg.setdefault(short, [0, 0.0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += c["SQ_VALU_MFMA_BUSY_CYCLES"]
+        a[2] += c["GRBM_GUI_ACTIVE"]
+        a[3] += c.get("SQ_INSTS_MFMA", 0.0)
+    out = {}
+    for k, (n, busy, gui, insts) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
+        if insts <= 0:
+            continue
+        out[k] = {"launches": n, "mfma_util": round(busy / (1024 * gui / 8), 4), "mfma_insts_per_launch": insts / n}
+    return out
+
+
 def main():
     tag = sys.argv[1]
     sub = sys.argv[2] if len(sys.argv) > 2 else "Conv2Dgrad"
@@ -49,6 +75,13 @@ def main():
            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of wide streaming reads), WRITE_SIZE KiB x1024",
            "source": "tools/profile_round.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) of "
                      "`python3 bench.py --no-cpu-baseline --no-gae-roofline`"}
+    mfma = mfma_util(os.path.join(OUT, "pmcb", "mfma_counter_collection.csv"))
+    if mfma:
+        json.dump({"tag": tag, "workload": json.loads(line)["config"]["workload"],
+                   "definition": "util = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x GRBM_GUI_ACTIVE / XCDs); "
+                                 "SIMDs = 1024, XCDs = 8 (GRBM_GUI_ACTIVE sums the 8 XCDs)",
+                   "kernels": mfma}, open(os.path.join(prof, f"{tag}_mfma.json"), "w"), indent=1)
+        out["mfma_util_file"] = f"profiles/{tag}_mfma.json"
     out["tag"] = tag
     out["workload"] = json.loads(line)["config"]["workload"]   # bench.py only uses traffic of the same workload
     json.dump(out, open(os.path.join(prof, f"{tag}_traffic.json"), "w"), indent=1)

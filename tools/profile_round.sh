@@ -13,4 +13,6 @@ grep '^{' gpurun_out/bench_full.log
 step stats timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-gae-roofline --no-boundary $BENCH_ARGS
 step fetch timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcb -o fetch -- python3 bench.py --no-cpu-baseline --no-gae-roofline --no-boundary $BENCH_ARGS
 step write timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$K" --output-format csv -d gpurun_out/pmcb -o write -- python3 bench.py --no-cpu-baseline --no-gae-roofline --no-boundary $BENCH_ARGS
+# MFMA utilisation of every kernel: pipeline-busy SIMD-cycles / (SIMDs x active cycles)
+step mfma timeout -k 10 900 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcb -o mfma -- python3 bench.py --no-cpu-baseline --no-gae-roofline --no-boundary --steps 1 --warmup 1 $BENCH_ARGS
 echo done
