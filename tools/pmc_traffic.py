@@ -38,7 +38,7 @@ def mfma_util(path):
     for (name, _), c in per.items():
         if "GRBM_GUI_ACTIVE" not in c or "SQ_VALU_MFMA_BUSY_CYCLES" not in c or c["GRBM_GUI_ACTIVE"] <= 0:
             continue
-        short = name.split("(")[0].replace("(anonymous namespace)::", "").replace("void ", "")[:80]
+        short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:80]
         a = agg.setdefault(short, [0, 0.0, 0.0, 0.0])
         a[0] += 1
         a[1] += c["SQ_VALU_MFMA_BUSY_CYCLES"]
