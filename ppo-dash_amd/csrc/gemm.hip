@@ -321,7 +321,10 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  const int cq = tid & 7;                 // dz staging: channel quad of this thread
+  // dz staging runs from the top thread down (u = NT - 1 - tid + NT i): the waves
+  // that expand the image (tid < 336) get the fewer dz units
+  const int rt = NT - 1 - tid;
+  const int cq = rt & 7;                  // dz staging: channel quad of this thread
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};   // bias partial of channels 4 cq .. +3
 
   f32x4 dzr[2][4];        // up to 2 units of 4 pixels x 4 channels
@@ -330,7 +333,7 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
     const float* dzb = dz1 + (size_t)b * NPX * 32;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int u = tid + NT * i;
+      const int u = rt + NT * i;
       if (u < 800) {
         const int p4 = u >> 3;
 #pragma unroll
@@ -347,7 +350,7 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
   auto put = [&]() {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int u = tid + NT * i;
+      const int u = rt + NT * i;
       if (u < 800) {
         const int p4 = u >> 3;
 #pragma unroll
@@ -443,7 +446,7 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
   if (tid < 32) {   // channel tid: the 64 threads of its quad, fixed order
     const int q = tid & 3, c8 = tid >> 2;
     float t = 0.f;
-    for (int j = c8; j < NT; j += 8) t += bred[j * 4 + q];
+    for (int j = 7 - c8; j < NT; j += 8) t += bred[j * 4 + q];   // threads with cq = c8
     slab_bias[(size_t)blockIdx.x * 32 + tid] = t;
   }
 }
