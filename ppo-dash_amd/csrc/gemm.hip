@@ -1576,7 +1576,7 @@ __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __rest
 //   repacking: lane (n, g) of k-step s reads W2d[n][64 g + 8 s .. +7].
 // Wave w owns n tile w (phase w >> 1, ci 16 (w & 1) + [0, 16)) for all of K,
 // its weight fragments (pre-split planes, 8 k-steps x 3) in 96 VGPRs.
-template <int NP, bool PIPE = false>
+template <int NP>
 __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __restrict__ dz2, int B,
                                                             const uint16_t* __restrict__ wpl,
                                                             const float* __restrict__ a1,
@@ -1627,8 +1627,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
 #pragma unroll
     for (int j = 0; j < MPER; ++j) {
       const int c = tid + 512 * j;
-      if (PIPE) mst[j] = ms[c < MC ? c : 0];
-      else if (c < MC) mst[j] = ms[c];
+      if (c < MC) mst[j] = ms[c];
     }
   };
   auto put = [&](int buf) {
@@ -1655,52 +1654,21 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
   };
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
-  // PIPE (experimental, ppo_tune_set("conv2_dgrad", 9); NOT parity-clean yet:
-  // test_conv2_dgrad_variants_vs_torch fails on it): staging is unconditional
-  // (images past the end re-read image B - 1 and are never used) and the
-  // epilogue is software-pipelined — the masked rows of image b stay in acc and
-  // are stored at the top of the next iteration, after that iteration's loads
-  // are issued and before its MFMA loop, so the stores drain under the next
-  // image's compute instead of stalling the next put() (which waits for its
-  // loads; the in-order vmcnt makes that wait for older stores too).  Every lane
-  // issues all 28 stores through a buffer resource; a dummy row (and the whole
-  // first, empty round: num_records 0) stores past num_records, which the
-  // hardware drops.
+  // (Tried: a software-pipelined epilogue — image b's stores issued after image
+  // b+1's loads, through a range-checked buffer resource — measured neutral,
+  // 2.454 vs 2.467 ms at the c3 minibatch; it is in the history, commit 3585bac.)
   const int cb = (ph >> 1) * 640 + (ph & 1) * 32 + ci;
-  f32x4 acc[MT];
-  auto store = [&](int bp, int bytes) {
-    const __amdgpu_buffer_rsrc_t dm =
-        __builtin_amdgcn_make_buffer_rsrc(dz1 + (size_t)bp * 12800, 0, bytes, 0x00020000);
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const int4 e = *reinterpret_cast<const int4*>(&etab[16 * t + 4 * g]);
-      const int eo[4] = {e.x, e.y, e.z, e.w};
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[t][r]), dm,
-                                              eo[r] >= 0 ? 4 * (eo[r] + cb) : 0x10000000, 0, 0);
-    }
-  };
   if (b < B) {
     fetch(b);
     put(0);
-    if (PIPE) fetch(min(b + G, B - 1));
-    else if (b + G < B) fetch(b + G);
+    if (b + G < B) fetch(b + G);
   }
   __syncthreads();
-  int bp = b;
   for (; b < B; b += G) {
-    if constexpr (PIPE) {
-      put(cur ^ 1);
-      fetch(min(b + 2 * G, B - 1));
-      store(bp, b == blockIdx.x ? 0 : 12800 * 4);
-      __builtin_amdgcn_sched_barrier(0);   // keep loads and stores ahead of the MFMA loop
-      bp = b;
-    } else {
-      if (b + G < B) put(cur ^ 1);
-      if (b + 2 * G < B) fetch(b + 2 * G);
-    }
+    if (b + G < B) put(cur ^ 1);
+    if (b + 2 * G < B) fetch(b + 2 * G);
     const char* Sb = reinterpret_cast<const char*>(S[cur][0]);
+    f32x4 acc[MT];
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = zero4();
 #pragma unroll
@@ -1735,21 +1703,14 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
       const int4 e = *reinterpret_cast<const int4*>(&etab[16 * t + 4 * g]);
       const int eo[4] = {e.x, e.y, e.z, e.w};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr (PIPE) {   // masked in place, stored next iteration
-          const int i = eo[r] >= 0 ? eo[r] + cb : 0;
-          acc[t][r] = mk[i] ? acc[t][r] : 0.f;
-        } else if (eo[r] >= 0) {
+      for (int r = 0; r < 4; ++r)
+        if (eo[r] >= 0) {
           const int i = eo[r] + cb;
           dm[i] = mk[i] ? acc[t][r] : 0.f;
         }
-      }
     }
     __syncthreads();   // every wave is done with S[cur]; S[cur ^ 1] is complete
     cur ^= 1;
-  }
-  if constexpr (PIPE) {
-    if (bp < B) store(bp, 12800 * 4);
   }
 }
 
@@ -2320,17 +2281,14 @@ PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const flo
 }
 
 PPO_API int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const float* a1, float* dz1, void* stream) {
-  if (g_tune[TK_CONV2_DGRAD] == 8 || g_tune[TK_CONV2_DGRAD] == 9) {
+  if (g_tune[TK_CONV2_DGRAD] == 8) {
     if (B <= 0) return 0;
     const int n_cu = device_cus();
     const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
     int slot;
     const bool prof = ppo_prof_begin("conv2_dgrad", as_stream(stream), &slot);
     const uint16_t* wpl = planes_of(w2d, 128 * 256);
-    if (g_tune[TK_CONV2_DGRAD] == 9)   // experimental pipelined epilogue (see the kernel)
-      conv2_dgrad_x9_kernel<6, true><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, a1, dz1);
-    else
-      PPO_LAUNCH_NP(conv2_dgrad_x9_kernel, nb, 512, as_stream(stream), dz2, B, wpl, a1, dz1);
+    PPO_LAUNCH_NP(conv2_dgrad_x9_kernel, nb, 512, as_stream(stream), dz2, B, wpl, a1, dz1);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
     PPO_LAUNCH_CHECK("conv2_dgrad_x9_kernel");
     return 0;
