@@ -95,6 +95,10 @@ int ppo_pack_weights(const float* w2, const float* w3, const float* w4, int H, f
  * to the accumulator (Σ w·u/255) */
 int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B, const float* w1,
                   const float* b1, float* out, void* stream);
+/* the same, also writing the ReLU mask of `out` as bits for the backward pass
+ * (mbits [B][400] u32: bit c of pixel p = out[p][c] > 0, 1.6 KB per image) */
+int ppo_conv1_fwd_mask(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
+                       const float* w1, const float* b1, float* out, uint32_t* mbits, void* stream);
 /* model.py:178 Conv2d(32,64,4,s2)+ReLU */
 int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream);
 /* model.py:179 Conv2d(64,32,3,s1)+ReLU */
@@ -121,6 +125,12 @@ int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N,
                           void* stream);
 int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream);
 int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const float* a1, float* dz1, void* stream);
+/* conv2 dgrad with conv1's ReLU mask as bits (from ppo_conv1_fwd_mask) instead of
+ * the fp32 activations: 1.6 KB instead of 51.2 KB read per image; available when
+ * ppo_conv2_dgrad_bits_ok() (the image-resident kernel is selected) */
+int ppo_conv2_dgrad_bits_ok(void);
+int ppo_conv2_dgrad_bits(const float* dz2, int B, const float* w2d, const uint32_t* m1bits, float* dz1,
+                         void* stream);
 int ppo_wgrad_splits(long long R, int tiles, int target_blocks, int min_ktiles);
 int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C,
                     int B, int Z, float* slab, float* slab_bias, void* stream);

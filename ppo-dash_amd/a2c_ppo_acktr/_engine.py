@@ -141,8 +141,15 @@ class CNNEngine:
         if out is None:
             out, ldo = ws.get("h", B * self.H, device=dev), self.H
         s = stream()
-        call("ppo_conv1_fwd", obs.data_ptr(), is_u8, ptr(idx, torch.int64, "idx"), 0, self.C, B, self.pv(self.W1),
-             self.pv(self.B1), a1.data_ptr(), s)
+        if ws is self.ws["train"]:
+            # training forward: conv1 also writes its ReLU mask as bits for conv2's dgrad
+            m1 = ws.get("m1bits", B * 400, dtype=torch.int32, device=dev)
+            call("ppo_conv1_fwd_mask", obs.data_ptr(), is_u8, ptr(idx, torch.int64, "idx"), 0, self.C, B,
+                 self.pv(self.W1), self.pv(self.B1), a1.data_ptr(), m1.data_ptr(), s)
+            self._m1_rows = B
+        else:
+            call("ppo_conv1_fwd", obs.data_ptr(), is_u8, ptr(idx, torch.int64, "idx"), 0, self.C, B,
+                 self.pv(self.W1), self.pv(self.B1), a1.data_ptr(), s)
         call("ppo_conv2_fwd", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), s)
         call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
         call("ppo_fc_fwd", a3.data_ptr(), B, self.pk(2), self.pv(self.B4), self.H, out.data_ptr(), ldo, s)
@@ -217,7 +224,11 @@ class CNNEngine:
         self._wgrad("fc", B, dh, a3, None, s)
         call("ppo_conv3_dgrad", dz3.data_ptr(), B, self.pk(4), a2.data_ptr(), dz2.data_ptr(), s)
         self._wgrad("conv3", B, dz3, a2, None, s)
-        call("ppo_conv2_dgrad", dz2.data_ptr(), B, self.pk(5), a1.data_ptr(), dz1.data_ptr(), s)
+        if getattr(self, "_m1_rows", None) == B and call("ppo_conv2_dgrad_bits_ok"):
+            call("ppo_conv2_dgrad_bits", dz2.data_ptr(), B, self.pk(5), ws.bufs["m1bits"].data_ptr(), dz1.data_ptr(),
+                 s)
+        else:
+            call("ppo_conv2_dgrad", dz2.data_ptr(), B, self.pk(5), a1.data_ptr(), dz1.data_ptr(), s)
         self._wgrad("conv2", B, dz2, a1, None, s)
         self._wgrad("conv1", B, dz1, obs, idx, s)
 

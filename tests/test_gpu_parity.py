@@ -807,6 +807,49 @@ def test_conv2_dgrad_variants_vs_torch(gpu, variant):
     assert err <= 1e-5 * ref.abs().max().item(), err
 
 
+@pytest.mark.parametrize("conv1_variant", [0, 9])
+def test_conv1_mask_bits_and_conv2_dgrad_bits(gpu, conv1_variant):
+    """ppo_conv1_fwd_mask (fused ballot epilogue: variant 0; conv + relu_bits
+    kernel: variant 9) writes bit c of word p = (a1[p][c] > 0) of its own fp32
+    output, bit-exactly, with a1 identical to ppo_conv1_fwd's; conv2 dgrad fed
+    those bits (ppo_conv2_dgrad_bits) equals the fp32-mask kernel bit for bit.
+    B = 300 > the persistent grid, gathered storage rows."""
+    Hh = _hip()
+    B = 300
+    g = torch.Generator().manual_seed(31)
+    obs = torch.randint(0, 256, (B + 5, 4, 84, 84), dtype=torch.uint8, generator=g).cuda()
+    idx = torch.randperm(B + 5, generator=g)[:B].cuda()
+    w1 = (torch.randn(32, 256, generator=g) * 0.05).cuda()
+    b1 = (torch.randn(32, generator=g) * 0.2).cuda()   # a mix of live and dead units
+    a1 = torch.full((B, 20, 20, 32), float("nan"), device=gpu)
+    a1m = torch.full_like(a1, float("nan"))
+    bits = torch.zeros(B * 400, dtype=torch.int32, device=gpu)
+    Hh.call("ppo_tune_set", b"conv1_fwd", conv1_variant)
+    try:
+        Hh.call("ppo_conv1_fwd", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, w1.data_ptr(), b1.data_ptr(),
+                a1.data_ptr(), _s())
+        Hh.call("ppo_conv1_fwd_mask", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, w1.data_ptr(), b1.data_ptr(),
+                a1m.data_ptr(), bits.data_ptr(), _s())
+        torch.cuda.synchronize()
+    finally:
+        Hh.call("ppo_tune_set", b"conv1_fwd", 0)
+    assert torch.equal(a1, a1m)
+    live = (a1 > 0).reshape(B * 400, 32).cpu().to(torch.int64)
+    want = (live << torch.arange(32, dtype=torch.int64)).sum(1)
+    got = bits.cpu().to(torch.int64) & 0xFFFFFFFF
+    assert torch.equal(got, want)
+    assert 0.2 < live.float().mean().item() < 0.8
+    _, _, pk = _packed(gpu, 64, 32)
+    dz2 = torch.randn(B, 9, 9, 64, generator=g).cuda()
+    d_ref = torch.full_like(a1, float("nan"))
+    d_bits = torch.full_like(a1, float("nan"))
+    Hh.call("ppo_conv2_dgrad", dz2.data_ptr(), B, pk[5], a1.data_ptr(), d_ref.data_ptr(), _s())
+    assert Hh.call("ppo_conv2_dgrad_bits_ok") == 1
+    Hh.call("ppo_conv2_dgrad_bits", dz2.data_ptr(), B, pk[5], bits.data_ptr(), d_bits.data_ptr(), _s())
+    torch.cuda.synchronize()
+    assert torch.equal(d_ref, d_bits)
+
+
 @pytest.mark.parametrize("variant", [0, 8, 10])
 def test_conv2_fwd_variants_vs_torch(gpu, variant):
     """conv2 forward (4x4 stride 2, 20x20x32 -> 9x9x64, bias + ReLU): the split-bf16
