@@ -101,6 +101,9 @@ int ppo_conv1_fwd_mask(const void* obs, int obs_is_u8, const int64_t* idx, long 
                        const float* w1, const float* b1, float* out, uint32_t* mbits, void* stream);
 /* model.py:178 Conv2d(32,64,4,s2)+ReLU */
 int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream);
+/* the same, also writing its ReLU mask as bits (mbits [B][81] u64: bit c of pixel p = out[p][c] > 0) */
+int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const float* b2, float* out, uint64_t* mbits,
+                       void* stream);
 /* model.py:179 Conv2d(64,32,3,s1)+ReLU */
 int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream);
 /* model.py:180 Linear(1568,H)+ReLU (generic Linear+ReLU) */
@@ -124,6 +127,11 @@ int ppo_transpose(const float* src, int rows, int cols, float* dst, void* stream
 int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
                           void* stream);
 int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream);
+/* conv3 dgrad with conv2's ReLU mask as bits (from ppo_conv2_fwd_mask): 648 B instead of
+ * 20.7 KB read per image; available when ppo_conv3_dgrad_bits_ok() */
+int ppo_conv3_dgrad_bits_ok(void);
+int ppo_conv3_dgrad_bits(const float* dz3, int B, const float* w3d, const uint64_t* m2bits, float* dz2,
+                         void* stream);
 int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const float* a1, float* dz1, void* stream);
 /* conv2 dgrad with conv1's ReLU mask as bits (from ppo_conv1_fwd_mask) instead of
  * the fp32 activations: 1.6 KB instead of 51.2 KB read per image; available when

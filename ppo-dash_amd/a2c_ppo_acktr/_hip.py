@@ -44,11 +44,14 @@ SIGNATURES = {
     "ppo_conv1_fwd": [c_p, c_int, c_p, c_ll, c_int, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv1_fwd_mask": [c_p, c_int, c_p, c_ll, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "ppo_conv2_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],
+    "ppo_conv2_fwd_mask": [c_p, c_int, c_p, c_p, c_p, c_p, c_p],
     "ppo_conv3_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_linear_relu_fwd": [c_p, c_int, c_int, c_p, c_p, c_int, c_p, c_p],
     "ppo_fc_fwd": [c_p, c_int, c_p, c_p, c_int, c_p, c_int, c_p],
     "ppo_linear_dgrad_mask": [c_p, c_int, c_int, c_p, c_int, c_p, c_p, c_p],
     "ppo_conv3_dgrad": [c_p, c_int, c_p, c_p, c_p, c_p],
+    "ppo_conv3_dgrad_bits_ok": [],
+    "ppo_conv3_dgrad_bits": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv2_dgrad": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv2_dgrad_bits_ok": [],
     "ppo_conv2_dgrad_bits": [c_p, c_int, c_p, c_p, c_p, c_p],
@@ -95,7 +98,7 @@ _RESTYPES = {"ppo_last_error": ctypes.c_char_p, "ppo_packed_weights_size": c_ll}
 # functions whose int return value is a result, not a status
 _VALUE_FUNCS = {"ppo_abi_version", "ppo_gae_partials_count", "ppo_adv_diff_partials_count",
                 "ppo_packed_weights_size", "ppo_wgrad_splits", "ppo_heads_train_blocks", "ppo_grad_partials_count",
-                "ppo_conv2_dgrad_bits_ok"}
+                "ppo_conv2_dgrad_bits_ok", "ppo_conv3_dgrad_bits_ok"}
 
 _LIB = None
 

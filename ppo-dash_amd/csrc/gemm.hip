@@ -753,7 +753,8 @@ template <int NP>
 __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restrict__ a1, int B,
                                                           const uint16_t* __restrict__ wpl,
                                                           const float* __restrict__ bias,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out,
+                                                          uint16_t* __restrict__ mbits) {
   constexpr int CS = 544, PLU = 4 * CS, MT = 6, KS = 8, UNITS = 400 * 4, UPER = (UNITS + 511) / 512;
   constexpr int WN = 64 * 512;
   __shared__ __attribute__((aligned(16))) uint16_t S[3 * PLU * 8];   // 3 planes x 4 chunks x CS units x 8 bf16
@@ -860,7 +861,12 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restri
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = 16 * t + 4 * g + r;
-          if (m < 81) o[m * 64] = fmaxf(v[r] + bv, 0.f);
+          const float y = fmaxf(v[r] + bv, 0.f);
+          if (m < 81) o[m * 64] = y;
+          if (mbits) {   // ReLU mask bits: lane (g, i16) -> pixel m, channel 16 nt + i16
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(y > 0.f);
+            if (i16 == 0 && m < 81) mbits[((size_t)b * 81 + m) * 4 + nt] = (uint16_t)(bal >> (16 * g));
+          }
         }
       }
     }
@@ -1194,7 +1200,9 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
 // bytes (2 x 5,184 B): the next image is staged before the compute, one barrier
 // per image.  Wave w: ci tile w & 3 (weights, 9 taps x 3 planes, in 108 VGPRs),
 // row tiles 3 (w >> 2) .. +2.
-template <int NP>
+// BITS: the a2 ReLU mask comes as bits (a2 points at u64 words [B][81] from
+// ppo_conv2_fwd_mask: 648 B instead of 20.7 KB per image).
+template <int NP, bool BITS = false>
 __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __restrict__ dz3, int B,
                                                             const uint16_t* __restrict__ wpl,
                                                             const float* __restrict__ a2,
@@ -1229,17 +1237,22 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
     qrow[t] = g * CS + (y + 2) * GW + x + 2;
   }
   f32x4 stg[2];
-  f32x4 mst[MPER];
+  f32x4 mst[BITS ? 1 : MPER];
+  uint2 mbv;
   auto fetch = [&](int b) {
     if (tid < DU) {
       const f32x4* src = reinterpret_cast<const f32x4*>(dz3 + (size_t)b * 1568);
       stg[0] = src[2 * tid];
       stg[1] = src[2 * tid + 1];
     }
-    const f32x4* ms = reinterpret_cast<const f32x4*>(a2 + (size_t)b * 5184);
+    if constexpr (BITS) {
+      if (tid < 81) mbv = reinterpret_cast<const uint2*>(a2)[(size_t)b * 81 + tid];
+    } else {
+      const f32x4* ms = reinterpret_cast<const f32x4*>(a2 + (size_t)b * 5184);
 #pragma unroll
-    for (int j = 0; j < MPER; ++j)
-      if (tid + 512 * j < MC) mst[j] = ms[tid + 512 * j];
+      for (int j = 0; j < MPER; ++j)
+        if (tid + 512 * j < MC) mst[j] = ms[tid + 512 * j];
+    }
   };
   auto put = [&](int buf) {
     if (tid < DU) {   // unit tid: dz3 pixel tid >> 2, co chunk tid & 3
@@ -1251,12 +1264,16 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
       *reinterpret_cast<bf16x8*>(&S[buf][8 * (PLU + q)]) = f.m;
       *reinterpret_cast<bf16x8*>(&S[buf][8 * (2 * PLU + q)]) = f.l;
     }
+    if constexpr (BITS) {
+      if (tid < 81) reinterpret_cast<uint2*>(Mk[buf])[tid] = mbv;
+    } else {
 #pragma unroll
-    for (int j = 0; j < MPER; ++j) {
-      const int c = tid + 512 * j;
-      if (c < MC)
-        Mk[buf][c] = (mst[j][0] > 0.f ? 1u : 0u) | (mst[j][1] > 0.f ? 0x100u : 0u) |
-                     (mst[j][2] > 0.f ? 0x10000u : 0u) | (mst[j][3] > 0.f ? 0x1000000u : 0u);
+      for (int j = 0; j < MPER; ++j) {
+        const int c = tid + 512 * j;
+        if (c < MC)
+          Mk[buf][c] = (mst[j][0] > 0.f ? 1u : 0u) | (mst[j][1] > 0.f ? 0x100u : 0u) |
+                       (mst[j][2] > 0.f ? 0x10000u : 0u) | (mst[j][3] > 0.f ? 0x1000000u : 0u);
+      }
     }
   };
   __syncthreads();   // the zeroed pads
@@ -1313,7 +1330,10 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 16 * tl[t] + 4 * g + r;
-        if (m < 81) o[m * 64] = mk[m * 64 + ci] ? acc[t][r] : 0.f;
+        if (m < 81) {
+          const bool keep = BITS ? ((Mk[cur][2 * m + (ci >> 5)] >> (ci & 31)) & 1u) != 0 : mk[m * 64 + ci] != 0;
+          o[m * 64] = keep ? acc[t][r] : 0.f;
+        }
       }
     __syncthreads();   // every wave is done with stage cur; stage cur ^ 1 is complete
     cur ^= 1;
@@ -2113,7 +2133,32 @@ static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, lo
 #undef SETUP1
 }
 
+static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float* b2, float* out, uint16_t* mbits,
+                          void* stream);
+
 PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream) {
+  return conv2_fwd_impl(a1, B, w2p, b2, out, nullptr, stream);
+}
+
+// conv2 forward that also writes the ReLU mask of its output as bits
+// (mbits [B][81] u64, bit c of pixel p = out[p][c] > 0) for ppo_conv3_dgrad_bits.
+PPO_API int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const float* b2, float* out,
+                               uint64_t* mbits, void* stream) {
+  PPO_REQUIRE(mbits != nullptr, "ppo_conv2_fwd_mask: null mask");
+  return conv2_fwd_impl(a1, B, w2p, b2, out, reinterpret_cast<uint16_t*>(mbits), stream);
+}
+
+static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float* b2, float* out, uint16_t* mbits,
+                          void* stream) {
+  if (mbits && g_tune[TK_CONV2_FWD] != 8) {   // no fused mask epilogue: the conv, then the mask
+    const int rc = conv2_fwd_impl(a1, B, w2p, b2, out, nullptr, stream);
+    if (rc != 0 || B <= 0) return rc;
+    const long long halves = (long long)B * 81 * 4;
+    const long long nb = (halves + 255) / 256;
+    relu_bits_kernel<<<(unsigned)(nb < 8192 ? nb : 8192), 256, 0, as_stream(stream)>>>(out, halves, mbits);
+    PPO_LAUNCH_CHECK("relu_bits_kernel");
+    return 0;
+  }
   if (g_tune[TK_CONV2_FWD] == 10) {   // LDS-DMA staged
     if (B <= 0) return 0;
     const int n_cu = device_cus();
@@ -2131,7 +2176,7 @@ PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float*
     const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
     int slot;
     const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
-    PPO_LAUNCH_NP(conv2_fwd_x9_kernel, nb, 512, as_stream(stream), a1, B, planes_of(w2p, 64 * 512), b2, out);
+    PPO_LAUNCH_NP(conv2_fwd_x9_kernel, nb, 512, as_stream(stream), a1, B, planes_of(w2p, 64 * 512), b2, out, mbits);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
     PPO_LAUNCH_CHECK("conv2_fwd_x9_kernel");
     return 0;
@@ -2321,18 +2366,33 @@ PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt
   return launch(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);
 }
 
+template <bool BITS>
+static int conv3_dgrad_img(const float* dz3, int B, const float* w3d, const float* mask, float* dz2, void* stream) {
+  if (B <= 0) return 0;
+  const int n_cu = device_cus();
+  const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+  int slot;
+  const bool prof = ppo_prof_begin("conv3_dgrad", as_stream(stream), &slot);
+  const uint16_t* wpl = planes_of(w3d, 64 * 288);
+  if (g_products == 9) conv3_dgrad_x9_kernel<9, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2);
+  else conv3_dgrad_x9_kernel<6, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2);
+  if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
+  PPO_LAUNCH_CHECK("conv3_dgrad_x9_kernel");
+  return 0;
+}
+
+// conv3 dgrad with conv2's ReLU mask as bits (m2bits [B][81] u64 from
+// ppo_conv2_fwd_mask); the image-resident kernel only (ppo_conv3_dgrad_bits_ok).
+PPO_API int ppo_conv3_dgrad_bits_ok() { return g_tune[TK_CONV3_DGRAD] == 8 ? 1 : 0; }
+PPO_API int ppo_conv3_dgrad_bits(const float* dz3, int B, const float* w3d, const uint64_t* m2bits, float* dz2,
+                                 void* stream) {
+  PPO_REQUIRE(ppo_conv3_dgrad_bits_ok(), "ppo_conv3_dgrad_bits: needs the image-resident kernel (tune 8)");
+  PPO_REQUIRE(m2bits != nullptr, "ppo_conv3_dgrad_bits: null mask");
+  return conv3_dgrad_img<true>(dz3, B, w3d, reinterpret_cast<const float*>(m2bits), dz2, stream);
+}
+
 PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream) {
-  if (g_tune[TK_CONV3_DGRAD] == 8) {
-    if (B <= 0) return 0;
-    const int n_cu = device_cus();
-    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
-    int slot;
-    const bool prof = ppo_prof_begin("conv3_dgrad", as_stream(stream), &slot);
-    PPO_LAUNCH_NP(conv3_dgrad_x9_kernel, nb, 512, as_stream(stream), dz3, B, planes_of(w3d, 64 * 288), a2, dz2);
-    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
-    PPO_LAUNCH_CHECK("conv3_dgrad_x9_kernel");
-    return 0;
-  }
+  if (g_tune[TK_CONV3_DGRAD] == 8) return conv3_dgrad_img<false>(dz3, B, w3d, a2, dz2, stream);
   if (use_x9_all()) {
     ConvDgradS1<9, 64, 3, 7, 32, XP64> p;
     p.dy = dz3; p.wd = w3d; p.act = a2; p.dx = dz2; p.M = B * 81;

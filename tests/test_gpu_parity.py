@@ -850,6 +850,45 @@ def test_conv1_mask_bits_and_conv2_dgrad_bits(gpu, conv1_variant):
     assert torch.equal(d_ref, d_bits)
 
 
+@pytest.mark.parametrize("conv2_variant", [8, 0])
+def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu, conv2_variant):
+    """ppo_conv2_fwd_mask (fused ballot epilogue: variant 8; conv + relu_bits
+    kernel: variant 0) writes bit c of word p = (a2[p][c] > 0) of its own fp32
+    output, with a2 identical to ppo_conv2_fwd's; conv3 dgrad fed those bits
+    (ppo_conv3_dgrad_bits) equals the fp32-mask kernel bit for bit.  B = 300."""
+    Hh = _hip()
+    B = 300
+    _, _, pk = _packed(gpu, 64, 41)
+    g = torch.Generator().manual_seed(42)
+    a1 = torch.relu(torch.randn(B, 20, 20, 32, generator=g)).cuda()
+    b2 = (torch.randn(64, generator=g) * 0.1).cuda()
+    a2 = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
+    a2m = torch.full_like(a2, float("nan"))
+    bits = torch.zeros(B * 81, dtype=torch.int64, device=gpu)
+    Hh.call("ppo_tune_set", b"conv2_fwd", conv2_variant)
+    try:
+        Hh.call("ppo_conv2_fwd", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2.data_ptr(), _s())
+        Hh.call("ppo_conv2_fwd_mask", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2m.data_ptr(), bits.data_ptr(), _s())
+        torch.cuda.synchronize()
+    finally:
+        Hh.call("ppo_tune_set", b"conv2_fwd", 8)
+    assert torch.equal(a2, a2m)
+    live = (a2 > 0).reshape(B * 81, 64).cpu()
+    got = bits.cpu()
+    for h in range(2):   # 32-bit halves (int64 arithmetic cannot hold bit 63 unsigned)
+        want = (live[:, 32 * h:32 * h + 32].to(torch.int64) << torch.arange(32, dtype=torch.int64)).sum(1)
+        assert torch.equal((got >> (32 * h)) & 0xFFFFFFFF, want)
+    assert 0.2 < live.float().mean().item() < 0.8
+    dz3 = torch.randn(B, 7, 7, 32, generator=g).cuda()
+    d_ref = torch.full_like(a2, float("nan"))
+    d_bits = torch.full_like(a2, float("nan"))
+    Hh.call("ppo_conv3_dgrad", dz3.data_ptr(), B, pk[4], a2.data_ptr(), d_ref.data_ptr(), _s())
+    assert Hh.call("ppo_conv3_dgrad_bits_ok") == 1
+    Hh.call("ppo_conv3_dgrad_bits", dz3.data_ptr(), B, pk[4], bits.data_ptr(), d_bits.data_ptr(), _s())
+    torch.cuda.synchronize()
+    assert torch.equal(d_ref, d_bits)
+
+
 @pytest.mark.parametrize("variant", [0, 8, 10])
 def test_conv2_fwd_variants_vs_torch(gpu, variant):
     """conv2 forward (4x4 stride 2, 20x20x32 -> 9x9x64, bias + ReLU): the split-bf16
