@@ -106,9 +106,6 @@ int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const float* b2
                        void* stream);
 /* model.py:179 Conv2d(64,32,3,s1)+ReLU */
 int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream);
-/* the same, also writing its ReLU mask as bits (mbits [B][49] u32: bit c of pixel p = out[p][c] > 0) */
-int ppo_conv3_fwd_mask(const float* a2, int B, const float* w3p, const float* b3, float* out, uint32_t* mbits,
-                       void* stream);
 /* model.py:180 Linear(1568,H)+ReLU (generic Linear+ReLU) */
 /* model.py:181 CNNBase fc + ReLU from the packed W4p segment (ppo_pack_weights; its bf16 planes follow it):
  * out[m * ldo + n] = relu(x[m] · W4p[n] + b[n]), x [M][1568] (p, c) order */
@@ -128,10 +125,6 @@ int ppo_transpose(const float* src, int rows, int cols, float* dst, void* stream
 /* algo/ppo.py:80-81 loss.backward() through the trunk: dgrad with the ReLU mask
  * of the layer below fused, wgrad as split-K partial slabs + deterministic reduce */
 int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
-                          void* stream);
-/* the same with the mask as bits (bits [M][N/32] u32, bit n & 31 of word n >> 5; N % 32 == 0):
- * the fc dgrad with conv3's mask from ppo_conv3_fwd_mask (196 B instead of 6.3 KB per row) */
-int ppo_linear_dgrad_bits(const float* dy, int M, int K, const float* wt, int N, const uint32_t* bits, float* dx,
                           void* stream);
 int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream);
 /* conv3 dgrad with conv2's ReLU mask as bits (from ppo_conv2_fwd_mask): 648 B instead of

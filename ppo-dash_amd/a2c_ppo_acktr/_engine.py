@@ -142,23 +142,20 @@ class CNNEngine:
             out, ldo = ws.get("h", B * self.H, device=dev), self.H
         s = stream()
         if ws is self.ws["train"]:
-            # training forward: conv1..conv3 also write their ReLU masks as bits, read
-            # by the conv2 / conv3 / fc dgrads instead of the fp32 activations
+            # training forward: conv1 and conv2 also write their ReLU masks as bits,
+            # read by the conv2 / conv3 dgrads instead of the fp32 activations
             m1 = ws.get("m1bits", B * 400, dtype=torch.int32, device=dev)
             m2 = ws.get("m2bits", B * 81, dtype=torch.int64, device=dev)
-            m3 = ws.get("m3bits", B * 49, dtype=torch.int32, device=dev)
             call("ppo_conv1_fwd_mask", obs.data_ptr(), is_u8, ptr(idx, torch.int64, "idx"), 0, self.C, B,
                  self.pv(self.W1), self.pv(self.B1), a1.data_ptr(), m1.data_ptr(), s)
             call("ppo_conv2_fwd_mask", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), m2.data_ptr(),
-                 s)
-            call("ppo_conv3_fwd_mask", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), m3.data_ptr(),
                  s)
             self._mask_rows = B
         else:
             call("ppo_conv1_fwd", obs.data_ptr(), is_u8, ptr(idx, torch.int64, "idx"), 0, self.C, B,
                  self.pv(self.W1), self.pv(self.B1), a1.data_ptr(), s)
             call("ppo_conv2_fwd", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), s)
-            call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
+        call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
         call("ppo_fc_fwd", a3.data_ptr(), B, self.pk(2), self.pv(self.B4), self.H, out.data_ptr(), ldo, s)
         return out
 
@@ -227,14 +224,9 @@ class CNNEngine:
         dz3 = ws.get("dz3", B * FEAT, device=dev)
         dz2 = ws.get("dz2", B * 81 * 64, device=dev)
         dz1 = ws.get("dz1", B * 400 * 32, device=dev)
-        bits = getattr(self, "_mask_rows", None) == B   # masks of this minibatch's forward
-        if bits:
-            call("ppo_linear_dgrad_bits", dh.data_ptr(), B, self.H, self.pk(3), FEAT, ws.bufs["m3bits"].data_ptr(),
-                 dz3.data_ptr(), s)
-        else:
-            call("ppo_linear_dgrad_mask", dh.data_ptr(), B, self.H, self.pk(3), FEAT, a3.data_ptr(), dz3.data_ptr(),
-                 s)
+        call("ppo_linear_dgrad_mask", dh.data_ptr(), B, self.H, self.pk(3), FEAT, a3.data_ptr(), dz3.data_ptr(), s)
         self._wgrad("fc", B, dh, a3, None, s)
+        bits = getattr(self, "_mask_rows", None) == B   # masks of this minibatch's forward
         if bits and call("ppo_conv3_dgrad_bits_ok"):
             call("ppo_conv3_dgrad_bits", dz3.data_ptr(), B, self.pk(4), ws.bufs["m2bits"].data_ptr(), dz2.data_ptr(),
                  s)

@@ -46,11 +46,9 @@ SIGNATURES = {
     "ppo_conv2_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv2_fwd_mask": [c_p, c_int, c_p, c_p, c_p, c_p, c_p],
     "ppo_conv3_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],
-    "ppo_conv3_fwd_mask": [c_p, c_int, c_p, c_p, c_p, c_p, c_p],
     "ppo_linear_relu_fwd": [c_p, c_int, c_int, c_p, c_p, c_int, c_p, c_p],
     "ppo_fc_fwd": [c_p, c_int, c_p, c_p, c_int, c_p, c_int, c_p],
     "ppo_linear_dgrad_mask": [c_p, c_int, c_int, c_p, c_int, c_p, c_p, c_p],
-    "ppo_linear_dgrad_bits": [c_p, c_int, c_int, c_p, c_int, c_p, c_p, c_p],
     "ppo_conv3_dgrad": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv3_dgrad_bits_ok": [],
     "ppo_conv3_dgrad_bits": [c_p, c_int, c_p, c_p, c_p, c_p],

@@ -1355,8 +1355,7 @@ template <int NP>
 __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restrict__ a2, int B,
                                                           const uint16_t* __restrict__ wpl,
                                                           const float* __restrict__ bias,
-                                                          float* __restrict__ out,
-                                                          uint16_t* __restrict__ mbits) {
+                                                          float* __restrict__ out) {
   constexpr int NPX = 84, PL = NPX * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, UPER = (UNITS + 511) / 512;
   __shared__ __attribute__((aligned(16))) uint16_t S[2][3 * PL];
   __shared__ __attribute__((aligned(16))) f32x4 R[2][2][2][2][64];   // [stage][co tile][row half][tile][lane]
@@ -1441,13 +1440,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = 16 * (2 * mh + u) + 4 * g + r, oy = m / 9, ox = m - 9 * oy;
-          const float y = fmaxf(v[r] + bv, 0.f);
-          if (ox < 7 && oy < 7) o[(7 * oy + ox) * 32] = y;
-          if (mbits) {   // ReLU mask bits: lane (g, i16) -> pixel 7 oy + ox, channel 16 nt + i16
-            const uint64_t bal = __builtin_amdgcn_ballot_w64(y > 0.f);
-            if (i16 == 0 && ox < 7 && oy < 7)
-              mbits[((size_t)b * 49 + 7 * oy + ox) * 2 + nt] = (uint16_t)(bal >> (16 * g));
-          }
+          if (ox < 7 && oy < 7) o[(7 * oy + ox) * 32] = fmaxf(v[r] + bv, 0.f);
         }
       }
     }
@@ -2201,39 +2194,14 @@ static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float*
 #undef T2
 }
 
-static int conv3_fwd_impl(const float* a2, int B, const float* w3p, const float* b3, float* out, uint16_t* mbits,
-                          void* stream);
-
 PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream) {
-  return conv3_fwd_impl(a2, B, w3p, b3, out, nullptr, stream);
-}
-
-// conv3 forward that also writes the ReLU mask of its output as bits
-// (mbits [B][49] u32, bit c of pixel p = out[p][c] > 0) for ppo_linear_dgrad_bits.
-PPO_API int ppo_conv3_fwd_mask(const float* a2, int B, const float* w3p, const float* b3, float* out,
-                               uint32_t* mbits, void* stream) {
-  PPO_REQUIRE(mbits != nullptr, "ppo_conv3_fwd_mask: null mask");
-  return conv3_fwd_impl(a2, B, w3p, b3, out, reinterpret_cast<uint16_t*>(mbits), stream);
-}
-
-static int conv3_fwd_impl(const float* a2, int B, const float* w3p, const float* b3, float* out, uint16_t* mbits,
-                          void* stream) {
-  if (mbits && g_tune[TK_CONV3_FWD] != 8) {   // no fused mask epilogue: the conv, then the mask
-    const int rc = conv3_fwd_impl(a2, B, w3p, b3, out, nullptr, stream);
-    if (rc != 0 || B <= 0) return rc;
-    const long long halves = (long long)B * 49 * 2;
-    const long long nb = (halves + 255) / 256;
-    relu_bits_kernel<<<(unsigned)(nb < 8192 ? nb : 8192), 256, 0, as_stream(stream)>>>(out, halves, mbits);
-    PPO_LAUNCH_CHECK("relu_bits_kernel");
-    return 0;
-  }
   if (g_tune[TK_CONV3_FWD] == 8) {
     if (B <= 0) return 0;
     const int n_cu = device_cus();
     const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
     int slot;
     const bool prof = ppo_prof_begin("conv3_fwd", as_stream(stream), &slot);
-    PPO_LAUNCH_NP(conv3_fwd_x9_kernel, nb, 512, as_stream(stream), a2, B, planes_of(w3p, 32 * 576), b3, out, mbits);
+    PPO_LAUNCH_NP(conv3_fwd_x9_kernel, nb, 512, as_stream(stream), a2, B, planes_of(w3p, 32 * 576), b3, out);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
     PPO_LAUNCH_CHECK("conv3_fwd_x9_kernel");
     return 0;
@@ -2369,23 +2337,8 @@ PPO_API int ppo_transpose(const float* src, int rows, int cols, float* dst, void
 }
 
 // dx [M][N] = (act > 0) * (dy [M][K] · wt [N][K]^T)
-static int linear_dgrad_mask_impl(const float* dy, int M, int K, const float* wt, int N, const float* act,
-                                  int mode, float* dx, void* stream);
-
 PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
                                   void* stream) {
-  return linear_dgrad_mask_impl(dy, M, K, wt, N, act, 1, dx, stream);
-}
-
-// the same with the ReLU mask as bits (bits [M][N/32] u32, from ppo_conv3_fwd_mask)
-PPO_API int ppo_linear_dgrad_bits(const float* dy, int M, int K, const float* wt, int N, const uint32_t* bits,
-                                  float* dx, void* stream) {
-  PPO_REQUIRE(N % 32 == 0 && bits != nullptr, "ppo_linear_dgrad_bits: N=%d (multiple of 32), bits required", N);
-  return linear_dgrad_mask_impl(dy, M, K, wt, N, reinterpret_cast<const float*>(bits), 3, dx, stream);
-}
-
-static int linear_dgrad_mask_impl(const float* dy, int M, int K, const float* wt, int N, const float* act,
-                                  int mode, float* dx, void* stream) {
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 4", K);
   if (use_x9()) {   // wt = the packed W4T segment [1568][H] (planes follow)
     PPO_REQUIRE(K % 8 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 8", K);
@@ -2393,7 +2346,6 @@ static int linear_dgrad_mask_impl(const float* dy, int M, int K, const float* wt
   {                                                                                 \
     DenseDgradMask<CFG> p;                                                          \
     p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;        \
-    p.mode = mode;                                                                  \
     set_planes(p, wt, (long long)N * K, N, K);                                      \
     return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K); \
   }
@@ -2410,7 +2362,7 @@ static int linear_dgrad_mask_impl(const float* dy, int M, int K, const float* wt
 #undef PPO_FCD
   }
   DenseDgradMask<CfgN128> p;
-  p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K; p.mode = mode;
+  p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;
   return launch(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);
 }
 

@@ -350,8 +350,7 @@ template <class C_>
 struct DenseDgradMask : C_ {
   const float* dy; const float* wt; const float* act; float* dx; int M, N, K;
   int ldact = 0;   // act row stride (0: N); act NULL: no mask
-  int mode = 1;    // 1: ReLU mask (act > 0), 2: tanh derivative (1 - act²),
-                   // 3: ReLU mask as bits (act = u32 words [M][N/32], bit n & 31 of word n >> 5)
+  int mode = 1;    // 1: ReLU mask (act > 0), 2: tanh derivative (1 - act²)
   using ACtx = typename C_::ACtx;
   using BCtx = typename C_::BCtx;
   __device__ ACtx a_ctx(int m, int) const { return {dy + (size_t)m * K, 0, 0, m < M}; }
@@ -368,9 +367,6 @@ struct DenseDgradMask : C_ {
       const size_t i = (size_t)m * N + n;
       if (!act) {
         dx[i] = v;
-      } else if (mode == 3) {
-        const uint32_t w = reinterpret_cast<const uint32_t*>(act)[(size_t)m * (N >> 5) + (n >> 5)];
-        dx[i] = ((w >> (n & 31)) & 1u) ? v : 0.f;
       } else {
         const float y = act[(size_t)m * (ldact ? ldact : N) + n];
         dx[i] = mode == 2 ? v * (1.0f - y * y) : (y > 0.f ? v : 0.f);

@@ -889,42 +889,6 @@ def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu, conv2_variant):
     assert torch.equal(d_ref, d_bits)
 
 
-@pytest.mark.parametrize("conv3_variant", [8, 0])
-def test_conv3_mask_bits_and_fc_dgrad_bits(gpu, conv3_variant):
-    """ppo_conv3_fwd_mask (fused ballot epilogue: variant 8; conv + relu_bits
-    kernel: variant 0) writes bit c of word p = (a3[p][c] > 0), with a3 identical
-    to ppo_conv3_fwd's; the fc dgrad fed those bits (ppo_linear_dgrad_bits)
-    equals the fp32-mask dgrad bit for bit.  B = 300, H = 64."""
-    Hh = _hip()
-    B, H = 300, 64
-    _, packed, pk = _packed(gpu, H, 51)   # keep the packed buffer alive
-    g = torch.Generator().manual_seed(52)
-    a2 = torch.relu(torch.randn(B, 9, 9, 64, generator=g)).cuda()
-    b3 = (torch.randn(32, generator=g) * 0.1).cuda()
-    a3 = torch.full((B, 7, 7, 32), float("nan"), device=gpu)
-    a3m = torch.full_like(a3, float("nan"))
-    bits = torch.zeros(B * 49, dtype=torch.int32, device=gpu)
-    Hh.call("ppo_tune_set", b"conv3_fwd", conv3_variant)
-    try:
-        Hh.call("ppo_conv3_fwd", a2.data_ptr(), B, pk[1], b3.data_ptr(), a3.data_ptr(), _s())
-        Hh.call("ppo_conv3_fwd_mask", a2.data_ptr(), B, pk[1], b3.data_ptr(), a3m.data_ptr(), bits.data_ptr(), _s())
-        torch.cuda.synchronize()
-    finally:
-        Hh.call("ppo_tune_set", b"conv3_fwd", 8)
-    assert torch.equal(a3, a3m)
-    live = (a3 > 0).reshape(B * 49, 32).cpu().to(torch.int64)
-    want = (live << torch.arange(32, dtype=torch.int64)).sum(1)
-    assert torch.equal(bits.cpu().to(torch.int64) & 0xFFFFFFFF, want)
-    assert 0.2 < live.float().mean().item() < 0.8
-    dh = torch.randn(B, H, generator=g).cuda()
-    d_ref = torch.full((B, 1568), float("nan"), device=gpu)
-    d_bits = torch.full_like(d_ref, float("nan"))
-    Hh.call("ppo_linear_dgrad_mask", dh.data_ptr(), B, H, pk[3], 1568, a3.data_ptr(), d_ref.data_ptr(), _s())
-    Hh.call("ppo_linear_dgrad_bits", dh.data_ptr(), B, H, pk[3], 1568, bits.data_ptr(), d_bits.data_ptr(), _s())
-    torch.cuda.synchronize()
-    assert torch.equal(d_ref, d_bits)
-
-
 @pytest.mark.parametrize("variant", [0, 8, 10])
 def test_conv2_fwd_variants_vs_torch(gpu, variant):
     """conv2 forward (4x4 stride 2, 20x20x32 -> 9x9x64, bias + ReLU): the split-bf16

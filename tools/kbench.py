@@ -50,9 +50,8 @@ def main():
     s = torch.cuda.current_stream().cuda_stream
     call("ppo_pack_weights", w2.data_ptr(), w3.data_ptr(), w4.data_ptr(), H, packed.data_ptr(), s)
     a1 = torch.empty(B * 400 * 32, device=dev)
-    m1 = torch.empty(B * 400, dtype=torch.int32, device=dev)   # ReLU mask bits of a1, a2, a3
+    m1 = torch.empty(B * 400, dtype=torch.int32, device=dev)   # ReLU mask bits of a1, a2
     m2 = torch.empty(B * 81, dtype=torch.int64, device=dev)
-    m3 = torch.empty(B * 49, dtype=torch.int32, device=dev)
     a2 = torch.empty(B * 81 * 64, device=dev)
     a3 = torch.empty(B * 1568, device=dev)
     h = torch.empty(B * H, device=dev)
@@ -94,17 +93,13 @@ def main():
                                      slab_b.data_ptr(), s), 2.0 * B * 49 * 32 * 576),
         "conv2_dgrad": (lambda: call("ppo_conv2_dgrad", dz2.data_ptr(), B, pk[5], a1.data_ptr(), dz1.data_ptr(), s),
                         2.0 * B * 81 * 64 * 512),
-        # the training-forward variants that also write ReLU mask bits, and the
-        # dgrads that read the bits instead of the fp32 activations
+        # training-forward variants that also write ReLU mask bits, and the dgrads
+        # that read the bits instead of the fp32 activations (the engine's path)
         "conv1_fwd_mask": (lambda: call("ppo_conv1_fwd_mask", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B,
                                         w1.data_ptr(), b1.data_ptr(), a1.data_ptr(), m1.data_ptr(), s),
                            2.0 * B * 400 * 32 * 256),
         "conv2_fwd_mask": (lambda: call("ppo_conv2_fwd_mask", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2.data_ptr(),
                                         m2.data_ptr(), s), 2.0 * B * 81 * 64 * 512),
-        "conv3_fwd_mask": (lambda: call("ppo_conv3_fwd_mask", a2.data_ptr(), B, pk[1], b3.data_ptr(), a3.data_ptr(),
-                                        m3.data_ptr(), s), 2.0 * B * 49 * 32 * 576),
-        "fc_dgrad_bits": (lambda: call("ppo_linear_dgrad_bits", dh.data_ptr(), B, H, pk[3], 1568, m3.data_ptr(),
-                                       dz3.data_ptr(), s), 2.0 * B * 1568 * H),
         "conv3_dgrad_bits": (lambda: call("ppo_conv3_dgrad_bits", dz3.data_ptr(), B, pk[4], m2.data_ptr(),
                                           dz2.data_ptr(), s), 2.0 * B * 49 * 32 * 576),
         "conv2_dgrad_bits": (lambda: call("ppo_conv2_dgrad_bits", dz2.data_ptr(), B, pk[5], m1.data_ptr(),
@@ -117,9 +112,7 @@ def main():
                                        gw.data_ptr(), gb.data_ptr(), 1.0 / 255, 0, s), 0.0),
     }
     # realistic activations for the backward kernels
-    K["conv1_fwd"][0](); K["conv2_fwd"][0](); K["conv3_fwd"][0](); K["fc_fwd"][0]()
-    if any("mask" in x or "bits" in x for x in a.only.split(",")):
-        K["conv1_fwd_mask"][0](); K["conv2_fwd_mask"][0](); K["conv3_fwd_mask"][0]()
+    K["conv1_fwd_mask"][0](); K["conv2_fwd_mask"][0](); K["conv3_fwd"][0](); K["fc_fwd"][0]()
     K["fc_dgrad"][0](); K["conv3_dgrad"][0](); K["conv2_dgrad"][0]()
     torch.cuda.synchronize()
     only = [x for x in a.only.split(",") if x]
