@@ -261,9 +261,13 @@ def pmc_mfma(workload):
         return {}, None
     out = {}
     for name, sym in PMC_SYMBOL.items():
-        for k, v in m["kernels"].items():
-            if k.startswith(sym):
-                out[name] = v["mfma_util"]
+        # all instantiations (e.g. the rollout and the mask-writing training
+        # forward): busy cycles are proportional to MFMA instructions, so the
+        # combined utilisation is Σ insts / Σ (insts / util)
+        parts = [(v["mfma_insts_per_launch"] * v["launches"], v["mfma_util"])
+                 for k, v in m["kernels"].items() if k.startswith(sym) and v["mfma_util"] > 0]
+        if parts:
+            out[name] = round(sum(w for w, _ in parts) / sum(w / u for w, u in parts), 4)
     return out, d["mfma_util_file"]
 
 

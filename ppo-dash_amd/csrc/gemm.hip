@@ -159,7 +159,7 @@ __global__ __launch_bounds__(512) void conv1_fwd_img_kernel(const uint8_t* __res
 // of 16 output pixels.  k-step s covers k = 32s + [0, 32); lane group
 // g = lane >> 4 supplies k = 32s + 8g + j, j = 0..7 — one kx row of the patch,
 // 8 adjacent pixels, so an A fragment is one 16-byte LDS read.
-template <int C>
+template <int C, bool MASK>   // MASK: also write the ReLU mask bits (training forward)
 __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __restrict__ obs,
                                                                const int64_t* __restrict__ idx, long long row0,
                                                                int B, const float* __restrict__ w,
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
         for (int r = 0; r < 4; ++r) {
           const float v = fmaxf(acc[t][r] * (1.0f / 255.0f) + bv, 0.f);
           o[(rt * 16 + 4 * g + r) * 32] = v;
-          if (mbits) {   // ReLU mask bits: lane (g, i16) -> pixel 16 rt + 4g + r, channel 16 ct + i16
+          if constexpr (MASK) {   // ReLU mask bits: lane (g, i16) -> pixel 16 rt + 4g + r, channel 16 ct + i16
             const uint64_t bal = __builtin_amdgcn_ballot_w64(v > 0.f);
             if (i16 == 0) mbits[((size_t)b * 400 + rt * 16 + 4 * g + r) * 2 + ct] = (uint16_t)(bal >> (16 * g));
           }
@@ -749,7 +749,7 @@ struct Conv2Dgrad : C_ {
 //   Wave w: n tile w & 3 (16 co), taps 8 (w >> 2) .. +7 (ky rows 0-1 / 2-3);
 //   its weight fragments (pre-split planes) in 96 VGPRs.  The two K halves are
 //   summed through LDS (half 1 writes, half 0 adds and stores).
-template <int NP>
+template <int NP, bool MASK = false>   // MASK: also write the ReLU mask bits (training forward)
 __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restrict__ a1, int B,
                                                           const uint16_t* __restrict__ wpl,
                                                           const float* __restrict__ bias,
@@ -863,7 +863,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restri
           const int m = 16 * t + 4 * g + r;
           const float y = fmaxf(v[r] + bv, 0.f);
           if (m < 81) o[m * 64] = y;
-          if (mbits) {   // ReLU mask bits: lane (g, i16) -> pixel m, channel 16 nt + i16
+          if constexpr (MASK) {   // ReLU mask bits: lane (g, i16) -> pixel m, channel 16 nt + i16
             const uint64_t bal = __builtin_amdgcn_ballot_w64(y > 0.f);
             if (i16 == 0 && m < 81) mbits[((size_t)b * 81 + m) * 4 + nt] = (uint16_t)(bal >> (16 * g));
           }
@@ -2115,8 +2115,12 @@ static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, lo
       conv1_fwd_img_kernel<4><<<blocks, 512, 0, as_stream(stream)>>>((const uint8_t*)obs, idx, row0, B, w1, b1, out);
     } else {
       const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
-      conv1_fwd_bf16x3_kernel<4><<<nb, 512, 0, as_stream(stream)>>>((const uint8_t*)obs, idx, row0, B, w1, b1, out,
-                                                                      mbits);
+      if (mbits)
+        conv1_fwd_bf16x3_kernel<4, true><<<nb, 512, 0, as_stream(stream)>>>((const uint8_t*)obs, idx, row0, B, w1,
+                                                                            b1, out, mbits);
+      else
+        conv1_fwd_bf16x3_kernel<4, false><<<nb, 512, 0, as_stream(stream)>>>((const uint8_t*)obs, idx, row0, B, w1,
+                                                                             b1, out, nullptr);
     }
     if (prof) ppo_prof_end(slot, as_stream(stream), fl);
     PPO_LAUNCH_CHECK("conv1_fwd_u8 (image-resident)");
@@ -2176,7 +2180,13 @@ static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float*
     const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
     int slot;
     const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
-    PPO_LAUNCH_NP(conv2_fwd_x9_kernel, nb, 512, as_stream(stream), a1, B, planes_of(w2p, 64 * 512), b2, out, mbits);
+    const uint16_t* wpl = planes_of(w2p, 64 * 512);
+    if (mbits && g_products == 9)
+      conv2_fwd_x9_kernel<9, true><<<nb, 512, 0, as_stream(stream)>>>(a1, B, wpl, b2, out, mbits);
+    else if (mbits)
+      conv2_fwd_x9_kernel<6, true><<<nb, 512, 0, as_stream(stream)>>>(a1, B, wpl, b2, out, mbits);
+    else
+      PPO_LAUNCH_NP(conv2_fwd_x9_kernel, nb, 512, as_stream(stream), a1, B, wpl, b2, out, nullptr);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
     PPO_LAUNCH_CHECK("conv2_fwd_x9_kernel");
     return 0;

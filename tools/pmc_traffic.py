@@ -62,11 +62,14 @@ def main():
     open(os.path.join(prof, f"{tag}_bench.json"), "w").write(line)
     fetch, nf = per_launch(os.path.join(OUT, "pmcb", "fetch_counter_collection.csv"), "FETCH_SIZE", sub)
     write, nw = per_launch(os.path.join(OUT, "pmcb", "write_counter_collection.csv"), "WRITE_SIZE", sub)
-    avg_ms = None
+    # every instantiation of the kernel (e.g. the rollout and the mask-writing
+    # training forward) together: the launch mix bench.py's events time
+    tot_ns, calls = 0.0, 0
     for r in csv.DictReader(open(os.path.join(OUT, "prof", "run_kernel_stats.csv"))):
         if sub in r["Name"]:
-            avg_ms = float(r["AverageNs"]) / 1e6
-            calls = int(r["Calls"])
+            tot_ns += float(r["TotalDurationNs"])
+            calls += int(r["Calls"])
+    avg_ms = tot_ns / calls / 1e6 if calls else None
     rd = 2.0 * fetch * 1024
     wr = write * 1024
     out = {"kernel": bench_kernel, "kernel_match": sub, "launches_fetch_pass": nf, "launches_write_pass": nw,
