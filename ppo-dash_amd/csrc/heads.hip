@@ -199,21 +199,48 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
   float s_vl = 0.f, s_al = 0.f, s_ent = 0.f;
   const float clip = a.clip;
   const long long r0 = ((long long)blockIdx.x * HW + wave) * a.rows_per_wave;
+  // The per-row storage scalars (the minibatch gather idx -> action, advantage,
+  // old log-prob, value, return) of all of this wave's rows are fetched up
+  // front, lane j holding row r0 + j (rows_per_wave <= 64), and broadcast with
+  // readlane per row; each row's features are loaded one row ahead.  Without
+  // this the wave waited on two dependent loads per row (latency-bound).
+  int q_act = 0;
+  float q_adv = 0.f, q_olp = 0.f, q_vo = 0.f, q_ret = 0.f;
+  if (lane < a.rows_per_wave && r0 + lane < a.B) {
+    const long long sr = a.idx ? (long long)a.idx[r0 + lane] : a.row0 + r0 + lane;
+    q_act = (int)a.actions[sr];
+    q_adv = a.adv[sr];
+    q_olp = a.old_logp[sr];
+    q_vo = a.vpred[sr];
+    q_ret = a.ret[sr];
+  }
+  auto bcast = [](float x, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j));
+  };
+  float fn[HC], fvn[HC];
+  auto load_row = [&](long long row) {
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+      const bool in = row < a.B && lane + 64 * c < H;
+      fn[c] = in ? a.feat[row * H + lane + 64 * c] : 0.f;
+      fvn[c] = a.feat_v ? (in ? a.feat_v[row * H + lane + 64 * c] : 0.f) : fn[c];
+    }
+  };
+  load_row(r0);
   for (int rr = 0; rr < a.rows_per_wave; ++rr) {
     const long long row = r0 + rr;
     if (row >= a.B) break;
     float f[HC], fv[HC];
 #pragma unroll
     for (int c = 0; c < HC; ++c) {
-      const bool in = lane + 64 * c < H;
-      f[c] = in ? a.feat[row * H + lane + 64 * c] : 0.f;
-      fv[c] = a.feat_v ? (in ? a.feat_v[row * H + lane + 64 * c] : 0.f) : f[c];
+      f[c] = fn[c];
+      fv[c] = fvn[c];
     }
+    if (rr + 1 < a.rows_per_wave) load_row(row + 1);
     float value, z[AMAX], nl[AMAX], p[AMAX];
     head_dots(w, f, fv, value, z, b0, a.ba, A);
     categorical(z, A, nl, p);
-    const long long sr = a.idx ? (long long)a.idx[row] : a.row0 + row;
-    const int act = (int)a.actions[sr];
+    const int act = __builtin_amdgcn_readlane(q_act, rr);
     float lp = 0.f, ent = 0.f;
 #pragma unroll
     for (int o = 0; o < AMAX; ++o) {
@@ -221,8 +248,8 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
       if (o < A) ent -= nl[o] * p[o];
     }
     // action loss (ppo.py:61-66)
-    const float adv = a.adv[sr];
-    const float ratio = expf(lp - a.old_logp[sr]);
+    const float adv = bcast(q_adv, rr);
+    const float ratio = expf(lp - bcast(q_olp, rr));
     const float surr1 = ratio * adv;
     const float rc = fminf(fmaxf(ratio, 1.0f - clip), 1.0f + clip);
     const float surr2 = rc * adv;
@@ -230,7 +257,7 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
     const float inr = (ratio >= 1.0f - clip && ratio <= 1.0f + clip) ? 1.f : 0.f;
     const float g_logp = -a.inv_b * (w1 * adv + (1.f - w1) * adv * inr) * ratio;
     // value loss (ppo.py:68-77)
-    const float vo = a.vpred[sr], R = a.ret[sr];
+    const float vo = bcast(q_vo, rr), R = bcast(q_ret, rr);
     float g_v, vl_row;
     if (a.use_clipped_value_loss) {
       const float dv = value - vo;
