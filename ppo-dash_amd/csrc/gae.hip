@@ -109,112 +109,6 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
   }
 }
 
-// The same recurrence, four env lanes per thread (N % 4 == 0): every plane row
-// is read and written as 16-B vectors, 1 KB per wave instruction instead of
-// 256 B, which is what reaches the HBM rate on the 1M-lane roofline workload.
-// Per lane the arithmetic is the scalar kernel's, op for op (bit-identical).
-constexpr int GAE_U4 = 4;  // time steps prefetched per chunk
-
-template <bool USE_GAE, bool PTL, bool FUSE_ADV>
-__global__ __launch_bounds__(GAE_THREADS) void gae4_kernel(
-    const float* __restrict__ rewards, float* __restrict__ value_preds,
-    const float* __restrict__ masks, const float* __restrict__ bad_masks,
-    const float* __restrict__ next_value, float* __restrict__ returns,
-    float* __restrict__ adv, double* __restrict__ partials, int T, int N, float g, float gl) {
-  const int n4 = blockIdx.x * GAE_THREADS + threadIdx.x;
-  double s = 0.0, q = 0.0;
-  if (n4 < (N >> 2)) {
-    const size_t NN = (size_t)N, n = 4 * (size_t)n4;
-    auto ld = [&](const float* p, int t) { return *reinterpret_cast<const f32x4*>(p + (size_t)t * NN + n); };
-    auto st = [&](float* p, int t, const f32x4& v) { *reinterpret_cast<f32x4*>(p + (size_t)t * NN + n) = v; };
-    const f32x4 nv = *reinterpret_cast<const f32x4*>(next_value + n);
-    f32x4 carry, vnext = nv;
-    if (USE_GAE) {
-      st(value_preds, T, nv);   // storage.py:90/:108
-      carry = f32x4{0.f, 0.f, 0.f, 0.f};
-    } else {
-      st(returns, T, nv);       // storage.py:101/:118
-      carry = nv;
-    }
-    for (int t0 = T - 1; t0 >= 0; t0 -= GAE_U4) {
-      f32x4 rr[GAE_U4], vv[GAE_U4], mm[GAE_U4], bb[GAE_U4];
-#pragma unroll
-      for (int j = 0; j < GAE_U4; ++j) {
-        const int t = t0 - j;
-        if (t >= 0) {
-          rr[j] = ld(rewards, t);
-          mm[j] = ld(masks, t + 1);
-          vv[j] = (USE_GAE || PTL || FUSE_ADV) ? ld(value_preds, t) : f32x4{0.f, 0.f, 0.f, 0.f};
-          bb[j] = PTL ? ld(bad_masks, t + 1) : f32x4{1.f, 1.f, 1.f, 1.f};
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < GAE_U4; ++j) {
-        const int t = t0 - j;
-        if (t >= 0) {
-          f32x4 out;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (USE_GAE) {
-              float a = g * vnext[e];            // gamma * value_preds[t+1]
-              a = a * mm[j][e];                  //   * masks[t+1]
-              float delta = rr[j][e] + a;        // rewards[t] + ...
-              delta = delta - vv[j][e];          //   - value_preds[t]
-              float b = gl * mm[j][e];           // (gamma*gae_lambda) * masks[t+1]
-              b = b * carry[e];                  //   * gae
-              float c = delta + b;
-              if (PTL) c = c * bb[j][e];         // gae * bad_masks[t+1]
-              carry[e] = c;
-              out[e] = c + vv[j][e];             // returns[t] = gae + value_preds[t]
-            } else {
-              float x = carry[e] * g;            // returns[t+1] * gamma
-              x = x * mm[j][e];                  //   * masks[t+1]
-              x = x + rr[j][e];                  //   + rewards[t]
-              if (PTL) {
-                x = x * bb[j][e];
-                float keep = 1.0f - bb[j][e];
-                keep = keep * vv[j][e];
-                x = x + keep;
-              }
-              out[e] = x;
-              carry[e] = x;
-            }
-          }
-          if (USE_GAE) vnext = vv[j];
-          st(returns, t, out);
-          if (FUSE_ADV) {
-            f32x4 d;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              d[e] = out[e] - vv[j][e];          // returns[:-1] - value_preds[:-1]
-              s += (double)d[e];
-              q += (double)d[e] * (double)d[e];
-            }
-            st(adv, t, d);
-          }
-        }
-      }
-    }
-  }
-  if (FUSE_ADV) {
-    __shared__ double red[2][GAE_THREADS / 64];
-    s = wave_sum_d(s);
-    q = wave_sum_d(q);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[0][w] = s; red[1][w] = q; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double ss = 0.0, qq = 0.0;
-      for (int i = 0; i < GAE_THREADS / 64; ++i) { ss += red[0][i]; qq += red[1][i]; }
-      partials[2 * blockIdx.x] = ss;
-      partials[2 * blockIdx.x + 1] = qq;
-      // ppo_gae_partials_count(N) is the scalar kernel's block count: zero the rest
-      const int nparts = (N + GAE_THREADS - 1) / GAE_THREADS;
-      for (int i = gridDim.x + blockIdx.x; i < nparts; i += gridDim.x) partials[2 * i] = partials[2 * i + 1] = 0.0;
-    }
-  }
-}
-
 // adv = returns - value_preds over the first T rows, plus moment partials
 // (used when storage was modified after compute_returns).
 __global__ __launch_bounds__(256) void adv_diff_kernel(const float* __restrict__ returns,
@@ -285,14 +179,6 @@ __global__ __launch_bounds__(256) void adv_normalize_kernel(float* __restrict__ 
 template <bool G, bool P, bool F>
 int launch_gae(const float* r, float* v, const float* m, const float* bm, const float* nv, float* ret,
                float* adv, double* partials, int T, int N, float g, float gl, hipStream_t st) {
-  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (N % 4 == 0 && a16(r) && a16(v) && a16(m) && (!bm || a16(bm)) && a16(nv) && a16(ret) && (!adv || a16(adv))) {
-    // 16-B vectors: with 16-B aligned planes and N % 4 == 0 every row is aligned
-    gae4_kernel<G, P, F><<<ceil_div(N / 4, GAE_THREADS), GAE_THREADS, 0, st>>>(r, v, m, bm, nv, ret, adv, partials,
-                                                                             T, N, g, gl);
-    PPO_LAUNCH_CHECK("gae4_kernel");
-    return 0;
-  }
   gae_kernel<G, P, F><<<ceil_div(N, GAE_THREADS), GAE_THREADS, 0, st>>>(r, v, m, bm, nv, ret, adv, partials,
                                                                        T, N, g, gl);
   PPO_LAUNCH_CHECK("gae_kernel");
@@ -301,9 +187,6 @@ int launch_gae(const float* r, float* v, const float* m, const float* bm, const 
 
 }  // namespace
 
-// upper bound on the blocks of the GAE launch = moment partials it writes (the
-// scalar kernel's count; the 4-lane kernel writes ceil(N/4 / 256) of them and
-// zeroes the rest of this count, so a finalize over this count is exact)
 PPO_API int ppo_gae_partials_count(int N) { return (int)ceil_div(N, GAE_THREADS); }
 
 // storage.py:82-121 (+ ppo.py:35 when adv != NULL).  value_preds[T] is
