@@ -98,15 +98,18 @@ __device__ __forceinline__ float exp_noise(uint64_t seed, uint64_t counter, long
 }
 
 // act / evaluate: value, action (sample | mode | given), log_prob, entropy
-template <int HC, int AMAX>
+// FAST: A == AMAX, H == 64·HC, no separate critic features (compile-time bounds)
+template <int HC, int AMAX, bool FAST>
 __global__ __launch_bounds__(64 * HW) void heads_act_kernel(
-    const float* __restrict__ feat, const float* __restrict__ feat_v, int N, int H, const float* __restrict__ wc,
-    const float* __restrict__ bc, const float* __restrict__ wa, const float* __restrict__ ba, int A,
+    const float* __restrict__ feat, const float* __restrict__ feat_v_, int N, int H_, const float* __restrict__ wc,
+    const float* __restrict__ bc, const float* __restrict__ wa, const float* __restrict__ ba, int A_,
     const float* __restrict__ noise,
     unsigned long long seed, unsigned long long counter, int deterministic, const int64_t* __restrict__ given,
     float* __restrict__ value_out, int64_t* __restrict__ action_out, float* __restrict__ logp_out,
     float* __restrict__ ent_out, int rows_per_wave) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int H = FAST ? 64 * HC : H_, A = FAST ? AMAX : A_;
+  const float* const feat_v = FAST ? nullptr : feat_v_;
   HeadW<HC, AMAX> w;
   load_head_w(w, wc, wa, A, H, lane);
   const float b0 = bc[0];
@@ -406,7 +409,12 @@ int launch_act(const float* feat, const float* feat_v, int N, int H, const float
   // ~2048 waves in flight (8 per CU): a rollout batch of 4096 rows takes 2 per wave
   const int rpw = (int)std::min<long long>(8, std::max<long long>(1, ceil_div(N, 2048)));
   const unsigned blocks = ceil_div(N, HW * rpw);
-  heads_act_kernel<HC, AMAX><<<blocks, 64 * HW, 0, st>>>(feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter,
+  if (A == AMAX && H == 64 * HC && !feat_v)
+    heads_act_kernel<HC, AMAX, true><<<blocks, 64 * HW, 0, st>>>(feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter,
+                                                        det,
+                                                        given, v, act, lp, ent, rpw);
+  else
+    heads_act_kernel<HC, AMAX, false><<<blocks, 64 * HW, 0, st>>>(feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter,
                                                         det,
                                                         given, v, act, lp, ent, rpw);
   PPO_LAUNCH_CHECK("heads_act_kernel");
