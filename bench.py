@@ -9,18 +9,29 @@ One bench "step" = one whole T/run.py:168-248 iteration on every rank:
   [RCCL grad all-reduce] + clip + Adam), after_update.
 value = envs_per_gpu * 128 * world * K / max-over-ranks(wall time of K steps).
 
-Multi-GPU (launched by torch.distributed.run, one rank per GPU): env lanes are
-sharded (weak scaling); each minibatch's flat gradient is all-reduced over RCCL.
+Multi-GPU, one rank per GPU: env lanes are sharded (weak scaling); each
+minibatch's flat gradient is all-reduced over RCCL.  Either launched by
+torch.distributed.run (RANK / WORLD_SIZE in the environment; WORLD_SIZE must
+equal --gpus), or, with `--gpus N` and no launcher, this script starts the N
+ranks itself as child processes before anything touches the GPU.
 
 Also reported on rank 0:
   roofline      the dominant kernel's achieved FLOP/s from HIP events recorded
                 around each of its launches during the timed region
   gae_roofline  fused GAE + advantage kernel on a 1M-lane buffer (> Infinity Cache)
-  cpu_baseline  the oracle's numpy port of the reference CPU path, bounded sample
+  cpu_baseline  the reference's CPU path restated in torch (oracle/torch_ref.py:
+                F.conv2d / linear, autograd, torch.optim.Adam, clip_grad_norm_),
+                timed on a bounded sample at 1 thread (T/run.py:55) and at the
+                host's core share, CPU model named
+  kernel_rooflines  every HIP kernel family of the iteration with its own
+                roofline; the MFMA trunk kernels are event-timed inside the timed
+                region, the rest in one extra profiled iteration after it
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,32 +49,64 @@ PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA = vector peak (d
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 PEAK_HBM_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
-# The kernels timed with HIP events inside the timed region, and the roofline
-# that bounds each one.  "work" is algorithmic fp32 FLOP per
-# launch (2·M·N·K of the layer).  The split-bf16 kernels execute P bf16 part
-# products per fp32 product on the matrix cores — 3 with a u8 operand (exact in
-# bf16), 6 (default) or 9 (ppo_tune_set("products")) with two fp32 operands — so
-# their MFMA ceiling is the dense bf16 peak / P in fp32-FLOP units.
+# Every HIP kernel family of the iteration and the roofline that bounds it
+# (DESIGN.md §5): name (as the library's event profiler tags the launch) ->
+# (bound, peak, work unit of the tag, instructions).  Work is algorithmic:
+# fp32 FLOP = 2·M·N·K of the layer for the GEMMs, compulsory HBM bytes for the
+# byte movers.  The split-bf16 kernels execute P bf16 part products per fp32
+# product on the matrix cores — 3 with a u8 operand (exact in bf16), 6 (default)
+# or 9 (ppo_tune_set("products")) with two fp32 operands — so their MFMA
+# ceiling is the dense bf16 peak / P in fp32-FLOP units.
 def profiled(products):
     split = (f"v_mfma_f32_16x16x32_bf16 x{products} "
              + ("(exact split)" if products == 9 else "(split, 6 products: fp32-accurate)"))
     pk = PEAK_BF16_MFMA_TFLOPS / products
+
+    def mf(how):
+        return ("mfma", pk, "flop", split + how)
+
+    def hbm(how):
+        return ("hbm", PEAK_HBM_GBPS, "bytes", how)
     return {
-        "conv2_fwd": ("mfma", pk, split + ", image-resident"),
-        "conv2_dgrad": ("mfma", pk, split + ", image-resident"),
-        "conv2_wgrad": ("mfma", pk, split + ", image-resident, ds_read_b64_tr_b16 im2col"),
-        "conv3_fwd": ("mfma", pk, split + ", image-resident"),
-        "conv3_dgrad": ("mfma", pk, split + ", image-resident"),
-        "conv3_wgrad": ("mfma", pk, split + ", image-resident, ds_read_b64_tr_b16 im2col"),
+        "conv2_fwd": mf(", image-resident"),
+        "conv2_dgrad": mf(", image-resident"),
+        "conv2_wgrad": mf(", image-resident, ds_read_b64_tr_b16 im2col"),
+        "conv3_fwd": mf(", image-resident"),
+        "conv3_dgrad": mf(", image-resident"),
+        "conv3_wgrad": mf(", image-resident, ds_read_b64_tr_b16 im2col"),
         # u8 pixels are exact in bf16: 3 products per fp32 product
-        "conv1_wgrad_u8": ("mfma", PEAK_BF16_MFMA_TFLOPS / 3,
+        "conv1_wgrad_u8": ("mfma", PEAK_BF16_MFMA_TFLOPS / 3, "flop",
                            "v_mfma_f32_32x32x16_bf16 x3 (u8 exact), image-resident"),
         # conv1 forward: 79,424 B of compulsory HBM traffic per sample (28,224 B u8 in, 51,200 B f32 out)
         # against 6.55 MFLOP at bf16/3 -> HBM-bound
-        "conv1_fwd_u8": ("hbm", PEAK_HBM_GBPS, "v_mfma_f32_16x16x32_bf16 x3 (u8 exact), image-resident"),
+        "conv1_fwd_u8": ("hbm", PEAK_HBM_GBPS, "conv1_flop", "v_mfma_f32_16x16x32_bf16 x3 (u8 exact), image-resident"),
+        "fc_fwd": mf(", fc 1568->H + ReLU (tile GEMM)"),
+        "linear_dgrad_mask": mf(", fc dgrad with conv3's ReLU mask"),
+        "linear_wgrad": mf(", fc / GRU weight gradients, split-K slabs"),
+        "linear_fwd_ex": mf(", GRU input projection / MLP layers"),
+        "linear_dgrad_ex": mf(", GRU input dgrad / MLP layers"),
+        "gru_seq_fwd": ("mfma", PEAK_FP32_MFMA_TFLOPS, "flop",
+                        "v_mfma_f32_16x16x4_f32 register-tiled GRU step kernels (cell fused), T launches"),
+        "gru_seq_bwd": ("mfma", PEAK_FP32_MFMA_TFLOPS, "flop",
+                        "v_mfma_f32_16x16x4_f32 BPTT step kernels fused with the gate backward"),
+        "heads_train": hbm("Categorical + PPO loss + analytic backward fused, one wave per row"),
+        "heads_act": hbm("value / logits / Categorical sample fused"),
+        "heads_reduce": hbm("head-gradient partial sums"),
+        "wgrad_reduce": hbm("split-K slab reduce into the flat gradient"),
+        "gae": hbm("GAE + advantage difference + moment partials"),
+        "adv_norm": hbm("advantage normalisation"),
+        "insert": hbm("RolloutStorage.insert scalars"),
+        "synth_env": hbm("synthetic env: u8 frames written into the storage slot"),
+        "grad_sumsq": hbm("clip_grad_norm_ partial sums"),
+        "clip_adam": hbm("clip + Adam"),
+        "pack_weights": hbm("per-step weight repack + bf16 split"),
     }
 
 
+# event-timed inside the timed region (the MFMA trunk kernels; the dominant one
+# is the `roofline` line); the rest are timed in one profiled iteration after it
+TIMED = ("conv2_fwd", "conv2_dgrad", "conv2_wgrad", "conv3_fwd", "conv3_dgrad", "conv3_wgrad", "conv1_wgrad_u8",
+         "conv1_fwd_u8")
 PROFILED = profiled(6)
 CONV1_FWD_BYTES_PER_FLOP = 79424.0 / (2.0 * 400 * 32 * 256)
 
@@ -80,13 +123,16 @@ def parse():
     p.add_argument("--hidden", type=int, default=None, help="default 512 (CNN) / 256 (GRU)")
     p.add_argument("--recurrent", action="store_true", help="c5: GRU policy + vector obs")
     p.add_argument("--vec-len", type=int, default=14, help="vector obs length with --recurrent (OTC v7: 14)")
-    p.add_argument("--profile-kernels", default=",".join(PROFILED),
-                   help="kernels timed with HIP events; the one with the most time is the roofline kernel")
+    p.add_argument("--profile-kernels", default=",".join(TIMED),
+                   help="kernels event-timed inside the timed region; the one with the most time is the roofline kernel")
+    p.add_argument("--no-profile-pass", action="store_true",
+                   help="skip the profiled iteration after the timed region (per-kernel breakdown)")
     p.add_argument("--products", type=int, default=6, choices=(6, 9),
                    help="part products per fp32 product in the split-bf16 GEMMs (9 = every product exact)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-envs", type=int, default=32)
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=None,
+                   help="threads of the multi-threaded CPU baseline (default: OMP_NUM_THREADS or the core count, <= 16)")
     p.add_argument("--no-gae-roofline", action="store_true")
     p.add_argument("--no-boundary", action="store_true", help="skip the observation-boundary measurement")
     p.add_argument("--gae-lanes", type=int, default=1 << 20)
@@ -271,31 +317,133 @@ def pmc_mfma(workload):
     return out, d["mfma_util_file"]
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(envs, T, E, M, hidden, threads):
-    """The oracle's numpy (fp32) restatement of the reference CPU path, timed on a
-    bounded sample: `envs` lanes x T steps, E x M minibatches."""
-    from threadpoolctl import threadpool_limits
-    from oracle import ppo_oracle as O
-    rng = np.random.default_rng(1)
-    shapes = O.cnn_param_shapes(hidden)
-    flat = np.concatenate([rng.standard_normal(int(np.prod(s))).astype(np.float32) * 0.05 for _, s in shapes])
-    obs = rng.integers(0, 256, (T + 1, envs, 4, 84, 84), dtype=np.uint8)
-    noise = rng.exponential(1.0, (T, envs, 8)).astype(np.float32)
-    rewards = rng.random((T, envs), np.float32)
-    masks = (rng.random((T, envs)) > 0.01).astype(np.float32)
-    perms = np.stack([rng.permutation(envs * T) for _ in range(E)])
-    with threadpool_limits(limits=threads):
-        t0 = time.perf_counter()
-        O.run_iteration(flat, shapes, obs, noise, rewards, masks, perms, num_mini_batch=M, dtype=np.float32)
-        dt = time.perf_counter() - t0
-    return {"value": round(envs * T / dt, 2), "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle numpy fp32 port of the reference CPU path (T/run.py:168-248), CNNBase H={hidden}, "
-                      f"{envs} envs x {T} steps, {E} epochs x {M} minibatches, one iteration, {dt:.1f} s"}
+    """The reference's CPU path (T/run.py:168-248: act -> env -> insert x T,
+    get_value, compute_returns, PPO.update with torch.optim.Adam and
+    clip_grad_norm_, after_update) restated in torch (oracle/torch_ref.py, pinned
+    to the reference's recorded iteration), fp32 observations as the reference
+    stores them, timed for one iteration of `envs` lanes x T steps — at 1 thread
+    (the reference's torch.set_num_threads(1), T/run.py:55) and at `threads`."""
+    from a2c_ppo_acktr.model import CNNBase, Policy
+    from a2c_ppo_acktr.synthetic import Discrete
+    from oracle import torch_ref as TR
+    saved = torch.get_num_threads()
+    rng_state = torch.get_rng_state()
+    torch.manual_seed(1)
+    pol = Policy((4, 84, 84), Discrete(8), base=CNNBase, base_kwargs={"recurrent": False, "hidden_size": hidden})
+    flat = torch.cat([q.detach().reshape(-1) for q in pol.parameters()])
+    runs = {}
+    try:
+        for th in sorted({1, threads}):
+            torch.set_num_threads(th)
+            p = TR.unflatten(flat, hidden, requires_grad=True)
+            opt = torch.optim.Adam(p, lr=1e-4, eps=1e-5)
+            gen = torch.Generator().manual_seed(123)
+            frames = TR.env_frames(envs, gen=gen)
+            t0 = time.perf_counter()
+            TR.run_iteration(p, opt, envs, T, ppo_epoch=E, num_mini_batch=M, gen=gen, frames=frames)
+            dt = time.perf_counter() - t0
+            runs[th] = (envs * T / dt, dt)
+    finally:
+        torch.set_num_threads(saved)
+        torch.set_rng_state(rng_state)
+    best = max(runs, key=lambda k: runs[k][0])
+    return {"value": round(runs[best][0], 2), "unit": "env-steps/s", "cores": best, "kind": "port",
+            "cpu_model": cpu_model(),
+            "by_threads": {str(k): {"value": round(v[0], 2), "seconds": round(v[1], 2)} for k, v in runs.items()},
+            "sample": f"the reference CPU path (T/run.py:168-248) restated in torch on the host "
+                      f"(oracle/torch_ref.py: F.conv2d/linear, autograd, torch.optim.Adam, clip_grad_norm_, "
+                      f"fp32 obs storage), CNNBase H={hidden}, {envs} envs x {T} steps, {E} epochs x {M} "
+                      f"minibatches, one iteration per thread setting; value = the faster setting"}
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N ranks of this script as child
+    processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each), wait
+    for all of them, and return the first non-zero exit status.  Nothing here
+    touches the GPU; if one rank fails the others are stopped (they would block
+    in a collective)."""
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.kill()
+        time.sleep(0.2)
+    return rc
+
+
+def kernel_entry(name, launches, ms_total, work, products, where):
+    bound, peak, unit_kind, how = profiled(products).get(
+        name, ("mfma", PEAK_FP32_MFMA_TFLOPS, "flop", "v_mfma_f32_32x32x2_f32"))
+    if unit_kind == "bytes":
+        achieved, unit = work / (ms_total * 1e-3) / 1e9, "GB/s"
+    elif unit_kind == "conv1_flop":
+        achieved, unit = work * CONV1_FWD_BYTES_PER_FLOP / (ms_total * 1e-3) / 1e9, "GB/s"
+    else:
+        achieved, unit = work / (ms_total * 1e-3) / 1e12, "TFLOP/s"
+    e = {"bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": unit,
+         "frac": round(achieved / peak, 4), "ms_total": round(ms_total, 3), "launches": int(launches),
+         "avg_launch_ms": round(ms_total / launches, 4), "instructions": how, "timed_in": where}
+    if unit_kind != "bytes":
+        e["fp32_tflops"] = round(work / (ms_total * 1e-3) / 1e12, 2)
+    return e
+
+
+def prof_collect(names):
+    out = {}
+    from a2c_ppo_acktr import _hip
+    for ki, name in enumerate(names):
+        prof = torch.zeros(3, dtype=torch.float64)
+        _hip.call("ppo_prof_collect_one", ki, prof.data_ptr())
+        out[name] = prof.tolist()
+    _hip.call("ppo_prof_enable", None, 0)
+    return out
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: one child process per rank (started before any GPU call here)
+        if args.dist_backend == "nccl" and torch.cuda.device_count() < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but {torch.cuda.device_count()} GPUs are visible", file=sys.stderr)
+            sys.exit(2)
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} does not match --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU; modulo the visible count only so a gloo rehearsal of the
@@ -308,6 +456,7 @@ def main():
             dist.init_process_group("nccl", device_id=device)   # RCCL over xGMI
         else:
             dist.init_process_group(args.dist_backend)
+        assert dist.get_world_size() == args.gpus
 
     from a2c_ppo_acktr import _hip
     from a2c_ppo_acktr.algo import PPO
@@ -361,9 +510,9 @@ def main():
     if rank == 0 and not args.no_boundary:
         evalp = eval_latency(device)
 
-    cap = args.steps * (T + 2 * E * M + 8) + 16
+    launches_per_iter = 8 * T + 32 * E * M + 64
     names = [k for k in args.profile_kernels.split(",") if k]
-    _hip.call("ppo_prof_enable", ",".join(names).encode(), cap * len(names))
+    _hip.call("ppo_prof_enable", ",".join(names).encode(), args.steps * launches_per_iter)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -375,12 +524,25 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    per_kernel = {}
-    for ki, name in enumerate(names):
-        prof = torch.zeros(3, dtype=torch.float64)
-        _hip.call("ppo_prof_collect_one", ki, prof.data_ptr())
-        per_kernel[name] = prof.tolist()
-    _hip.call("ppo_prof_enable", None, 0)
+    per_kernel = prof_collect(names)
+
+    # per-kernel breakdown: one more iteration with every kernel family event-timed
+    # (outside the timed region: the extra events would perturb `value`)
+    pass_info, pass_kernels = None, {}
+    if not args.no_profile_pass:
+        all_names = list(profiled(args.products))
+        _hip.call("ppo_prof_enable", ",".join(all_names).encode(), launches_per_iter * 2)
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        iteration()
+        torch.cuda.synchronize()
+        pass_ms = (time.perf_counter() - tp) * 1e3
+        pass_kernels = prof_collect(all_names)
+        covered = sum(v[1] for v in pass_kernels.values())
+        pass_info = {"iteration_ms": round(pass_ms, 2), "event_timed_ms": round(covered, 2),
+                     "coverage": round(covered / pass_ms, 4),
+                     "note": "sum of the event-timed kernel families / wall time of one profiled iteration"}
+
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -393,26 +555,25 @@ def main():
                 + f", {N} env lanes x {T} steps per GPU, PPO {E} epochs x {M} minibatches "
                   f"(rollout + GAE + update, fp32)")
     kernels = {}
-    for name, (launches, ms_total, flops) in per_kernel.items():
-        if launches <= 0 or ms_total <= 0:
-            continue
-        bound, peak, how = profiled(args.products).get(name, ("mfma", PEAK_FP32_MFMA_TFLOPS, "v_mfma_f32_32x32x2_f32"))
-        tflops = flops / (ms_total * 1e-3) / 1e12
-        if bound == "hbm":
-            achieved, unit = flops * CONV1_FWD_BYTES_PER_FLOP / (ms_total * 1e-3) / 1e9, "GB/s"
-        else:
-            achieved, unit = tflops, "TFLOP/s"
-        kernels[name] = {"bound": bound, "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": unit,
-                         "frac": round(achieved / peak, 4), "ms_total": round(ms_total, 2),
-                         "launches": int(launches), "avg_launch_ms": round(ms_total / launches, 4),
-                         "fp32_tflops": round(tflops, 2), "instructions": how}
+    for name, (launches, ms_total, work) in per_kernel.items():
+        if launches > 0 and ms_total > 0:
+            kernels[name] = kernel_entry(name, launches, ms_total, work, args.products, "timed region")
+    for name, (launches, ms_total, work) in pass_kernels.items():
+        if launches > 0 and ms_total > 0:
+            e = kernel_entry(name, launches, ms_total, work, args.products, "profile pass")
+            e["ms_per_iteration"] = round(ms_total, 3)
+            if name in kernels:
+                kernels[name]["ms_per_iteration"] = e["ms_per_iteration"]
+            else:
+                kernels[name] = e
     util, util_src = pmc_mfma(workload)
     for name, u in util.items():
         if name in kernels:
             kernels[name]["mfma_util_pmc"] = u
     roof = None
-    if kernels:
-        dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
+    timed = {k: v for k, v in kernels.items() if v["timed_in"] == "timed region"}
+    if timed:
+        dom = max(timed, key=lambda k: timed[k]["ms_total"])
         kd = kernels[dom]
         traffic, tsrc = pmc_traffic(dom, workload)
         roof = {"bound": kd["bound"], "achieved": kd["achieved"], "peak": kd["peak"], "unit": kd["unit"],
@@ -423,7 +584,8 @@ def main():
                 "flop_per_launch": round(per_kernel[dom][2] / per_kernel[dom][0])}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_envs, T, E, M, H, args.cpu_threads)
+        threads = args.cpu_threads or min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1))
+        cpu = cpu_baseline(args.cpu_envs, T, E, M, H, threads)
     value = N * T * world * args.steps / elapsed
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
@@ -432,12 +594,13 @@ def main():
         "data": "synthetic: counter-hash u8 4x84x84 obs, U[0,1) rewards, Bernoulli(0.01) dones; random-init weights",
         "config": {"workload": workload,
                    "envs_per_gpu": N, "num_steps": T, "ppo_epoch": E, "num_mini_batch": M, "hidden": H,
-                   "global_batch": N * T * world, "parallelism": f"dp{world}"},
+                   "global_batch": N * T * world, "parallelism": f"dp{world}",
+                   "dist_backend": (args.dist_backend if world > 1 else None)},
         "roofline": roof, "cpu_baseline": cpu, "gae_roofline": gae, "boundary_roofline": boundary, "eval_latency": evalp,
-        "kernel_rooflines": kernels,
+        "profile_pass": pass_info, "kernel_rooflines": kernels,
         "losses": [round(x, 6) for x in losses],
     }
-    print(json.dumps(out))
+    print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -234,7 +234,11 @@ int ppo_heads_act(const float* feat, const float* feat_v, int N, int H, const fl
 /* algo/ppo.py:57-81 evaluate_actions + clipped surrogate + clipped value loss +
  * entropy, forward and analytic backward to dL/dfeature (through the features'
  * activation feat_act: 0 none, 1 ReLU, 2 tanh), head-gradient partials; with
- * feat_v the critic branch's gradient goes to dfeat_v */
+ * feat_v the critic branch's gradient goes to dfeat_v.  part_loss holds 4 floats
+ * per block and loss_acc 4 doubles: {value loss, action loss, entropy, number of
+ * stored actions outside [0, A)} — the last is where the reference's
+ * log_probs gather raises (distributions.py:22); PPO.update raises on it.
+ * ppo_heads_act with `given` writes a NaN log-prob for such a row. */
 int ppo_heads_train_blocks(int B);
 int ppo_heads_train(const float* feat, const float* feat_v, int B, int H, const float* wc, const float* bc,
                     const float* wa,

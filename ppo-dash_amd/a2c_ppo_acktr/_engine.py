@@ -16,6 +16,8 @@ Per PPO minibatch (every box is a libppo_hip.so kernel):
   wgrad slab reduces -> flat grad  [RCCL all-reduce when world_size > 1]
   grad Σg² -> clip + Adam -> pack weights
 """
+import contextlib
+
 import torch
 
 from ._hip import call, ptr, stream
@@ -56,6 +58,7 @@ class CNNEngine:
                                       "(the reference crashes there too: Categorical expects hidden_size inputs)")
         self.params = list(policy.parameters())
         self.ws = {"act": _Workspace(), "train": _Workspace()}
+        self.act_ws = "act"   # workspace of the forward (act / get_value / evaluate) paths
         self.packed = None
         self._pack_key = None
         self.epoch = 0  # bumped by every in-place parameter write done by HIP kernels
@@ -80,6 +83,17 @@ class CNNEngine:
                 off += k
         self.flat, self.grad, self.numel = flat, grad, n
         self.epoch += 1
+
+    @contextlib.contextmanager
+    def using_workspace(self, name):
+        """Route the forward paths through workspace `name` (e.g. a captured HIP
+        graph's own buffers, which no eager call may reallocate)."""
+        self.ws.setdefault(name, _Workspace())
+        prev, self.act_ws = self.act_ws, name
+        try:
+            yield self.ws[name]
+        finally:
+            self.act_ws = prev
 
     def is_bound(self):
         base = self.flat.data_ptr()
@@ -197,7 +211,7 @@ class CNNEngine:
         self.pack()
         obs = self._check_obs(obs)
         B = obs.shape[0]
-        h = self.trunk(obs, None, B, self.ws["act"])
+        h = self.trunk(obs, None, B, self.ws[self.act_ws])
         return self._heads(h, B, deterministic, noise, given, want_entropy, value_only)
 
     # --------------------------------------------------------------- training
@@ -206,7 +220,7 @@ class CNNEngine:
         nblk = call("ppo_heads_train_blocks", B)
         part_w = ws.get("part_w", nblk * (1 + A) * H, device=dev)
         part_b = ws.get("part_b", nblk * (1 + A), device=dev)
-        part_l = ws.get("part_l", nblk * 3, device=dev)
+        part_l = ws.get("part_l", nblk * 4, device=dev)
         inv_b = 1.0 / B
         call("ppo_heads_train", feat.data_ptr(), ptr(feat_v), B, H, self.pv(self.WC), self.pv(self.BC), self.pv(self.WA),
              self.pv(self.BA), A, idx.data_ptr(), 0, storage.actions.data_ptr(), storage.action_log_probs.data_ptr(),
@@ -354,7 +368,7 @@ class RecurrentEngine(CNNEngine):
         self.pack()
         obs = self._check_obs(obs)
         B = obs.shape[0]
-        ws = self.ws["act"]
+        ws = self.ws[self.act_ws]
         _, gi = self._input(obs, self._vec(vec, B), None, B, ws)
         hxs = hxs.to(self.device, torch.float32).reshape(B, self.H).contiguous()
         m = masks.to(self.device, torch.float32).reshape(B).contiguous() if masks is not None else None
@@ -372,7 +386,7 @@ class RecurrentEngine(CNNEngine):
         R = obs.shape[0]
         N = hxs.shape[0]
         T = R // N
-        ws = self.ws["act"]
+        ws = self.ws[self.act_ws]
         _, gi = self._input(obs, self._vec(vec, R), None, R, ws)
         hxs = hxs.to(self.device, torch.float32).reshape(N, self.H).contiguous()
         m = masks.to(self.device, torch.float32).reshape(R).contiguous()
@@ -446,6 +460,7 @@ class MLPEngine(CNNEngine):
             raise NotImplementedError(f"MLPBase hidden_size {self.H}: multiples of 4 up to 512")
         self.params = list(policy.parameters())
         self.ws = {"act": _Workspace(), "train": _Workspace()}
+        self.act_ws = "act"
         self.packed = None
         self._pack_key = None
         self.epoch = 0
@@ -499,7 +514,7 @@ class MLPEngine(CNNEngine):
         B = obs.shape[0]
         if obs.shape[1] != self.obs_dim:
             raise RuntimeError(f"MLPBase expects [N,{self.obs_dim}] observations, got {tuple(obs.shape)}")
-        ws = self.ws["act"]
+        ws = self.ws[self.act_ws]
         v = vec.to(self.device, torch.float32).reshape(B, self.V).contiguous() if self.V else None
         x = self._x(obs, v, None, B, ws)
         t = self.towers(x, B, ws)

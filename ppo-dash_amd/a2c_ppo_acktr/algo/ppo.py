@@ -46,9 +46,17 @@ class FlatAdam(object):
     def _step_flat(self, eng):
         """all-reduce (G>1) -> Σg² partials -> fused clip + Adam on eng.flat."""
         n = eng.numel
-        if self.exp_avg is None or self.exp_avg.numel() != n or self.exp_avg.device != eng.device:
+        if self.exp_avg is None:
             self.exp_avg = torch.zeros(n, device=eng.device)
             self.exp_avg_sq = torch.zeros(n, device=eng.device)
+        elif self.exp_avg.numel() != n or self.exp_avg_sq is None or self.exp_avg_sq.numel() != n:
+            raise RuntimeError(f"Adam state holds {self.exp_avg.numel()} moments for {n} parameters "
+                               "(optimizer state of a different policy?)")
+        elif self.exp_avg.device != eng.device or self.exp_avg_sq.device != eng.device:
+            # restored on another device (e.g. a checkpoint loaded before .to(device)):
+            # keep the moments — step_count's bias correction assumes them
+            self.exp_avg = self.exp_avg.to(eng.device, torch.float32).contiguous()
+            self.exp_avg_sq = self.exp_avg_sq.to(eng.device, torch.float32).contiguous()
         if self._partials is None or self._partials.device != eng.device:   # also after load_state_dict
             self._partials = torch.empty(call("ppo_grad_partials_count", n), dtype=torch.float64, device=eng.device)
             self._norm = torch.zeros(1, dtype=torch.float64, device=eng.device)
@@ -106,7 +114,8 @@ class PPO():
         eng = self.actor_critic.hip_engine()
         advantages = rollouts.normalized_advantages()            # ppo.py:35-37
         if self._loss_acc is None or self._loss_acc.device != eng.device:
-            self._loss_acc = torch.zeros(3, dtype=torch.float64, device=eng.device)
+            # {value loss, action loss, entropy} sums + the count of stored actions outside [0, A)
+            self._loss_acc = torch.zeros(4, dtype=torch.float64, device=eng.device)
         else:
             self._loss_acc.zero_()
         hp = {"clip": float(self.clip_param), "value_coef": float(self.value_loss_coef),
@@ -151,6 +160,10 @@ class PPO():
     def _losses(self):
         _dist.allreduce_losses(self._loss_acc)
         num_updates = self.ppo_epoch * self.num_mini_batch        # ppo.py:90 (not the drop_last count)
-        losses = (self._loss_acc / num_updates).tolist()           # one D2H per update
-        value_loss_epoch, action_loss_epoch, dist_entropy_epoch = losses
+        acc = self._loss_acc.tolist()                              # one D2H per update
+        if acc[3] > 0:
+            # the reference's log_probs gather (distributions.py:22) raises on such an index
+            raise IndexError("PPO.update: {:.0f} stored action(s) outside [0, {}) in the rollout".format(
+                acc[3] * _dist.world_size(), self.actor_critic.hip_engine().A))
+        value_loss_epoch, action_loss_epoch, dist_entropy_epoch = (x / num_updates for x in acc[:3])
         return value_loss_epoch, action_loss_epoch, dist_entropy_epoch

@@ -91,14 +91,19 @@ def save_checkpoint(path, actor_critic, ob_rms=None, agent=None, extra=None):
 def load_checkpoint(path, device=None, actor_critic=None, agent=None):
     """-> (actor_critic, ob_rms), as `torch.load(...)` returns them at T/run.py:64-66.
     Loads with weights_only=True.  Rebuilds the Policy from the recorded config
-    unless one is passed in (its parameters are then overwritten in place);
-    restores the optimizer state into `agent` when given."""
+    unless one is passed in, or `agent` is (then agent.actor_critic is used; its
+    parameters are overwritten in place); restores the optimizer state into
+    `agent` when given."""
     from . import model as M
 
     ck = torch.load(path, map_location="cpu", weights_only=True)
     if ck.get("format") != FORMAT:
         raise ValueError("%s: not a %s file" % (path, FORMAT))
     cfg = ck["config"]
+    if actor_critic is None and agent is not None:
+        # the agent trains agent.actor_critic: load into that policy, or the
+        # rollouts would act with new weights while the update trains stale ones
+        actor_critic = agent.actor_critic
     if actor_critic is None:
         base = {"CNNBase": M.CNNBase, "MLPBase": M.MLPBase}[cfg["base"]]
         actor_critic = M.Policy(tuple(cfg["obs_shape"]), _Space(cfg["action_space"]), base=base,

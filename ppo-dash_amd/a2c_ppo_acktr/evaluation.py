@@ -7,11 +7,14 @@ drives hipStreamBeginCapture on the current stream, which is where every
 libppo_hip.so launch goes) and replays it per step: inputs are copied into
 static buffers, one graph launch runs the whole forward.
 
-The graph holds pointers to the engine's flat parameters and packed weights,
-so it stays valid while the policy trains in place: before each replay the
-packed planes are refreshed if the parameters changed since the last pack.
-Only deterministic acting is graphed (the stochastic sampler's RNG counter is
-a launch argument and would freeze inside a graph).
+The graph holds raw pointers, so everything it touches is kept stable: the
+forward runs in the engine's own "graph" workspace (no eager act, get_value or
+rollout at another batch size reallocates it), the packed weight planes are
+refreshed in place before a replay when the parameters changed, and the graph is
+re-captured when the flat parameter buffer or the packed planes were
+reallocated (Policy re-bound, moved, or a new engine).  Only deterministic
+acting is graphed (the stochastic sampler's RNG counter is a launch argument
+and would freeze inside a graph).
 """
 import torch
 
@@ -19,7 +22,7 @@ import torch
 class GraphedActor(object):
     def __init__(self, policy, num_envs=1, obs_dtype=torch.float32, device=None, warmup=2):
         eng = policy.hip_engine(device)
-        self.policy, self.eng, self.device = policy, eng, eng.device
+        self.policy, self.device, self.warmup = policy, eng.device, warmup
         base = policy.base
         C = base.main[0].weight.shape[1]
         V = getattr(base, "vector_obs_len", 0)
@@ -29,16 +32,25 @@ class GraphedActor(object):
         self.vec = torch.zeros(num_envs, V, device=dev)
         self.hxs = torch.zeros(num_envs, Hh, device=dev)
         self.masks = torch.ones(num_envs, 1, device=dev)
+        self.captures = 0
+        self._capture()
+
+    def _capture(self):
+        dev = self.device
+        self.eng = self.policy.hip_engine(dev)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):   # warm-up: workspaces, packed weights, device attributes
-            for _ in range(warmup):
-                self._act()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out = self._act()
+        with self.eng.using_workspace("graph"):
+            with torch.cuda.stream(side):   # warm-up: workspaces, packed weights, device attributes
+                for _ in range(self.warmup):
+                    self._act()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.out = self._act()
         self._key = self._pack_key()
+        self._ptrs = self._pointers()
+        self.captures += 1
 
     def _act(self):
         with torch.no_grad():
@@ -47,12 +59,21 @@ class GraphedActor(object):
     def _pack_key(self):
         return (sum(p._version for p in self.eng.params), self.eng.epoch)
 
+    def _pointers(self):
+        """every buffer address baked into the graph that could be reallocated"""
+        e = self.eng
+        gp = getattr(e, "gru_packed", None)
+        return (id(e), e.flat.data_ptr(), e.packed.data_ptr(), None if gp is None else gp.data_ptr(),
+                tuple((k, t.data_ptr()) for k, t in sorted(e.ws["graph"].bufs.items())))
+
     def act(self, visual_inputs, vector_inputs, rnn_hxs, masks, deterministic=True):
         """Policy.act (model.py:54-66) for the captured batch -> (value, action, log_prob, rnn_hxs)"""
         if not deterministic:
             raise NotImplementedError("GraphedActor replays deterministic acting only; use Policy.act to sample")
-        self.eng.ensure_bound()
-        if self._pack_key() != self._key:   # parameters were updated in place: refresh the packed planes
+        eng = self.policy.hip_engine(self.device)   # re-binds (new flat buffer) if the parameters were replaced
+        if eng is not self.eng or self._pointers() != self._ptrs:
+            self._capture()                          # buffers moved: the old graph's pointers are stale
+        elif self._pack_key() != self._key:          # parameters updated in place: refresh the packed planes
             self.eng.pack(force=True)
             self._key = self._pack_key()
         for dst, src in ((self.obs, visual_inputs), (self.vec, vector_inputs), (self.hxs, rnn_hxs),

@@ -73,6 +73,18 @@ void ppo_set_error(const char* fmt, ...);
 bool ppo_prof_begin(const char* name, hipStream_t st, int* slot);
 void ppo_prof_end(int slot, hipStream_t st, double work);
 
+// the same for a whole API call (all launches it makes): events at entry and exit
+struct ProfScope {
+  hipStream_t st;
+  double work;
+  int slot = -1;
+  bool on;
+  ProfScope(const char* name, hipStream_t s, double w) : st(s), work(w) { on = ppo_prof_begin(name, s, &slot); }
+  ~ProfScope() {
+    if (on) ppo_prof_end(slot, st, work);
+  }
+};
+
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline unsigned ceil_div(long long a, long long b) { return (unsigned)((a + b - 1) / b); }

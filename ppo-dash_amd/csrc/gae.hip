@@ -200,6 +200,7 @@ PPO_API int ppo_compute_returns(const float* rewards, float* value_preds, const 
   PPO_REQUIRE(rewards && value_preds && masks && next_value && returns, "ppo_compute_returns: null pointer");
   PPO_REQUIRE(!use_proper_time_limits || bad_masks, "ppo_compute_returns: bad_masks required");
   PPO_REQUIRE((adv == nullptr) == (partials == nullptr), "ppo_compute_returns: adv and partials go together");
+  ProfScope prof("gae", as_stream(stream), (adv ? 20.0 : 16.0) * T * N);
   const float g = (float)gamma;
   const float gl = (float)(gamma * gae_lambda);  // Python double product, then fp32
   hipStream_t st = as_stream(stream);
@@ -241,6 +242,7 @@ PPO_API int ppo_adv_finalize(const double* partials, int nparts, double count, d
 
 PPO_API int ppo_adv_normalize(float* adv, long long n, const double* stats, void* stream) {
   PPO_REQUIRE(n > 0, "ppo_adv_normalize: n=%lld", n);
+  ProfScope prof("adv_norm", as_stream(stream), 8.0 * n);
   long long b = (n + 255) / 256;
   adv_normalize_kernel<<<(unsigned)(b < 4096 ? b : 4096), 256, 0, as_stream(stream)>>>(adv, n, stats);
   PPO_LAUNCH_CHECK("adv_normalize_kernel");

@@ -1913,6 +1913,7 @@ static inline const uint16_t* planes_of(const float* seg, long long n) {
 }
 
 PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, int H, float* packed, void* stream) {
+  ProfScope prof("pack_weights", as_stream(stream), 4.0 * 4.0 * ppo_packed_weights_size(H));
   PPO_REQUIRE(H > 0 && H % 4 == 0, "ppo_pack_weights: hidden size %d must be a positive multiple of 4", H);
   long long n[6];
   pack_segments(H, n);
@@ -2612,6 +2613,7 @@ PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int 
 PPO_API int ppo_wgrad_reduce(const float* slab, const float* slab_bias, int Z, int M, int NW, int kind, int a, int b,
                              float* gw, float* gb, float scale, int accumulate, void* stream) {
   PPO_REQUIRE(kind >= 0 && kind <= 3, "ppo_wgrad_reduce: kind=%d", kind);
+  ProfScope prof("wgrad_reduce", as_stream(stream), 4.0 * (double)Z * M * (NW + 1) + 4.0 * M * (NW + 1));
   hipStream_t st = as_stream(stream);
   const long long cols = (long long)M * NW;
   int rc = colsum(slab, cols, Z, cols, ColMap{kind, a, b, NW}, gw, scale, accumulate, st);

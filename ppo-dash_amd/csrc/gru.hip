@@ -469,6 +469,7 @@ PPO_API int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* 
                             const float* bhh, const float* gi, int T, int n, int H, float* hout, float* save_r,
                             float* save_z, float* save_n, float* save_ghn, float* save_hin, void* stream) {
   PPO_REQUIRE(T >= 0 && n >= 0 && H > 0 && H % 32 == 0, "ppo_gru_seq_fwd: T=%d n=%d H=%d", T, n, H);
+  ProfScope prof("gru_seq_fwd", as_stream(stream), 2.0 * T * n * 3.0 * H * H);
   const bool sv = save_r != nullptr;
   for (int t = 0; t < T; ++t) {
     const size_t o = (size_t)t * n * H;
@@ -488,6 +489,7 @@ PPO_API int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float*
                             const float* whhT, int T, int n, int H, float* dgi, float* dgh, float* dhz, float* carry,
                             void* stream) {
   PPO_REQUIRE(T >= 0 && n >= 0 && H > 0 && H % 4 == 0, "ppo_gru_seq_bwd: T=%d n=%d H=%d", T, n, H);
+  ProfScope prof("gru_seq_bwd", as_stream(stream), 2.0 * T * n * 3.0 * H * H);
   const bool fused = (H == 64 || H == 128 || H == 256 || H == 512) && g_gru_variant == 0;
   for (int t = T - 1; t >= 0; --t) {
     const size_t o = (size_t)t * n * H, op = o - (size_t)n * H;

@@ -141,7 +141,9 @@ __global__ __launch_bounds__(64 * HW) void heads_act_kernel(
         }
       }
     }
-    float lp = 0.f, ent = 0.f;
+    // an action index outside [0, A) has no log-prob: the reference's gather
+    // raises there (distributions.py:22); NaN marks the row here
+    float lp = (unsigned)act < (unsigned)A ? 0.f : __int_as_float(0x7fc00000), ent = 0.f;
 #pragma unroll
     for (int o = 0; o < AMAX; ++o) {
       if (o == act) lp = nl[o];
@@ -179,7 +181,7 @@ struct TrainArgs {
   float* dfeat_v;          // [B][H] critic-branch gradient (MLPBase) or NULL
   float* part_w;           // [blocks][1+A][H]
   float* part_b;           // [blocks][1+A]
-  float* part_loss;        // [blocks][3]: Σ max(l1,l2), Σ min(s1,s2), Σ H
+  float* part_loss;        // [blocks][4]: Σ max(l1,l2), Σ min(s1,s2), Σ H, # actions outside [0, A)
   int rows_per_wave;
 };
 
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
 #pragma unroll
     for (int c = 0; c < HC; ++c) gwa[o][c] = 0.f;
   }
-  float s_vl = 0.f, s_al = 0.f, s_ent = 0.f;
+  float s_vl = 0.f, s_al = 0.f, s_ent = 0.f, s_bad = 0.f;
   const float clip = a.clip;
   const long long r0 = ((long long)blockIdx.x * HW + wave) * a.rows_per_wave;
   // The per-row storage scalars (the minibatch gather idx -> action, advantage,
@@ -250,6 +252,7 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
     head_dots(w, f, fv, value, z, b0, a.ba, A);
     categorical(z, A, nl, p);
     const int act = __builtin_amdgcn_readlane(q_act, rr);
+    s_bad += (unsigned)act < (unsigned)A ? 0.f : 1.f;   // counted; PPO.update raises (gather's IndexError)
     float lp = 0.f, ent = 0.f;
 #pragma unroll
     for (int o = 0; o < AMAX; ++o) {
@@ -312,7 +315,7 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
   }
   // block reduction of the head-gradient partials across the HW waves
   __shared__ float red[HW][64 * HC];
-  __shared__ float redb[HW][AMAX + 4];
+  __shared__ float redb[HW][AMAX + 5];
   const int NO = 1 + A;
   for (int o = 0; o < NO; ++o) {
 #pragma unroll
@@ -342,6 +345,7 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
     redb[wave][AMAX + 1] = s_vl;
     redb[wave][AMAX + 2] = s_al;
     redb[wave][AMAX + 3] = s_ent;
+    redb[wave][AMAX + 4] = s_bad;
   }
   __syncthreads();
   if (threadIdx.x < NO) {
@@ -349,36 +353,32 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
     for (int q = 0; q < HW; ++q) s += redb[q][threadIdx.x];
     a.part_b[(size_t)blockIdx.x * NO + threadIdx.x] = s;
   }
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < 4) {
     float s = 0.f;
     for (int q = 0; q < HW; ++q) s += redb[q][AMAX + 1 + threadIdx.x];
-    a.part_loss[(size_t)blockIdx.x * 3 + threadIdx.x] = s;
+    a.part_loss[(size_t)blockIdx.x * 4 + threadIdx.x] = s;
   }
 }
 
-// loss partials -> acc[0..2] += {0.5·Σvl/B, -Σal/B, Σent/B} (double, fixed order)
+// loss partials -> acc[0..3] += {0.5·Σvl/B, -Σal/B, Σent/B, # bad actions} (double, fixed order)
 __global__ __launch_bounds__(256) void loss_reduce_kernel(const float* __restrict__ part_loss, int nblk,
                                                           double* __restrict__ loss_acc, double inv_b) {
-  __shared__ double r[3][256];
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-  for (int b = threadIdx.x; b < nblk; b += 256) {
-    a0 += (double)part_loss[(size_t)b * 3];
-    a1 += (double)part_loss[(size_t)b * 3 + 1];
-    a2 += (double)part_loss[(size_t)b * 3 + 2];
-  }
-  r[0][threadIdx.x] = a0;
-  r[1][threadIdx.x] = a1;
-  r[2][threadIdx.x] = a2;
+  __shared__ double r[4][256];
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int b = threadIdx.x; b < nblk; b += 256)
+    for (int q = 0; q < 4; ++q) acc[q] += (double)part_loss[(size_t)b * 4 + q];
+  for (int q = 0; q < 4; ++q) r[q][threadIdx.x] = acc[q];
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if (threadIdx.x < o)
-      for (int q = 0; q < 3; ++q) r[q][threadIdx.x] += r[q][threadIdx.x + o];
+      for (int q = 0; q < 4; ++q) r[q][threadIdx.x] += r[q][threadIdx.x + o];
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     loss_acc[0] += 0.5 * r[0][0] * inv_b;
     loss_acc[1] += -r[1][0] * inv_b;
     loss_acc[2] += r[2][0] * inv_b;
+    loss_acc[3] += r[3][0];
   }
 }
 
@@ -472,6 +472,7 @@ PPO_API int ppo_heads_act(const float* feat, const float* feat_v, int N, int H, 
                           int64_t* action, float* logp, float* entropy, void* stream) {
   PPO_REQUIRE(N >= 0 && A >= 1 && A <= 16, "ppo_heads_act: N=%d A=%d (1..16 actions)", N, A);
   PPO_REQUIRE(H > 0 && H <= 512, "ppo_heads_act: hidden size %d (1..512)", H);
+  ProfScope prof("heads_act", as_stream(stream), (double)N * (4.0 * H * (feat_v ? 2 : 1) + 16.0));
   if (N == 0) return 0;
   hipStream_t st = as_stream(stream);
   const int HC = hc_of(H);
@@ -496,6 +497,8 @@ PPO_API int ppo_heads_train(const float* feat, const float* feat_v, int B, int H
                             float* part_loss, void* stream) {
   PPO_REQUIRE(B > 0 && A >= 1 && A <= 16, "ppo_heads_train: B=%d A=%d", B, A);
   PPO_REQUIRE(H > 0 && H <= 512, "ppo_heads_train: hidden size %d (1..512)", H);
+  ProfScope prof("heads_train", as_stream(stream),
+                 (double)B * (8.0 * H * (feat_v ? 2 : 1) + (idx ? 8.0 : 0.0) + 32.0));
   TrainArgs a;
   a.feat = feat; a.feat_v = feat_v; a.B = B; a.H = H; a.A = A; a.wc = wc; a.bc = bc; a.wa = wa; a.ba = ba;
   a.idx = idx; a.row0 = row0; a.actions = actions; a.old_logp = old_logp; a.adv = adv; a.vpred = vpred; a.ret = ret;
@@ -516,6 +519,7 @@ PPO_API int ppo_heads_reduce(const float* part_w, const float* part_b, const flo
                              float* g_wc, float* g_bc, float* g_wa, float* g_ba, double* loss_acc, double inv_b,
                              float scale, int use_clipped_value_loss, void* stream) {
   (void)use_clipped_value_loss;  // both value losses are 0.5·mean(·)
+  ProfScope prof("heads_reduce", as_stream(stream), 4.0 * nblk * (1.0 + A) * (H + 1));
   const long long NO = 1 + A;
   int rc;
   if ((rc = ppo_colsum(part_w, NO * H, nblk, H, g_wc, scale, 0, stream))) return rc;

@@ -82,6 +82,7 @@ PPO_API int ppo_grad_partials_count(long long n) {
 
 PPO_API int ppo_grad_sumsq(const float* g, long long n, float scale, double* partials, void* stream) {
   PPO_REQUIRE(n > 0, "ppo_grad_sumsq: n=%lld", n);
+  ProfScope prof("grad_sumsq", as_stream(stream), 4.0 * n);
   sumsq_kernel<<<ppo_grad_partials_count(n), OPT_THREADS, 0, as_stream(stream)>>>(g, n, scale, partials);
   PPO_LAUNCH_CHECK("sumsq_kernel");
   return 0;
@@ -93,6 +94,7 @@ PPO_API int ppo_clip_adam(float* params, float* grads, float* exp_avg, float* ex
                           const double* partials, float scale, double max_norm, double lr, double beta1, double beta2,
                           double eps, long long step, double* norm_out, void* stream) {
   PPO_REQUIRE(n > 0 && step >= 1, "ppo_clip_adam: n=%lld step=%lld", n, step);
+  ProfScope prof("clip_adam", as_stream(stream), 28.0 * n);
   const double bc1 = 1.0 - pow(beta1, (double)step);
   const double bc2 = 1.0 - pow(beta2, (double)step);
   const float step_size = (float)(lr / bc1);

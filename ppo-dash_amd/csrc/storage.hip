@@ -28,7 +28,7 @@ PPO_API const char* ppo_last_error(void) { return g_err; }
 // ---------------------------------------------------------------- profiler
 // HIP events around the launches of the named kernels (comma-separated list),
 // on the stream each launch goes to.
-static char g_prof_names[256] = "";
+static char g_prof_names[1024] = "";
 static int g_prof_cap = 0, g_prof_n = 0;
 static hipEvent_t* g_ev0 = nullptr;
 static hipEvent_t* g_ev1 = nullptr;
@@ -276,6 +276,7 @@ PPO_API int ppo_storage_insert_scalars(int N, int step, const int64_t* action, c
                                        int64_t* actions, float* action_log_probs, float* value_preds,
                                        float* rewards, float* masks, float* bad_masks, void* stream) {
   PPO_REQUIRE(N > 0 && step >= 0, "ppo_storage_insert_scalars: N=%d step=%d", N, step);
+  ProfScope prof("insert", as_stream(stream), 48.0 * N);
   insert_scalars_kernel<<<ceil_div(N, 256), 256, 0, as_stream(stream)>>>(
       N, step, action, logp, value, reward, mask, bad_mask, actions, action_log_probs, value_preds, rewards, masks,
       bad_masks);
@@ -325,6 +326,7 @@ PPO_API int ppo_synth_env_step(uint8_t* obs, int N, long long obs_bytes, float* 
   PPO_REQUIRE(N > 0 && obs_bytes > 0 && obs_bytes % 16 == 0, "ppo_synth_env_step: N=%d obs_bytes=%lld", N,
               obs_bytes);
   PPO_REQUIRE(((uintptr_t)obs & 15) == 0, "ppo_synth_env_step: obs not 16-B aligned");
+  ProfScope prof("synth_env", as_stream(stream), (double)N * (obs_bytes + 12));
   long long work = (obs_bytes / 16) * N;
   long long b = (work + 255) / 256;
   long long bmin = (N + 255) / 256;

@@ -1,0 +1,188 @@
+"""Full-size parity (BASELINE.json configs c2, c3, c5 at their own shapes): one
+whole rollout of the drop-in API on the synthetic env, then
+
+  * returns bit-exact vs the C oracle of compute_returns (storage.py:82-121) on
+    the storage that rollout produced, advantage statistics vs the oracle;
+  * stored values / log-probs on a strided subset vs the float64 forward;
+  * one full minibatch gradient (c3: 65,536 rows, c2: 16,384 rows) vs float64
+    autograd of the reference's loss (oracle/torch_ref.py: algo/ppo.py:57-81 with
+    torch.distributions.Categorical, convolutions as explicit im2col GEMMs in
+    float64 on the GPU), 1e-5 of each tensor's max |g|, losses 2e-5 relative;
+  * c5: one 512-env x 256-step recurrent minibatch (H=256, V=14): the GRU, head
+    and trunk gradients vs float64 — the oracle's BPTT (oracle.gru_backward) on the
+    engine's own GRU inputs, and float64 autograd of the trunk driven by the
+    oracle's dL/dx — 1e-5 of each tensor's max |g|.
+
+These take seconds to minutes on the MI355X; the float64 references run on the
+GPU (torch) and on the host (numpy, GRU only)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ppo_oracle as O
+from oracle import torch_ref as TR
+
+pytestmark = pytest.mark.gpu
+
+HP = {"clip": 0.1, "value_coef": 0.5, "entropy_coef": 0.001, "use_clipped_value_loss": True}
+
+
+class _GradCapture(object):
+    """FlatAdam stand-in: keeps the minibatch's flat gradient (no parameter step)."""
+
+    def _step_flat(self, eng):
+        self.grad = eng.grad.clone()
+
+
+def _rollout(pol, st, env, T, vec=None):
+    for step in range(T):
+        with torch.no_grad():
+            v, a, lp, h = pol.act(st.obs[step], st.vector_obs[step], st.recurrent_hidden_states[step], st.masks[step])
+        r, m, bm = env.step_into(st.obs[step + 1], a)
+        st.insert(st.obs[step + 1], vec if vec is not None else st.vector_obs[step + 1], h, a, lp, v, r, m, bm)
+    with torch.no_grad():
+        nv = pol.get_value(st.obs[-1], st.vector_obs[-1], st.recurrent_hidden_states[-1], st.masks[-1])
+    return nv
+
+
+def _check_returns(st, nv):
+    """compute_returns bit-exact vs the C oracle on this storage; advantage
+    statistics vs the oracle's (ppo.py:35-37)."""
+    r = st.rewards[..., 0].cpu().numpy()
+    v = st.value_preds[..., 0].cpu().numpy().copy()
+    m = st.masks[..., 0].cpu().numpy()
+    bm = st.bad_masks[..., 0].cpu().numpy()
+    st.compute_returns(nv, True, 0.99, 0.95, False)
+    eret, ev = O.compute_returns(r, v, m, bm, nv.reshape(-1).cpu().numpy(), True, 0.99, 0.95, False)
+    T = r.shape[0]
+    assert np.array_equal(st.returns[:T, :, 0].cpu().numpy(), eret[:T])
+    assert np.array_equal(st.value_preds[..., 0].cpu().numpy(), ev)
+    adv = st.normalized_advantages()
+    ref = O.normalize_advantages(eret, ev)
+    np.testing.assert_allclose(adv.cpu().numpy(), ref, rtol=1e-6, atol=1e-6)
+    mean, std = O.adv_stats(eret, ev)
+    stats = st._adv_stats.cpu().numpy()
+    np.testing.assert_allclose(stats[1] / stats[0], mean, rtol=1e-6, atol=1e-9)
+    return adv
+
+
+def _check_grads(got_flat, ref_list, shapes, tol=1e-5):
+    got = O.unflatten(got_flat, shapes)
+    for (name, _), ref in zip(shapes, ref_list):
+        ref = ref.detach().cpu().numpy() if torch.is_tensor(ref) else ref
+        err = np.abs(got[name] - ref).max()
+        assert err <= tol * max(np.abs(ref).max(), 1e-6), (name, err, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("N", [4096, 1024])   # c3, c2 (T=128, 8 minibatches)
+def test_cnn_iteration_full_size(gpu, N):
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import SyntheticVecEnv
+    T, H, Mb = 128, 512, 8
+    torch.manual_seed(1)
+    env = SyntheticVecEnv(N, seed=123, p_done=0.01, device=gpu)
+    pol = M.Policy((4, 84, 84), env.action_space, base=M.CNNBase, base_kwargs={"recurrent": False, "hidden_size": H})
+    flat0 = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).clone()
+    pol.to(gpu)
+    st = RolloutStorage(T, N, (4, 84, 84), [0], env.action_space, 1, obs_dtype=torch.uint8, device=gpu)
+    env.reset_into(st.obs[0])
+    nv = _rollout(pol, st, env, T)
+    torch.cuda.synchronize()
+
+    # stored values / log-probs of the rollout vs the float64 forward (strided subset)
+    shapes = O.cnn_param_shapes(H)
+    p64 = O.unflatten(flat0.numpy(), shapes)
+    ts, ns = np.array([0, T // 2, T - 1]), np.arange(0, N, 64)
+    obs = st.obs[ts][:, ns].cpu().numpy().reshape(-1, 4, 84, 84)
+    value, logits, _ = O.cnn_forward(p64, O.decode_obs(obs))
+    c = O.categorical(logits)
+    acts = st.actions[ts][:, ns].cpu().numpy().reshape(-1)
+    lp_ref = np.take_along_axis(c["norm_logits"], acts[:, None], 1)[:, 0]
+    np.testing.assert_allclose(st.value_preds[ts][:, ns].cpu().numpy().reshape(-1), value, atol=1e-4)
+    np.testing.assert_allclose(st.action_log_probs[ts][:, ns].cpu().numpy().reshape(-1), lp_ref, atol=1e-4)
+
+    adv = _check_returns(st, nv)
+
+    # the first minibatch of the update: its gradient vs float64 autograd
+    eng = pol.hip_engine()
+    B = N * T // Mb
+    idx = torch.randperm(N * T)[:B].to(gpu)
+    loss = torch.zeros(4, dtype=torch.float64, device=gpu)
+    cap = _GradCapture()
+    eng.train_minibatch(st, adv, idx, HP, loss, cap)
+    torch.cuda.synchronize()
+    p = TR.unflatten(flat0, H, dtype=torch.float64, device=gpu, requires_grad=True)
+    flat = lambda t: t[:T].reshape(T * N, *t.shape[2:])  # noqa: E731
+    grads, losses = TR.minibatch_grads(p, flat(st.obs), flat(st.actions), flat(st.action_log_probs),
+                                       adv.reshape(-1), flat(st.value_preds), flat(st.returns), idx=idx,
+                                       clip=HP["clip"], value_coef=HP["value_coef"], entropy_coef=HP["entropy_coef"])
+    _check_grads(cap.grad.cpu().numpy(), grads, shapes)
+    np.testing.assert_allclose(loss[:3].cpu().numpy(), losses, rtol=2e-5, atol=1e-7)
+    assert loss[3].item() == 0
+
+
+def test_recurrent_minibatch_full_size(gpu):
+    """c5: GRU H=256 + 14 vector obs; one recurrent_generator minibatch of 512
+    envs x 256 steps (131,072 rows) from a 1024-lane rollout."""
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import SyntheticVecEnv
+    N, T, H, V, n = 1024, 256, 256, 14, 512
+    torch.manual_seed(2)
+    env = SyntheticVecEnv(N, seed=321, p_done=0.01, device=gpu)
+    pol = M.Policy((4, 84, 84), env.action_space, base=M.CNNBase, base_kwargs={"recurrent": True, "hidden_size": H},
+                   vector_obs_len=V)
+    flat0 = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).clone()
+    pol.to(gpu)
+    st = RolloutStorage(T, N, (4, 84, 84), [V], env.action_space, H, obs_dtype=torch.uint8, device=gpu)
+    env.reset_into(st.obs[0])
+    vec = torch.rand(N, V, generator=torch.Generator().manual_seed(3)).to(gpu)
+    st.vector_obs[0].copy_(vec)
+    nv = _rollout(pol, st, env, T, vec=vec)
+    torch.cuda.synchronize()
+    adv = _check_returns(st, nv)
+
+    eng = pol.hip_engine()
+    envs = torch.randperm(N)[:n].to(gpu)
+    loss = torch.zeros(4, dtype=torch.float64, device=gpu)
+    cap = _GradCapture()
+    eng.train_minibatch_rec(st, adv, envs, HP, loss, cap)
+    torch.cuda.synchronize()
+    R = T * n
+    I, Ip = H + V, eng.Ip
+    x = eng.ws["train"].bufs["xpad"][:R * Ip].reshape(R, Ip)[:, :I].double().cpu().numpy()   # the GRU inputs used
+    ev = envs.cpu().numpy()
+    rows = (np.arange(T)[:, None] * N + ev[None, :]).reshape(-1)                             # row t*n + j
+    # the engine's GRU inputs are fc(obs) | vector obs: check them against float64 first
+    shapes = O.cnn_param_shapes(H, recurrent=True, vector_obs_len=V)
+    names = [nm for nm, _ in shapes]
+    p64 = O.unflatten(flat0.numpy(), shapes)
+    trunk_p = [torch.tensor(p64[nm], device=gpu, requires_grad=True) for nm in names[4:12]]
+    obs_flat = st.obs[:T].reshape(T * N, 4, 84, 84)
+    ridx = torch.from_numpy(rows).to(gpu)
+    sub = np.arange(0, R, 97)
+    with torch.no_grad():
+        feat = TR.trunk(trunk_p, obs_flat[ridx[sub]].double() / 255.0, TR.conv_unfold).cpu().numpy()
+    np.testing.assert_allclose(x[sub, :H], feat, rtol=0, atol=2e-5 * max(1.0, np.abs(feat).max()))
+    np.testing.assert_array_equal(x[:, H:], st.vector_obs[:T].reshape(T * N, V).cpu().numpy()[rows].astype(np.float64))
+    # float64 GRU + heads + loss (oracle), BPTT to dL/dx
+    h0 = st.recurrent_hidden_states[0].cpu().numpy()[ev].astype(np.float64)
+    masks = st.masks[:T, :, 0].cpu().numpy()[:, ev].astype(np.float64)
+    out, gcache = O.gru_sequence_cache(p64, x, h0, masks)
+    value, logits = O.heads(p64, out)
+    f = lambda t: t[:T].reshape(-1).cpu().numpy()[rows]  # noqa: E731
+    lg = O.loss_head_grads(value, logits, f(st.actions), f(st.action_log_probs), adv.reshape(-1).cpu().numpy()[rows],
+                           f(st.value_preds), f(st.returns), HP["clip"], HP["value_coef"], HP["entropy_coef"])
+    g = {"base.critic_linear.weight": lg["g_value"][None, :] @ out,
+         "base.critic_linear.bias": np.array([lg["g_value"].sum()]),
+         "dist.linear.weight": lg["g_logits"].T @ out, "dist.linear.bias": lg["g_logits"].sum(0)}
+    dout = lg["g_value"][:, None] * p64["base.critic_linear.weight"] + lg["g_logits"] @ p64["dist.linear.weight"]
+    gg, dx = O.gru_backward(p64, x, masks, gcache, dout)
+    g.update(gg)
+    tg = TR.trunk_grads(trunk_p, obs_flat, torch.from_numpy(dx[:, :H]).to(gpu), idx=ridx)
+    for nm, t in zip(names[4:12], tg):
+        g[nm] = t.cpu().numpy()
+    _check_grads(cap.grad.cpu().numpy(), [g[nm] for nm in names], shapes)
+    np.testing.assert_allclose(loss[:3].cpu().numpy(), [lg["value_loss"], lg["action_loss"], lg["entropy"]],
+                               rtol=2e-5, atol=1e-7)

@@ -306,7 +306,7 @@ def test_loss_and_backward_vs_oracle(gpu, B, H):
     adv = torch.randn(T, N, generator=g).to(gpu)
     idx = torch.randperm(T * N, generator=g)[: (T * N) // 2].to(gpu)
     hp = {"clip": 0.1, "value_coef": 0.5, "entropy_coef": 0.01, "use_clipped_value_loss": True}
-    loss = torch.zeros(3, dtype=torch.float64, device=gpu)
+    loss = torch.zeros(4, dtype=torch.float64, device=gpu)   # 3 losses + bad-action count
     opt = FlatAdam(pol.parameters(), lr=0.0, eps=1e-5, max_grad_norm=None)  # lr 0: grads only
     eng.train_minibatch(st, adv, idx, hp, loss, opt)
     torch.cuda.synchronize()
@@ -325,7 +325,7 @@ def test_loss_and_backward_vs_oracle(gpu, B, H):
         ref = grads[name]
         err = np.abs(got[name] - ref).max()
         assert err <= 1e-5 * max(np.abs(ref).max(), 1e-3), (name, err, np.abs(ref).max())
-    np.testing.assert_allclose(loss.cpu().numpy(), [lg["value_loss"], lg["action_loss"], lg["entropy"]],
+    np.testing.assert_allclose(loss.cpu().numpy()[:3], [lg["value_loss"], lg["action_loss"], lg["entropy"]],
                                rtol=2e-5, atol=1e-6)
 
 
@@ -533,7 +533,7 @@ def test_recurrent_minibatch_grads_vs_oracle(gpu, H, V):
     adv = torch.randn(T, N, generator=g).to(gpu)
     envs = torch.tensor([4, 0, 3], dtype=torch.int64)
     hp = {"clip": 0.1, "value_coef": 0.5, "entropy_coef": 0.01, "use_clipped_value_loss": True}
-    loss = torch.zeros(3, dtype=torch.float64, device=gpu)
+    loss = torch.zeros(4, dtype=torch.float64, device=gpu)   # 3 losses + bad-action count
     opt = FlatAdam(pol.parameters(), lr=0.0, eps=1e-5, max_grad_norm=None)
     eng.train_minibatch_rec(st, adv, envs.to(gpu), hp, loss, opt)
     torch.cuda.synchronize()
@@ -556,7 +556,7 @@ def test_recurrent_minibatch_grads_vs_oracle(gpu, H, V):
         ref = grads[name]
         err = np.abs(got[name] - ref).max()
         assert err <= 2e-5 * max(np.abs(ref).max(), 1e-3), (name, err, np.abs(ref).max())
-    np.testing.assert_allclose(loss.cpu().numpy(), [lg["value_loss"], lg["action_loss"], lg["entropy"]],
+    np.testing.assert_allclose(loss.cpu().numpy()[:3], [lg["value_loss"], lg["action_loss"], lg["entropy"]],
                                rtol=2e-5, atol=1e-6)
 
 
@@ -649,7 +649,7 @@ def test_mlp_minibatch_grads_vs_oracle(gpu, I, V, H, A, B):
     adv = torch.randn(T, N, generator=g).to(gpu)
     idx = torch.randperm(T * N, generator=g)[:B].to(gpu)
     hp = {"clip": 0.1, "value_coef": 0.5, "entropy_coef": 0.01, "use_clipped_value_loss": True}
-    loss = torch.zeros(3, dtype=torch.float64, device=gpu)
+    loss = torch.zeros(4, dtype=torch.float64, device=gpu)   # 3 losses + bad-action count
     opt = FlatAdam(pol.parameters(), lr=0.0, eps=1e-5, max_grad_norm=None)
     eng.train_minibatch(st, adv, idx, hp, loss, opt)
     torch.cuda.synchronize()
@@ -670,7 +670,7 @@ def test_mlp_minibatch_grads_vs_oracle(gpu, I, V, H, A, B):
         ref = grads[name]
         err = np.abs(got[name] - ref).max()
         assert err <= 1e-5 * max(np.abs(ref).max(), 1e-3), (name, err, np.abs(ref).max())
-    np.testing.assert_allclose(loss.cpu().numpy(), [lg["value_loss"], lg["action_loss"], lg["entropy"]],
+    np.testing.assert_allclose(loss.cpu().numpy()[:3], [lg["value_loss"], lg["action_loss"], lg["entropy"]],
                                rtol=2e-5, atol=1e-6)
 
 
@@ -1207,3 +1207,71 @@ def test_conv1_wgrad_variants_vs_torch(gpu, variant):
     for got, ref in ((gw.cpu().double().view(32, 4, 8, 8), ref_w), (gb.cpu().double(), ref_b)):
         err = (got - ref).abs().max().item()
         assert err <= 1e-5 * ref.abs().max().item(), err
+
+
+def _run_procs(cmds, timeout=300):
+    import subprocess
+    procs = [subprocess.Popen(c, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for c in cmds]
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, e[-3000:]
+        outs.append(o)
+    return outs
+
+
+def test_split_minibatch_gradient_equals_single_gpu(tmp_path):
+    """the same global minibatch on one rank, or split over two
+    ranks that each own half of the env lanes (gloo on the one GPU; RCCL takes the
+    same calls on a node), gives the same averaged gradient — global advantage
+    statistics from the 3-double all-reduce, per-rank mean over B/2 rows, Σ/G of
+    the all-reduced flat gradient.  Tolerance: 2e-6 of each tensor's max |g|
+    (only the fp32 summation order differs), losses 1e-6 relative."""
+    import os
+    import socket
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = str(s.getsockname()[1])
+    s.close()
+    worker = os.path.join(os.path.dirname(__file__), "helpers", "split_grad_worker.py")
+    one, two = str(tmp_path / "g1.npz"), str(tmp_path / "g2.npz")
+    _run_procs([[sys.executable, worker, "0", "1", port, one]])
+    _run_procs([[sys.executable, worker, str(r), "2", port, two] for r in range(2)])
+    a, b = np.load(one), np.load(two)
+    np.testing.assert_allclose(b["stats"], a["stats"], rtol=1e-12)
+    np.testing.assert_allclose(b["loss"][:3], a["loss"][:3], rtol=1e-6, atol=1e-9)
+    shapes = O.cnn_param_shapes(128)
+    ga, gb = O.unflatten(a["grad"], shapes), O.unflatten(b["grad"], shapes)
+    for name, _ in shapes:
+        ref = ga[name]
+        err = np.abs(gb[name] - ref).max()
+        assert err <= 2e-6 * max(np.abs(ref).max(), 1e-6), (name, err, np.abs(ref).max())
+
+
+def test_bench_self_launches_ranks():
+    """`bench.py --gpus 2` without a launcher starts its two ranks itself (here
+    both on the one GPU with --dist-backend gloo) and reports n_gpus 2; a
+    WORLD_SIZE that disagrees with --gpus is refused."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "1",
+           "--warmup", "0", "--envs", "64", "--num-steps", "8", "--no-cpu-baseline", "--no-gae-roofline",
+           "--no-boundary", "--no-profile-pass"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
+    assert line["config"]["global_batch"] == 2 * 64 * 8 and line["value"] > 0
+    bad = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run(cmd, env=bad, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "does not match" in r.stderr

@@ -135,3 +135,65 @@ def test_cartpole_restatement_terminates_and_resets():
     assert len(lens) >= N and 5 <= min(lens) and max(lens) <= 30
     st, k, *_ = O.cartpole_step(np.zeros((2, 4)), np.array([0, 9]), np.array([0, 1]), 7, 0, max_steps=10)
     assert list(k) == [1, 0]
+
+
+def test_torch_ref_replays_reference_iteration():
+    """oracle/torch_ref.py (the reference's CPU path restated in torch: the CPU
+    baseline bench.py times, and the float64 gradient of tests/test_full_size.py)
+    replays the recorded reference iteration: same actions (bit-exact), returns,
+    losses and final parameters."""
+    import torch
+    from oracle import torch_ref as TR
+    d = golden("cnn_update.npz")
+    hidden, N, T, E, Mb = (int(x) for x in d["meta"])
+    torch.set_num_threads(1)
+    p = TR.unflatten(torch.from_numpy(d["init_params"]), hidden, requires_grad=True)
+    obs = torch.from_numpy(d["obs_u8"]).float() / 255.0
+    noise = torch.from_numpy(d["exp_noise"])
+    vpred = torch.zeros(T + 1, N, 1)
+    logps = torch.zeros(T, N, 1)
+    actions = torch.zeros(T, N, 1, dtype=torch.int64)
+    masks = torch.ones(T + 1, N, 1)
+    masks[1:] = torch.from_numpy(d["masks"])
+    for t in range(T):
+        with torch.no_grad():
+            v, a, lp = TR.act(p, obs[t], noise=noise[t])
+        vpred[t], actions[t], logps[t] = v, a, lp
+    assert np.array_equal(actions.numpy(), d["actions"])
+    np.testing.assert_allclose(logps.numpy(), d["action_log_probs"], atol=1e-6)
+    with torch.no_grad():
+        nv, _ = TR.cnn_forward(p, obs[-1])
+    ret = TR.compute_returns(torch.from_numpy(d["rewards"]), vpred, masks, nv, 0.99, 0.95)
+    np.testing.assert_allclose(ret.numpy(), d["returns"], atol=1e-6)
+    opt = torch.optim.Adam(p, lr=float(d["lr"][0]), eps=1e-5)
+    losses = TR.ppo_update(p, opt, obs, actions, logps, vpred, ret, ppo_epoch=E, num_mini_batch=Mb, clip=0.1,
+                           value_coef=0.5, entropy_coef=0.001, max_grad_norm=0.5, perms=torch.from_numpy(d["perms"]))
+    np.testing.assert_allclose(losses, d["losses"], rtol=1e-5, atol=1e-7)
+    final = torch.cat([t.detach().reshape(-1) for t in p]).numpy()
+    np.testing.assert_allclose(final, d["final_params"], rtol=0, atol=1e-6)
+
+
+def test_torch_ref_minibatch_grads_match_oracle():
+    """torch_ref.minibatch_grads (chunked float64 autograd) equals the oracle's
+    analytic float64 backward on the same minibatch (independent derivations)."""
+    import torch
+    from oracle import torch_ref as TR
+    rng = np.random.default_rng(8)
+    H, B = 64, 12
+    shapes = O.cnn_param_shapes(H)
+    flat = np.concatenate([rng.standard_normal(int(np.prod(s))) * 0.05 for _, s in shapes])
+    obs = rng.integers(0, 256, (B, 4, 84, 84), dtype=np.uint8)
+    act = rng.integers(0, 8, B)
+    olp, adv = np.log(rng.random(B)) * 0.3 - 2.0, rng.standard_normal(B)
+    vp, ret = rng.standard_normal(B) * 0.1, rng.standard_normal(B)
+    p = TR.unflatten(torch.from_numpy(flat), H, dtype=torch.float64, requires_grad=True)
+    t = lambda a: torch.from_numpy(np.asarray(a))  # noqa: E731
+    grads, losses = TR.minibatch_grads(p, t(obs), t(act), t(olp), t(adv), t(vp), t(ret), clip=0.1, value_coef=0.5,
+                                       entropy_coef=0.01, chunk=5)
+    po = O.unflatten(flat, shapes)
+    value, logits, cache = O.cnn_forward(po, obs.astype(np.float64) / 255.0)
+    lg = O.loss_head_grads(value, logits, act, olp, adv, vp, ret, 0.1, 0.5, 0.01)
+    ref = O.cnn_backward(po, cache, lg["g_value"], lg["g_logits"])
+    for (name, _), g in zip(shapes, grads):
+        np.testing.assert_allclose(g.numpy(), ref[name], rtol=1e-9, atol=1e-12 * max(1.0, np.abs(ref[name]).max()))
+    np.testing.assert_allclose(losses, [lg["value_loss"], lg["action_loss"], lg["entropy"]], rtol=1e-10)
