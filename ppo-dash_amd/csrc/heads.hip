@@ -146,7 +146,7 @@ __global__ __launch_bounds__(64 * HW) void heads_act_kernel(
     float lp = (unsigned)act < (unsigned)A ? 0.f : __int_as_float(0x7fc00000), ent = 0.f;
 #pragma unroll
     for (int o = 0; o < AMAX; ++o) {
-      if (o == act) lp = nl[o];
+      if (o == act && o < A) lp = nl[o];
       if (o < A) ent -= nl[o] * p[o];
     }
     if (lane == 0) {
