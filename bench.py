@@ -172,7 +172,39 @@ def gae_roofline(device, lanes, T=128, reps=10):
     return {"bound": "hbm", "achieved": round(gbps, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
             "frac": round(gbps / PEAK_HBM_GBPS, 4), "traffic": None,
             "config": f"T={T} x {lanes} lanes (fp32 planes, {nbytes / 1e9:.2f} GB algorithmic per launch)",
-            "ms_per_launch": round(ms, 4)}
+            "ms_per_launch": round(ms, 4), "small_shapes": gae_small(device)}
+
+
+def gae_small(device, T=128, reps=50):
+    """c1 / c2-sized compute_returns (8 and 1024 lanes): the bit-exact
+    lane-sequential kernel (one thread per lane walks T steps) vs the
+    time-parallel scan (16 lanes x 16 time chunks per block), µs per launch."""
+    from a2c_ppo_acktr._hip import call, stream
+    out = {}
+    for lanes in (8, 1024, 4096):
+        g = torch.Generator(device=device).manual_seed(1)
+        r = torch.rand(T, lanes, device=device, generator=g)
+        v = torch.randn(T + 1, lanes, device=device, generator=g)
+        m = torch.ones(T + 1, lanes, device=device)
+        nv = torch.randn(lanes, device=device, generator=g)
+        ret = torch.empty(T + 1, lanes, device=device)
+        adv = torch.empty(T, lanes, device=device)
+        parts = torch.empty(2 * lanes, dtype=torch.float64, device=device)
+        res = {}
+        for name in ("ppo_compute_returns", "ppo_compute_returns_scan"):
+            args = (r.data_ptr(), v.data_ptr(), m.data_ptr(), m.data_ptr(), nv.data_ptr(), ret.data_ptr(),
+                    adv.data_ptr(), parts.data_ptr(), T, lanes, 0.99, 0.95, 1, 0, stream())
+            call(name, *args)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                call(name, *args)
+            e1.record()
+            torch.cuda.synchronize()
+            res["scan_us" if name.endswith("scan") else "exact_us"] = round(e0.elapsed_time(e1) / reps * 1e3, 2)
+        out[f"{lanes}x{T}"] = res
+    return out
 
 
 def boundary_roofline(device, frames=16384, reps=5, cpu_frames=64):

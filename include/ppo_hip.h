@@ -48,6 +48,14 @@ int ppo_gae_partials_count(int N);
 int ppo_compute_returns(const float* rewards, float* value_preds, const float* masks, const float* bad_masks,
                         const float* next_value, float* returns, float* adv, double* partials, int T, int N,
                         double gamma, double gae_lambda, int use_gae, int use_proper_time_limits, void* stream);
+/* time-parallel compute_returns (same arguments and side effects; within
+ * tolerance, not bit-exact): each lane's affine recurrence folded per time chunk,
+ * chunk carries composed through LDS — for few lanes / long T (c1, c2);
+ * partials: 2*ppo_gae_scan_partials_count(N) doubles */
+int ppo_gae_scan_partials_count(int N);
+int ppo_compute_returns_scan(const float* rewards, float* value_preds, const float* masks, const float* bad_masks,
+                             const float* next_value, float* returns, float* adv, double* partials, int T, int N,
+                             double gamma, double gae_lambda, int use_gae, int use_proper_time_limits, void* stream);
 /* algo/ppo.py:35 advantages = returns[:-1] - value_preds[:-1] (+ partials) */
 int ppo_adv_diff_partials_count(long long n);
 int ppo_adv_diff(const float* returns, const float* value_preds, float* adv, double* partials, long long n,

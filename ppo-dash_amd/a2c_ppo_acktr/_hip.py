@@ -25,6 +25,8 @@ SIGNATURES = {
     # gae.hip
     "ppo_gae_partials_count": [c_int],
     "ppo_compute_returns": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_d, c_d, c_int, c_int, c_p],
+    "ppo_gae_scan_partials_count": [c_int],
+    "ppo_compute_returns_scan": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_d, c_d, c_int, c_int, c_p],
     "ppo_adv_diff_partials_count": [c_ll],
     "ppo_adv_diff": [c_p, c_p, c_p, c_p, c_ll, c_p],
     "ppo_adv_finalize": [c_p, c_int, c_d, c_p, c_p],
@@ -96,7 +98,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"ppo_last_error": ctypes.c_char_p, "ppo_packed_weights_size": c_ll}
 # functions whose int return value is a result, not a status
-_VALUE_FUNCS = {"ppo_abi_version", "ppo_gae_partials_count", "ppo_adv_diff_partials_count",
+_VALUE_FUNCS = {"ppo_abi_version", "ppo_gae_partials_count", "ppo_gae_scan_partials_count", "ppo_adv_diff_partials_count",
                 "ppo_packed_weights_size", "ppo_wgrad_splits", "ppo_heads_train_blocks", "ppo_grad_partials_count",
                 "ppo_conv2_dgrad_bits_ok", "ppo_conv3_dgrad_bits_ok"}
 

@@ -12,6 +12,11 @@ Extensions (keyword-only, defaults keep the reference's behaviour):
   obs_dtype=torch.uint8  store observations as raw bytes (4x less HBM than the
                          reference's fp32); Policy decodes u8/255 inside conv1.
   device=...             allocate directly on the device (skips the host copy).
+  gae_mode="exact"       compute_returns kernel: "exact" (default) walks each lane
+                         sequentially in the reference's op order (bit-identical);
+                         "scan" is the time-parallel affine scan (within fp32
+                         tolerance; fills the GPU when there are few lanes, e.g.
+                         c1's 8 or c2's 1024); "auto" picks scan below 16,384 lanes.
 """
 import torch
 
@@ -26,7 +31,10 @@ def _flatten_helper(T, N, _tensor):
 
 class RolloutStorage(object):
     def __init__(self, num_steps, num_processes, obs_shape, vector_obs_shape, action_space,
-                 recurrent_hidden_state_size, *, obs_dtype=torch.float32, device=None):
+                 recurrent_hidden_state_size, *, obs_dtype=torch.float32, device=None, gae_mode="exact"):
+        if gae_mode not in ("exact", "scan", "auto"):
+            raise ValueError(f"gae_mode {gae_mode!r}: 'exact', 'scan' or 'auto'")
+        self.gae_mode = gae_mode
         kw = {} if device is None else {"device": device}
         self.obs = torch.zeros(num_steps + 1, num_processes, *obs_shape, dtype=obs_dtype, **kw)
         self.vector_obs = torch.zeros(num_steps + 1, num_processes, *vector_obs_shape, **kw)
@@ -136,17 +144,19 @@ class RolloutStorage(object):
         if nv.numel() != N:
             raise RuntimeError(f"next_value has {nv.numel()} elements, expected {N}")
         self._ensure_adv(T, N)
-        call("ppo_compute_returns", self.rewards.data_ptr(), self.value_preds.data_ptr(), self.masks.data_ptr(),
-             self.bad_masks.data_ptr(), nv.data_ptr(), self.returns.data_ptr(), self._adv.data_ptr(),
-             self._adv_partials.data_ptr(), T, N, float(gamma), float(gae_lambda), int(bool(use_gae)),
-             int(bool(use_proper_time_limits)), stream())
+        scan = self.gae_mode == "scan" or (self.gae_mode == "auto" and N < 16384)
+        call("ppo_compute_returns_scan" if scan else "ppo_compute_returns", self.rewards.data_ptr(),
+             self.value_preds.data_ptr(), self.masks.data_ptr(), self.bad_masks.data_ptr(), nv.data_ptr(),
+             self.returns.data_ptr(), self._adv.data_ptr(), self._adv_partials.data_ptr(), T, N, float(gamma),
+             float(gae_lambda), int(bool(use_gae)), int(bool(use_proper_time_limits)), stream())
         self._adv_key = (self.returns._version, self.value_preds._version)
         self._adv_ready = True
-        self._adv_nparts = call("ppo_gae_partials_count", N)
+        self._adv_nparts = call("ppo_gae_scan_partials_count" if scan else "ppo_gae_partials_count", N)
 
     def _ensure_adv(self, T, N):
         dev = self.value_preds.device
-        nparts = max(call("ppo_gae_partials_count", N), call("ppo_adv_diff_partials_count", T * N))
+        nparts = max(call("ppo_gae_partials_count", N), call("ppo_gae_scan_partials_count", N),
+                     call("ppo_adv_diff_partials_count", T * N))
         if self._adv is None or self._adv.shape != (T, N) or self._adv.device != dev:
             self._adv = torch.empty(T, N, device=dev)
             self._adv_partials = torch.empty(2 * nparts, dtype=torch.float64, device=dev)

@@ -109,6 +109,111 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Time-parallel mode (tolerance, not bit-exact): for few lanes (c1: 8, c2: 1024)
+// the lane-sequential kernel above occupies 1-4 CUs for T dependent steps.  The
+// recurrence is affine in the carry,
+//   GAE:      g_t   = (δ_t + (γλ·m_{t+1})·g_{t+1})·bm_{t+1}      ret_t = g_t + v_t
+//   returns:  ret_t = (γ·m_{t+1}·ret_{t+1} + r_t)·bm_{t+1} + (1 − bm_{t+1})·v_t
+// i.e. x_t = a_t + b_t·x_{t+1}, and affine maps compose:  (A, B) after (a, b)
+// = (a + b·A, b·B).  A block holds SCAN_LANES consecutive lanes x SCAN_CH time
+// chunks (one thread each; the lanes of a chunk row read 64 contiguous bytes):
+//   1. every thread folds its chunk into one map (A_c, B_c)       (T/CH steps)
+//   2. the carry entering chunk c is the composition of chunks > c applied to
+//      x_T, through LDS                                            (≤ CH-1 steps)
+//   3. every thread re-walks its chunk from that carry and writes returns (+ adv
+//      and its moment partials).
+// Only the association of the sums changes: |err| ~ T·ε·max|x| (tests hold it
+// to the bit-exact kernel within 2e-6 of max|returns|).
+constexpr int SCAN_LANES = 16;
+constexpr int SCAN_CH = 16;
+
+template <bool USE_GAE, bool PTL>
+__device__ __forceinline__ void gae_affine(const float* __restrict__ rewards, const float* __restrict__ value_preds,
+                                           const float* __restrict__ masks, const float* __restrict__ bad_masks,
+                                           float nv, size_t NN, int n, int t, int T, float g, float gl, float& a,
+                                           float& b, float& v) {
+  const float r = rewards[(size_t)t * NN + n];
+  const float m = masks[(size_t)(t + 1) * NN + n];
+  const float bm = PTL ? bad_masks[(size_t)(t + 1) * NN + n] : 1.0f;
+  v = value_preds[(size_t)t * NN + n];
+  if (USE_GAE) {
+    const float vn = t + 1 < T ? value_preds[(size_t)(t + 1) * NN + n] : nv;
+    const float delta = (r + (g * vn) * m) - v;
+    a = PTL ? delta * bm : delta;
+    b = PTL ? (gl * m) * bm : gl * m;
+  } else {
+    a = PTL ? r * bm + (1.0f - bm) * v : r;
+    b = PTL ? (g * m) * bm : g * m;
+  }
+}
+
+template <bool USE_GAE, bool PTL, bool FUSE_ADV>
+__global__ __launch_bounds__(SCAN_LANES * SCAN_CH) void gae_scan_kernel(
+    const float* __restrict__ rewards, float* __restrict__ value_preds, const float* __restrict__ masks,
+    const float* __restrict__ bad_masks, const float* __restrict__ next_value, float* __restrict__ returns,
+    float* __restrict__ adv, double* __restrict__ partials, int T, int N, float g, float gl) {
+  const int l = threadIdx.x % SCAN_LANES, c = threadIdx.x / SCAN_LANES;
+  const int n = blockIdx.x * SCAN_LANES + l;
+  const int L = (T + SCAN_CH - 1) / SCAN_CH;
+  const int t_lo = c * L, t_hi = min(T, t_lo + L);
+  const size_t NN = (size_t)N;
+  __shared__ float mapA[SCAN_CH][SCAN_LANES], mapB[SCAN_CH][SCAN_LANES];
+  const bool live = n < N;
+  const float nv = live ? next_value[n] : 0.0f;
+  // 1. this chunk's composite map x_{t_lo} = A + B·x_{t_hi}
+  float A = 0.0f, B = 1.0f;
+  if (live) {
+    for (int t = t_hi - 1; t >= t_lo; --t) {
+      float a, b, v;
+      gae_affine<USE_GAE, PTL>(rewards, value_preds, masks, bad_masks, nv, NN, n, t, T, g, gl, a, b, v);
+      A = a + b * A;
+      B = b * B;
+    }
+  }
+  mapA[c][l] = A;
+  mapB[c][l] = B;
+  __syncthreads();
+  // 2. carry entering this chunk from above: x_T, then the chunks after this one
+  float x = USE_GAE ? 0.0f : nv;
+  for (int k = SCAN_CH - 1; k > c; --k) x = mapA[k][l] + mapB[k][l] * x;
+  // 3. re-walk with the carry; the storage side effects of the exact kernel
+  double s = 0.0, q = 0.0;
+  if (live) {
+    if (t_lo < T && t_hi == T) {   // the last non-empty chunk
+      if (USE_GAE) value_preds[(size_t)T * NN + n] = nv;   // storage.py:90/:108
+      else returns[(size_t)T * NN + n] = nv;               // storage.py:101/:118
+    }
+    for (int t = t_hi - 1; t >= t_lo; --t) {
+      float a, b, v;
+      gae_affine<USE_GAE, PTL>(rewards, value_preds, masks, bad_masks, nv, NN, n, t, T, g, gl, a, b, v);
+      x = a + b * x;
+      const float out = USE_GAE ? x + v : x;
+      returns[(size_t)t * NN + n] = out;
+      if (FUSE_ADV) {
+        const float d = out - v;
+        adv[(size_t)t * NN + n] = d;
+        s += (double)d;
+        q += (double)d * (double)d;
+      }
+    }
+  }
+  if (FUSE_ADV) {
+    __shared__ double red[2][SCAN_LANES * SCAN_CH / 64];
+    s = wave_sum_d(s);
+    q = wave_sum_d(q);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = s; red[1][w] = q; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double ss = 0.0, qq = 0.0;
+      for (int i = 0; i < SCAN_LANES * SCAN_CH / 64; ++i) { ss += red[0][i]; qq += red[1][i]; }
+      partials[2 * blockIdx.x] = ss;
+      partials[2 * blockIdx.x + 1] = qq;
+    }
+  }
+}
+
 // adv = returns - value_preds over the first T rows, plus moment partials
 // (used when storage was modified after compute_returns).
 __global__ __launch_bounds__(256) void adv_diff_kernel(const float* __restrict__ returns,
@@ -185,9 +290,49 @@ int launch_gae(const float* r, float* v, const float* m, const float* bm, const 
   return 0;
 }
 
+template <bool G, bool P, bool F>
+int launch_gae_scan(const float* r, float* v, const float* m, const float* bm, const float* nv, float* ret,
+                    float* adv, double* partials, int T, int N, float g, float gl, hipStream_t st) {
+  gae_scan_kernel<G, P, F><<<ceil_div(N, SCAN_LANES), SCAN_LANES * SCAN_CH, 0, st>>>(r, v, m, bm, nv, ret, adv,
+                                                                                      partials, T, N, g, gl);
+  PPO_LAUNCH_CHECK("gae_scan_kernel");
+  return 0;
+}
+
 }  // namespace
 
 PPO_API int ppo_gae_partials_count(int N) { return (int)ceil_div(N, GAE_THREADS); }
+PPO_API int ppo_gae_scan_partials_count(int N) { return (int)ceil_div(N, SCAN_LANES); }
+
+// Time-parallel compute_returns (same arguments and side effects as
+// ppo_compute_returns; partials: 2*ppo_gae_scan_partials_count(N) doubles).
+// Within tolerance of the bit-exact kernel, for few lanes / long T.
+PPO_API int ppo_compute_returns_scan(const float* rewards, float* value_preds, const float* masks,
+                                     const float* bad_masks, const float* next_value, float* returns, float* adv,
+                                     double* partials, int T, int N, double gamma, double gae_lambda, int use_gae,
+                                     int use_proper_time_limits, void* stream) {
+  PPO_REQUIRE(T > 0 && N > 0, "ppo_compute_returns_scan: bad shape T=%d N=%d", T, N);
+  PPO_REQUIRE(rewards && value_preds && masks && next_value && returns, "ppo_compute_returns_scan: null pointer");
+  PPO_REQUIRE(!use_proper_time_limits || bad_masks, "ppo_compute_returns_scan: bad_masks required");
+  PPO_REQUIRE((adv == nullptr) == (partials == nullptr), "ppo_compute_returns_scan: adv and partials go together");
+  ProfScope prof("gae_scan", as_stream(stream), (adv ? 20.0 : 16.0) * T * N);
+  const float g = (float)gamma;
+  const float gl = (float)(gamma * gae_lambda);
+  hipStream_t st = as_stream(stream);
+  const bool F = adv != nullptr;
+#define PPO_SCAN(G_, P_)                                                                                         \
+  return F ? launch_gae_scan<G_, P_, true>(rewards, value_preds, masks, bad_masks, next_value, returns, adv,    \
+                                          partials, T, N, g, gl, st)                                            \
+           : launch_gae_scan<G_, P_, false>(rewards, value_preds, masks, bad_masks, next_value, returns, adv,   \
+                                           partials, T, N, g, gl, st);
+  if (use_gae) {
+    if (use_proper_time_limits) PPO_SCAN(true, true)
+    PPO_SCAN(true, false)
+  }
+  if (use_proper_time_limits) PPO_SCAN(false, true)
+  PPO_SCAN(false, false)
+#undef PPO_SCAN
+}
 
 // storage.py:82-121 (+ ppo.py:35 when adv != NULL).  value_preds[T] is
 // overwritten with next_value in the GAE branches, returns[T] with next_value

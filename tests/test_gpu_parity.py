@@ -1275,3 +1275,64 @@ def test_bench_self_launches_ranks():
     bad = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run(cmd, env=bad, capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "does not match" in r.stderr
+
+
+@pytest.mark.parametrize("use_gae", [True, False])
+@pytest.mark.parametrize("ptl", [True, False])
+@pytest.mark.parametrize("T,N", [(128, 8), (128, 1024), (77, 1031), (5, 1), (300, 33), (1, 17)])
+def test_gae_time_parallel_scan(gpu, use_gae, ptl, T, N):
+    """ppo_compute_returns_scan (time-parallel affine scan, storage.py:82-121 in
+    every branch) vs the C oracle (the reference's fp32 op order): returns within
+    2e-6 of max|returns| (reassociation only), the storage side effect on
+    value_preds[T] / returns[T] exact, fused advantages + moments vs the oracle."""
+    H = _hip()
+    rng = np.random.default_rng(T * 31 + N + 7 * use_gae + ptl)
+    r = rng.random((T, N), np.float32)
+    v = (3 * rng.standard_normal((T + 1, N))).astype(np.float32)
+    m = (rng.random((T + 1, N)) > 0.05).astype(np.float32)
+    bm = (rng.random((T + 1, N)) > 0.05).astype(np.float32)
+    nv = rng.standard_normal(N).astype(np.float32)
+    rd, vd, md, bmd, nvd = _dev(r), _dev(v), _dev(m), _dev(bm), _dev(nv)
+    ret = torch.zeros(T + 1, N, device=gpu)
+    adv = torch.zeros(T, N, device=gpu)
+    nparts = H.call("ppo_gae_scan_partials_count", N)
+    parts = torch.zeros(2 * nparts, dtype=torch.float64, device=gpu)
+    stats = torch.zeros(3, dtype=torch.float64, device=gpu)
+    H.call("ppo_compute_returns_scan", rd.data_ptr(), vd.data_ptr(), md.data_ptr(), bmd.data_ptr(), nvd.data_ptr(),
+           ret.data_ptr(), adv.data_ptr(), parts.data_ptr(), T, N, 0.99, 0.95, int(use_gae), int(ptl), _s())
+    H.call("ppo_adv_finalize", parts.data_ptr(), nparts, float(T * N), stats.data_ptr(), _s())
+    eret, ev = O.compute_returns(r, v, m, bm, nv, use_gae, 0.99, 0.95, ptl)
+    got = ret.cpu().numpy()
+    scale = np.abs(eret[:T]).max()
+    np.testing.assert_allclose(got[:T], eret[:T], rtol=0, atol=2e-6 * scale)
+    assert np.array_equal(vd.cpu().numpy(), ev)               # value_preds[T] = next_value (GAE)
+    if not use_gae:
+        assert np.array_equal(got[T], nv)                     # returns[T] = next_value
+    d = got[:T].astype(np.float64) - v[:T]
+    np.testing.assert_allclose(adv.cpu().numpy(), d, rtol=0, atol=2e-6 * scale)
+    st = stats.cpu().numpy()
+    np.testing.assert_allclose(st[1], d.sum(), rtol=1e-6, atol=1e-6 * scale * d.size)
+
+
+def test_storage_gae_mode_scan(gpu):
+    """RolloutStorage(gae_mode="scan") drives the time-parallel kernel through the
+    drop-in API at c2's shape: returns and normalised advantages within
+    tolerance of the bit-exact default."""
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import Discrete
+    T, N = 128, 1024
+    g = torch.Generator().manual_seed(3)
+    outs = []
+    for mode in ("exact", "scan"):
+        st = RolloutStorage(T, N, (4, 84, 84), [0], Discrete(8), 1, obs_dtype=torch.uint8, device=gpu, gae_mode=mode)
+        g.manual_seed(3)
+        st.rewards.copy_(torch.rand(T, N, 1, generator=g))
+        st.value_preds.copy_(torch.randn(T + 1, N, 1, generator=g))
+        st.masks.copy_((torch.rand(T + 1, N, 1, generator=g) > 0.01).float())
+        st.compute_returns(torch.randn(N, 1, generator=g).to(gpu), True, 0.99, 0.95, False)
+        outs.append((st.returns.cpu().numpy(), st.normalized_advantages().cpu().numpy()))
+    scale = np.abs(outs[0][0]).max()
+    np.testing.assert_allclose(outs[1][0], outs[0][0], rtol=0, atol=2e-6 * scale)
+    np.testing.assert_allclose(outs[1][1], outs[0][1], rtol=0, atol=1e-5)
+    with pytest.raises(ValueError):
+        RolloutStorage(T, N, (4, 84, 84), [0], Discrete(8), 1, device=gpu, gae_mode="fast")
