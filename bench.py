@@ -59,8 +59,10 @@ PEAK_HBM_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # ceiling is the dense bf16 peak / P in fp32-FLOP units.
 def profiled(products):
     split = (f"v_mfma_f32_16x16x32_bf16 x{products} "
-             + ("(exact split)" if products == 9 else "(split, 6 products: fp32-accurate)"))
+             + {9: "(exact split)", 6: "(split, 6 products: fp32-accurate)",
+                1: "(half-precision mode: bf16 operands)"}[products])
     pk = PEAK_BF16_MFMA_TFLOPS / products
+    u8 = 1 if products == 1 else 3   # conv1: weight parts against the exact u8 pixels
 
     def mf(how):
         return ("mfma", pk, "flop", split + how)
@@ -75,8 +77,8 @@ def profiled(products):
         "conv3_dgrad": mf(", image-resident"),
         "conv3_wgrad": mf(", image-resident, ds_read_b64_tr_b16 im2col"),
         # u8 pixels are exact in bf16: 3 products per fp32 product
-        "conv1_wgrad_u8": ("mfma", PEAK_BF16_MFMA_TFLOPS / 3, "flop",
-                           "v_mfma_f32_32x32x16_bf16 x3 (u8 exact), image-resident"),
+        "conv1_wgrad_u8": ("mfma", PEAK_BF16_MFMA_TFLOPS / u8, "flop",
+                           f"v_mfma_f32_32x32x16_bf16 x{u8} (u8 exact), image-resident"),
         # conv1 forward: 79,424 B of compulsory HBM traffic per sample (28,224 B u8 in, 51,200 B f32 out)
         # against 6.55 MFLOP at bf16/3 -> HBM-bound
         "conv1_fwd_u8": ("hbm", PEAK_HBM_GBPS, "conv1_flop", "v_mfma_f32_16x16x32_bf16 x3 (u8 exact), image-resident"),
@@ -129,6 +131,9 @@ def parse():
                    help="skip the profiled iteration after the timed region (per-kernel breakdown)")
     p.add_argument("--products", type=int, default=6, choices=(6, 9),
                    help="part products per fp32 product in the split-bf16 GEMMs (9 = every product exact)")
+    p.add_argument("--half-precision", action="store_true",
+                   help="T/run.py --half-precision: Policy.half() (one bf16 MFMA product per GEMM product, fp32 "
+                        "accumulation and masters) — a separate line, never the fp32 headline")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-envs", type=int, default=32)
     p.add_argument("--cpu-threads", type=int, default=None,
@@ -505,6 +510,8 @@ def main():
     policy = Policy((4, 84, 84), env.action_space, base=CNNBase,
                     base_kwargs={"recurrent": args.recurrent, "hidden_size": H}, vector_obs_len=V)
     policy.to(device)
+    if args.half_precision:
+        policy.half()
     agent = PPO(policy, 0.1, E, M, 0.5, 0.001, lr=1e-4, eps=1e-5, max_grad_norm=0.5)
     rollouts = RolloutStorage(T, N, (4, 84, 84), [V], env.action_space, policy.recurrent_hidden_state_size,
                               obs_dtype=torch.uint8, device=device)
@@ -585,14 +592,16 @@ def main():
 
     workload = ((f"c5: CNNBase+GRU H={H} + {V} vector obs" if args.recurrent else f"c3: CNNBase H={H}")
                 + f", {N} env lanes x {T} steps per GPU, PPO {E} epochs x {M} minibatches "
-                  f"(rollout + GAE + update, fp32)")
+                  f"(rollout + GAE + update, " + ("--half-precision: bf16 GEMM operands, fp32 accumulation"
+                                                  if args.half_precision else "fp32") + ")")
     kernels = {}
+    products = 1 if args.half_precision else args.products
     for name, (launches, ms_total, work) in per_kernel.items():
         if launches > 0 and ms_total > 0:
-            kernels[name] = kernel_entry(name, launches, ms_total, work, args.products, "timed region")
+            kernels[name] = kernel_entry(name, launches, ms_total, work, products, "timed region")
     for name, (launches, ms_total, work) in pass_kernels.items():
         if launches > 0 and ms_total > 0:
-            e = kernel_entry(name, launches, ms_total, work, args.products, "profile pass")
+            e = kernel_entry(name, launches, ms_total, work, products, "profile pass")
             e["ms_per_iteration"] = round(ms_total, 3)
             if name in kernels:
                 kernels[name]["ms_per_iteration"] = e["ms_per_iteration"]
@@ -622,7 +631,8 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "split_products": args.products,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.half_precision else "f32",
+        "split_products": 1 if args.half_precision else args.products,
         "data": "synthetic: counter-hash u8 4x84x84 obs, U[0,1) rewards, Bernoulli(0.01) dones; random-init weights",
         "config": {"workload": workload,
                    "envs_per_gpu": N, "num_steps": T, "ppo_epoch": E, "num_mini_batch": M, "hidden": H,

@@ -77,6 +77,10 @@ int ppo_storage_insert_scalars(int N, int step, const int64_t* action, const flo
 /* storage.py:143-157 feed_forward_generator `[indices]` row gathers */
 int ppo_gather_rows(const void* src, const int64_t* idx, void* dst, long long nrows, long long row_bytes,
                     void* stream);
+/* half-precision storage (storage.py:48-58 RolloutStorage.half()): fp16 observation
+ * rows src[idx[r]] (idx NULL: row r) -> fp32 rows for the conv1 loaders */
+int ppo_gather_f16_to_f32(const void* src, const int64_t* idx, float* dst, long long nrows, long long row_elems,
+                          void* stream);
 /* storage.py:181-205 recurrent_generator env-column stacking */
 int ppo_gather_env_columns(const void* src, const int64_t* envs, void* dst, int T, int N, int nsel,
                            long long row_bytes, void* stream);

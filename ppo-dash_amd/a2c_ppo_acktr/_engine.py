@@ -25,6 +25,25 @@ from ._hip import call, ptr, stream
 FEAT = 32 * 7 * 7  # conv3 output, flattened
 
 
+def _with_precision(fn):
+    """Run an engine entry point at the policy's arithmetic precision: the split
+    GEMMs' part-product count is 6 (fp32-accurate) normally and 1 — bf16-rounded
+    operands, fp32 accumulation — after Policy.half() (T/run.py:84-85)."""
+    def wrapper(self, *args, **kwargs):
+        if not getattr(self.policy, "_half_mode", False):
+            return fn(self, *args, **kwargs)
+        prev = call("ppo_tune_get", b"products")
+        if prev != 1:
+            call("ppo_tune_set", b"products", 1)
+        try:
+            return fn(self, *args, **kwargs)
+        finally:
+            if prev != 1:
+                call("ppo_tune_set", b"products", prev)
+    wrapper.__name__, wrapper.__doc__ = fn.__name__, fn.__doc__
+    return wrapper
+
+
 class _Workspace:
     def __init__(self):
         self.bufs = {}
@@ -141,13 +160,25 @@ class CNNEngine:
             return 1
         if obs.dtype == torch.float32:
             return 0
-        raise TypeError(f"observations must be uint8 or float32, got {obs.dtype}")
+        raise TypeError(f"observations must be uint8, float32 or float16, got {obs.dtype}")
+
+    def _obs_f32(self, obs, idx, B, ws):
+        """fp16 observations (RolloutStorage.half(), storage.py:48-58): the rows the
+        trunk reads (idx into the plane, or the batch) converted to an fp32
+        workspace; u8 / fp32 observations pass through."""
+        if obs.dtype != torch.float16:
+            return obs, idx
+        x = ws.get("obs32", B * self.C * 84 * 84, device=self.device)
+        call("ppo_gather_f16_to_f32", obs.data_ptr(), ptr(idx, torch.int64, "idx"), x.data_ptr(), B,
+             self.C * 84 * 84, stream())
+        return x, None
 
     def trunk(self, obs, idx, B, ws, out=None, ldo=None):
         """conv1..fc on B samples: obs is either a [B,C,84,84] batch (idx None) or the
         storage plane whose rows idx[b] are gathered inside conv1.  Writes the fc
         output (post-ReLU) to `out` (row stride ldo) or a workspace [B,H]."""
         dev = self.device
+        obs, idx = self._obs_f32(obs, idx, B, ws)
         is_u8 = self._obs_args(obs)
         a1 = ws.get("a1", B * 400 * 32, device=dev)
         a2 = ws.get("a2", B * 81 * 64, device=dev)
@@ -206,6 +237,7 @@ class CNNEngine:
         call("ppo_mean_f32", x.data_ptr(), x.numel(), out.data_ptr(), stream())
         return out
 
+    @_with_precision
     def act(self, obs, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False):
         self.ensure_bound()
         self.pack()
@@ -253,6 +285,8 @@ class CNNEngine:
         else:
             call("ppo_conv2_dgrad", dz2.data_ptr(), B, self.pk(5), a1.data_ptr(), dz1.data_ptr(), s)
         self._wgrad("conv2", B, dz2, a1, None, s)
+        if obs.dtype == torch.float16:   # the rows trunk() converted for this minibatch
+            obs, idx = ws.bufs["obs32"], None
         self._wgrad("conv1", B, dz1, obs, idx, s)
 
     def _finish_step(self, optimizer):
@@ -260,6 +294,7 @@ class CNNEngine:
         self.epoch += 1
         self.pack(force=True)
 
+    @_with_precision
     def train_minibatch(self, storage, adv, idx, hp, loss_acc, optimizer):
         """Forward + backward + (all-reduce) + clip + Adam for one minibatch of
         storage rows idx (int64 [B], device)."""
@@ -361,6 +396,7 @@ class RecurrentEngine(CNNEngine):
             return None
         return vec.to(self.device, torch.float32).reshape(B, self.V).contiguous()
 
+    @_with_precision
     def act(self, obs, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False,
             vec=None, hxs=None, masks=None):
         """Single step (model.py:112-115): returns (value, action, logp, entropy, hxs')."""
@@ -378,6 +414,7 @@ class RecurrentEngine(CNNEngine):
         value, action, logp, ent = self._heads(hout, B, deterministic, noise, given, want_entropy, value_only)
         return value, action, logp, ent, hout
 
+    @_with_precision
     def evaluate_sequence(self, obs, vec, hxs, masks, action):
         """Multi-step branch (model.py:116-165): rows are t*N + n."""
         self.ensure_bound()
@@ -397,6 +434,7 @@ class RecurrentEngine(CNNEngine):
         value, _, logp, ent = self._heads(hout, R, given=action.to(self.device, torch.int64), want_entropy=True)
         return value, logp, ent, hout[(T - 1) * N:]
 
+    @_with_precision
     def train_minibatch_rec(self, storage, adv, envs, hp, loss_acc, optimizer):
         """recurrent_generator minibatch (storage.py:162-223): whole T-sequences of
         the n envs `envs` (int64 device), BPTT over the full T, then one Adam step."""
@@ -507,6 +545,7 @@ class MLPEngine(CNNEngine):
             out[name] = (h1, h2)
         return out
 
+    @_with_precision
     def act(self, obs, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False, vec=None):
         self.ensure_bound()
         self.pack()
@@ -520,6 +559,7 @@ class MLPEngine(CNNEngine):
         t = self.towers(x, B, ws)
         return self._heads(t["a"][1], B, deterministic, noise, given, want_entropy, value_only, hv=t["c"][1])
 
+    @_with_precision
     def train_minibatch(self, storage, adv, idx, hp, loss_acc, optimizer):
         self.ensure_bound()
         self.pack()

@@ -37,6 +37,7 @@ SIGNATURES = {
     "ppo_storage_insert_scalars": [c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "ppo_gather_rows": [c_p, c_p, c_p, c_ll, c_ll, c_p],
     "ppo_gather_env_columns": [c_p, c_p, c_p, c_int, c_int, c_int, c_ll, c_p],
+    "ppo_gather_f16_to_f32": [c_p, c_p, c_p, c_ll, c_ll, c_p],
     "ppo_synth_env_step": [c_p, c_int, c_ll, c_p, c_p, c_p, c_ull, c_ull, c_f, c_p],
     "ppo_cartpole_step": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_ull, c_ull, c_int, c_p],
     # gemm.hip
@@ -100,7 +101,7 @@ _RESTYPES = {"ppo_last_error": ctypes.c_char_p, "ppo_packed_weights_size": c_ll}
 # functions whose int return value is a result, not a status
 _VALUE_FUNCS = {"ppo_abi_version", "ppo_gae_partials_count", "ppo_gae_scan_partials_count", "ppo_adv_diff_partials_count",
                 "ppo_packed_weights_size", "ppo_wgrad_splits", "ppo_heads_train_blocks", "ppo_grad_partials_count",
-                "ppo_conv2_dgrad_bits_ok", "ppo_conv3_dgrad_bits_ok"}
+                "ppo_conv2_dgrad_bits_ok", "ppo_conv3_dgrad_bits_ok", "ppo_tune_get"}
 
 _LIB = None
 

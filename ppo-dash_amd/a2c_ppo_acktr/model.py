@@ -84,6 +84,26 @@ class Policy(nn.Module):
     def forward(self, visual_inputs, vector_inputs, rnn_hxs, masks):
         raise NotImplementedError
 
+    # ------------------------------------------------------------- precision
+    def half(self):
+        """--half-precision (T/run.py:84-85 calls actor_critic.half()): every
+        trunk / GRU / head GEMM then multiplies bf16-rounded operands — one
+        bf16 MFMA product with fp32 accumulation instead of the six-product fp32
+        emulation — which is the matrix cores' native rate.  Unlike the
+        reference (fp16 parameters and fp16 Adam state), the parameters,
+        gradients and Adam moments stay fp32 masters; Policy.float() returns to
+        fp32 arithmetic.  Returns self, as nn.Module.half() does."""
+        self._half_mode = True
+        return self
+
+    def float(self):
+        self._half_mode = False
+        return super(Policy, self).float()
+
+    @property
+    def half_precision(self):
+        return getattr(self, "_half_mode", False)
+
     # ------------------------------------------------------------- engine
     def __getstate__(self):
         st = self.__dict__.copy()

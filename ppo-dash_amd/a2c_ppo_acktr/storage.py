@@ -69,9 +69,15 @@ class RolloutStorage(object):
         self._adv_ready = False
 
     def half(self):
-        raise NotImplementedError(
-            "RolloutStorage.half(): the MI355X engine keeps fp32 planes; store observations as bytes with "
-            "RolloutStorage(..., obs_dtype=torch.uint8) instead")
+        """storage.py:48-58 (--half-precision, T/run.py:137-138): a float image
+        observation plane becomes fp16, half the HBM of the reference's fp32 plane
+        (u8 planes are already a quarter and stay bytes).  The per-step scalar
+        planes (2 MB each at c3), vector obs and hidden states stay fp32 — GAE and
+        the loss keep the reference's fp32 arithmetic — and actions stay int64;
+        insert() converts fp16 masks / values written by the caller."""
+        if self.obs.dtype.is_floating_point and self.obs.dim() >= 5:
+            self.obs = self.obs.half()
+        return self
 
     def _on_device(self):
         if not self.value_preds.is_cuda:

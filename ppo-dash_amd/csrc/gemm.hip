@@ -159,7 +159,8 @@ __global__ __launch_bounds__(512) void conv1_fwd_img_kernel(const uint8_t* __res
 // of 16 output pixels.  k-step s covers k = 32s + [0, 32); lane group
 // g = lane >> 4 supplies k = 32s + 8g + j, j = 0..7 — one kx row of the patch,
 // 8 adjacent pixels, so an A fragment is one 16-byte LDS read.
-template <int C, bool MASK>   // MASK: also write the ReLU mask bits (training forward)
+// NPW: weight parts summed (3: exact fp32 weights; 1: half-precision mode, bf16 weights)
+template <int C, bool MASK, int NPW = 3>   // MASK: also write the ReLU mask bits (training forward)
 __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __restrict__ obs,
                                                                const int64_t* __restrict__ idx, long long row0,
                                                                int B, const float* __restrict__ w,
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
           a[t] = __builtin_bit_cast(bf16x8, v);
         }
 #pragma unroll
-      for (int part = 0; part < 3; ++part)
+      for (int part = 0; part < NPW; ++part)
 #pragma unroll
         for (int t = 0; t < NT; ++t)
           if (t < ntile) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t], wf[part][s], acc[t], 0, 0, 0);
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(256) void relu_bits_kernel(const float* __restrict_
 // the k-groups' partial sums are combined in a fixed order at the end.
 // Output: the usual split-K slab [Z][32][256] (u8 integers: the reduce applies
 // 1/255) and bias partials [Z][32].
-template <int C>
+template <int C, int NPD = 3>   // NPD: dz parts summed (3 exact; 1 half-precision mode)
 __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __restrict__ dz1,
                                                                  const uint8_t* __restrict__ obs,
                                                                  const int64_t* __restrict__ idx, long long row0,
@@ -434,8 +435,10 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
       if (st + 4 < KS) rd(st + 4, xa0, xa1, bq);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.l, bc[t], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.m, bc[t], acc[t], 0, 0, 0);
+        if constexpr (NPD == 3) {
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.l, bc[t], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.m, bc[t], acc[t], 0, 0, 0);
+        }
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.h, bc[t], acc[t], 0, 0, 0);
       }
     }
@@ -1937,7 +1940,7 @@ static int g_tune[TK_N] = {0, 8, 8, 8, 1, 0, 8, 1, 8, 8, 0, 0};  // fc_fwd 0: ti
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   if (strcmp(key, "products") == 0) {
-    PPO_REQUIRE(value == 6 || value == 9, "ppo_tune_set: products must be 6 or 9, got %d", value);
+    PPO_REQUIRE(value == 1 || value == 6 || value == 9, "ppo_tune_set: products must be 1, 6 or 9, got %d", value);
     g_products = value;
     return 0;
   }
@@ -2116,12 +2119,16 @@ static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, lo
       conv1_fwd_img_kernel<4><<<blocks, 512, 0, as_stream(stream)>>>((const uint8_t*)obs, idx, row0, B, w1, b1, out);
     } else {
       const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
-      if (mbits)
-        conv1_fwd_bf16x3_kernel<4, true><<<nb, 512, 0, as_stream(stream)>>>((const uint8_t*)obs, idx, row0, B, w1,
-                                                                            b1, out, mbits);
-      else
-        conv1_fwd_bf16x3_kernel<4, false><<<nb, 512, 0, as_stream(stream)>>>((const uint8_t*)obs, idx, row0, B, w1,
-                                                                             b1, out, nullptr);
+      const uint8_t* o8 = (const uint8_t*)obs;
+      hipStream_t st = as_stream(stream);
+      if (g_products == 1) {   // half-precision mode: bf16 weights
+        if (mbits) conv1_fwd_bf16x3_kernel<4, true, 1><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, mbits);
+        else conv1_fwd_bf16x3_kernel<4, false, 1><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, nullptr);
+      } else if (mbits) {
+        conv1_fwd_bf16x3_kernel<4, true><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, mbits);
+      } else {
+        conv1_fwd_bf16x3_kernel<4, false><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, nullptr);
+      }
     }
     if (prof) ppo_prof_end(slot, as_stream(stream), fl);
     PPO_LAUNCH_CHECK("conv1_fwd_u8 (image-resident)");
@@ -2184,6 +2191,8 @@ static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float*
     const uint16_t* wpl = planes_of(w2p, 64 * 512);
     if (mbits && g_products == 9)
       conv2_fwd_x9_kernel<9, true><<<nb, 512, 0, as_stream(stream)>>>(a1, B, wpl, b2, out, mbits);
+    else if (mbits && g_products == 1)
+      conv2_fwd_x9_kernel<1, true><<<nb, 512, 0, as_stream(stream)>>>(a1, B, wpl, b2, out, mbits);
     else if (mbits)
       conv2_fwd_x9_kernel<6, true><<<nb, 512, 0, as_stream(stream)>>>(a1, B, wpl, b2, out, mbits);
     else
@@ -2386,6 +2395,7 @@ static int conv3_dgrad_img(const float* dz3, int B, const float* w3d, const floa
   const bool prof = ppo_prof_begin("conv3_dgrad", as_stream(stream), &slot);
   const uint16_t* wpl = planes_of(w3d, 64 * 288);
   if (g_products == 9) conv3_dgrad_x9_kernel<9, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2);
+  else if (g_products == 1) conv3_dgrad_x9_kernel<1, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2);
   else conv3_dgrad_x9_kernel<6, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2);
   if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
   PPO_LAUNCH_CHECK("conv3_dgrad_x9_kernel");
@@ -2426,6 +2436,7 @@ static int conv2_dgrad_img(const float* dz2, int B, const float* w2d, const floa
   const bool prof = ppo_prof_begin("conv2_dgrad", as_stream(stream), &slot);
   const uint16_t* wpl = planes_of(w2d, 128 * 256);
   if (g_products == 9) conv2_dgrad_x9_kernel<9, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1);
+  else if (g_products == 1) conv2_dgrad_x9_kernel<1, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1);
   else conv2_dgrad_x9_kernel<6, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1);
   if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
   PPO_LAUNCH_CHECK("conv2_dgrad_x9_kernel");
@@ -2505,8 +2516,12 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
     if (B <= 0 || Z <= 0) return 0;
     int slot;
     const bool prof = ppo_prof_begin("conv1_wgrad_u8", as_stream(stream), &slot);
-    conv1_wgrad_bf16x3_kernel<4><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
-                                                                   slab_bias);
+    if (g_products == 1)   // half-precision mode: bf16 dz
+      conv1_wgrad_bf16x3_kernel<4, 1><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
+                                                                        slab, slab_bias);
+    else
+      conv1_wgrad_bf16x3_kernel<4><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
+                                                                     slab_bias);
     if (prof) ppo_prof_end(slot, as_stream(stream), fl);
     PPO_LAUNCH_CHECK("conv1_wgrad_bf16x3_kernel");
     return 0;

@@ -71,21 +71,26 @@ __device__ __forceinline__ f32x4 mma(const bf16x8& a, const bf16x8& b, const f32
 // products); NP = 6 (default) drops l·l, l·m and m·l, whose sum is below
 // 2^-26 |a·b| — a quarter of the rounding unit of one fp32 product, so the GEMM
 // keeps fp32 accuracy (the six-pass fp32 emulation, "bf16_6x").  Smallest first.
+// NP = 1 is the half-precision mode (Policy.half()): bf16-rounded operands, one
+// product, fp32 accumulation.
 #define PPO_PRODUCTS(NP, PART)                  \
   if constexpr (NP == 9) { PART(l, l) PART(l, m) PART(m, l) } \
-  PART(m, m) PART(l, h) PART(m, h) PART(h, l) PART(h, m) PART(h, h)
+  if constexpr (NP >= 6) { PART(m, m) PART(l, h) PART(m, h) PART(h, l) PART(h, m) } \
+  PART(h, h)
 
-// split-product count of the launches below (ppo_tune_set("products", 6 | 9))
+// split-product count of the launches below (ppo_tune_set("products", 1 | 6 | 9))
 static int g_products = 6;
 #define PPO_LAUNCH_NP(KERNEL, GRID, BLOCK, ST, ...)                   \
   do {                                                                \
     if (g_products == 9) KERNEL<9><<<GRID, BLOCK, 0, ST>>>(__VA_ARGS__); \
+    else if (g_products == 1) KERNEL<1><<<GRID, BLOCK, 0, ST>>>(__VA_ARGS__); \
     else KERNEL<6><<<GRID, BLOCK, 0, ST>>>(__VA_ARGS__);              \
   } while (0)
 
 // c += Σ over the part pairs (smallest first); exact operands have hi only
 template <bool AX, bool BX, int NP>
 __device__ __forceinline__ f32x4 mma9(const Frag3& a, const Frag3& b, f32x4 c) {
+  if constexpr (NP == 1) return mma(a.h, b.h, c);   // half-precision mode
   if constexpr (!AX && !BX) {
     if constexpr (NP == 9) {
       c = mma(a.l, b.l, c);
@@ -375,6 +380,7 @@ int launch_x9(const P& p, long long M, int N, int Z, hipStream_t st, const char*
   int slot;
   const bool prof = ppo_prof_begin(name, st, &slot);
   if (g_products == 9) igemm_x9_kernel<P, 9><<<grid, P::NT, 0, st>>>(p);
+  else if (g_products == 1) igemm_x9_kernel<P, 1><<<grid, P::NT, 0, st>>>(p);
   else igemm_x9_kernel<P, 6><<<grid, P::NT, 0, st>>>(p);
   if (prof) ppo_prof_end(slot, st, flops);
   PPO_LAUNCH_CHECK(name);

@@ -153,6 +153,29 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const V* __restrict__ 
   for (long long i = threadIdx.x & 63; i < row_elems; i += 64) d[i] = s[i];
 }
 
+// fp16 observation rows (RolloutStorage.half(), storage.py:48-58) -> fp32 rows for
+// the conv1 loaders: dst[r] = (float)src[idx ? idx[r] : r], 8 halves per lane step.
+__global__ __launch_bounds__(256) void gather_f16_f32_kernel(const uint4* __restrict__ src,
+                                                             const int64_t* __restrict__ idx, float4* __restrict__ dst,
+                                                             long long nrows, long long row_vec8) {
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= nrows) return;
+  const uint4* s = src + (idx ? idx[row] : row) * row_vec8;
+  float4* d = dst + row * 2 * row_vec8;
+  for (long long i = threadIdx.x & 63; i < row_vec8; i += 64) {
+    const uint4 v = s[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    float f[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f[2 * q] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[q] & 0xFFFF));
+      f[2 * q + 1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[q] >> 16));
+    }
+    d[2 * i] = make_float4(f[0], f[1], f[2], f[3]);
+    d[2 * i + 1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+
 // Env-column gather for recurrent_generator (storage.py:181-205):
 // dst[t][j] = src[t][envs[j]] for t < T, rows of row_bytes.
 template <typename V>
@@ -299,6 +322,18 @@ PPO_API int ppo_gather_rows(const void* src, const int64_t* idx, void* dst, long
   else
     gather_rows_kernel<uint8_t><<<blocks, 256, 0, st>>>((const uint8_t*)src, idx, (uint8_t*)dst, nrows, row_bytes);
   PPO_LAUNCH_CHECK("gather_rows_kernel");
+  return 0;
+}
+
+PPO_API int ppo_gather_f16_to_f32(const void* src, const int64_t* idx, float* dst, long long nrows,
+                                  long long row_elems, void* stream) {
+  PPO_REQUIRE(nrows >= 0 && row_elems > 0 && row_elems % 8 == 0, "ppo_gather_f16_to_f32: nrows=%lld row_elems=%lld",
+              nrows, row_elems);
+  PPO_REQUIRE(((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0, "ppo_gather_f16_to_f32: 16-B alignment");
+  if (nrows == 0) return 0;
+  gather_f16_f32_kernel<<<ceil_div(nrows, 4), 256, 0, as_stream(stream)>>>((const uint4*)src, idx, (float4*)dst,
+                                                                           nrows, row_elems / 8);
+  PPO_LAUNCH_CHECK("gather_f16_f32_kernel");
   return 0;
 }
 

@@ -112,8 +112,12 @@ def test_storage_host_errors():
     st = RolloutStorage(4, 2, (1,), [0], Discrete(2), 1)
     with pytest.raises(RuntimeError, match="move it to the MI355X"):
         st.compute_returns(torch.zeros(2, 1), True, 0.99, 0.95)
-    with pytest.raises(NotImplementedError):
-        st.half()
+    assert st.half() is st and st.obs.dtype == torch.float32   # vector obs planes stay fp32
+    img = RolloutStorage(2, 2, (4, 84, 84), [0], Discrete(2), 1)
+    img.half()
+    assert img.obs.dtype == torch.float16 and img.rewards.dtype == torch.float32 and img.actions.dtype == torch.int64
+    u8 = RolloutStorage(2, 2, (4, 84, 84), [0], Discrete(2), 1, obs_dtype=torch.uint8)
+    assert u8.half().obs.dtype == torch.uint8
     with pytest.raises(AssertionError):
         next(st.feed_forward_generator(torch.zeros(4, 2, 1), 100))
 
