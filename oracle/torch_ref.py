@@ -221,6 +221,11 @@ def run_iteration(p, optimizer, N, T, *, ppo_epoch=3, num_mini_batch=8, clip=0.1
     return losses
 
 
+def _decode(obs, dev, dt):
+    x = obs.to(dev).to(dt)
+    return x / 255.0 if obs.dtype == torch.uint8 else x
+
+
 def minibatch_grads(p, obs_u8, actions, old_logp, adv, vpred, ret, *, clip, value_coef, entropy_coef,
                     idx=None, chunk=2048, use_clipped_value_loss=True, conv=conv_unfold):
     """Gradient of the PPO minibatch loss (algo/ppo.py:57-81, mean over all B rows)
@@ -228,8 +233,8 @@ def minibatch_grads(p, obs_u8, actions, old_logp, adv, vpred, ret, *, clip, valu
     a mean of per-row terms, so Σ_chunks of the chunk losses scaled by |chunk|/B has
     the same gradient.  Row b is storage row idx[b] of the flat planes (obs_u8
     [R,C,84,84], the others [R]) — all rows in order when idx is None.
-    Observations are decoded as u8/255 (SURVEY §8c input convention) on p's device
-    and dtype.  Returns (grads list, [value loss, action loss, entropy])."""
+    u8 observations are decoded as u8/255 (SURVEY §8c input convention), float
+    ones (fp16 / fp32 planes) used as stored, on p's device and dtype.  Returns (grads list, [value loss, action loss, entropy])."""
     dt, dev = p[0].dtype, p[0].device
     B = obs_u8.shape[0] if idx is None else idx.numel()
     grads = [torch.zeros_like(t) for t in p]
@@ -237,7 +242,7 @@ def minibatch_grads(p, obs_u8, actions, old_logp, adv, vpred, ret, *, clip, valu
     for s in range(0, B, chunk):
         e = min(B, s + chunk)
         rows = slice(s, e) if idx is None else idx[s:e].to(obs_u8.device)
-        x = obs_u8[rows].to(dev).to(dt) / 255.0
+        x = _decode(obs_u8[rows], dev, dt)
         f = lambda t: t[rows].to(dev, dt).reshape(-1, 1)  # noqa: E731
         loss, vl, al, ent = ppo_loss(p, x, actions[rows].to(dev).reshape(-1, 1), f(old_logp), f(adv), f(vpred),
                                      f(ret), clip, value_coef, entropy_coef, use_clipped_value_loss, conv)
@@ -260,7 +265,7 @@ def trunk_grads(p_trunk, obs_u8, dfeat, *, idx=None, chunk=2048, conv=conv_unfol
     for s in range(0, B, chunk):
         e = min(B, s + chunk)
         rows = slice(s, e) if idx is None else idx[s:e].to(obs_u8.device)
-        x = obs_u8[rows].to(dev).to(dt) / 255.0
+        x = _decode(obs_u8[rows], dev, dt)
         h = trunk(p_trunk, x, conv)
         g = torch.autograd.grad(h, p_trunk, grad_outputs=dfeat[s:e].to(dev, dt))
         for acc, gi in zip(grads, g):

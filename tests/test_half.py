@@ -50,7 +50,7 @@ def test_half_minibatch_gradient_vs_float64(gpu, obs_dtype):
     assert pol.half() is pol and pol.half_precision
     assert next(pol.parameters()).dtype == torch.float32          # fp32 masters
     st = _storage(gpu, T, N, A, 5, torch.uint8)
-    if obs_dtype == torch.float16:   # u8 values as fp16 (exact), the decode convention /255 applied by the net input
+    if obs_dtype == torch.float16:   # normalised frames stored as fp16 (make_env.py:81-104)
         st.obs = (st.obs.float() / 255.0).half()
     adv = torch.randn(T, N, generator=torch.Generator().manual_seed(6)).to(gpu)
     idx = torch.randperm(T * N, generator=torch.Generator().manual_seed(7))[:4096].to(gpu)
@@ -60,9 +60,7 @@ def test_half_minibatch_gradient_vs_float64(gpu, obs_dtype):
     eng.train_minibatch(st, adv, idx, HP, loss, cap)
     torch.cuda.synchronize()
     p = TR.unflatten(flat0, H, dtype=torch.float64, device=gpu, requires_grad=True)
-    obs_u8 = st.obs[:T].reshape(T * N, 4, 84, 84)
-    if obs_dtype == torch.float16:
-        obs_u8 = (obs_u8.float() * 255.0).round().to(torch.uint8)
+    obs_u8 = st.obs[:T].reshape(T * N, 4, 84, 84)   # fp16 planes: the stored fp16 values, exactly
     fl = lambda t: t[:T].reshape(T * N, *t.shape[2:])  # noqa: E731
     grads, losses = TR.minibatch_grads(p, obs_u8, fl(st.actions), fl(st.action_log_probs), adv.reshape(-1),
                                        fl(st.value_preds), fl(st.returns), idx=idx, clip=HP["clip"],

@@ -17,8 +17,8 @@ run() {  # name timeout cmd...
 export PYTHONDONTWRITEBYTECODE=1
 for s in $STEPS; do
   case $s in
-    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
-    pytestall) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    pytestall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench 900 python bench.py --no-cpu-baseline --steps 2 --warmup 1 ;;
