@@ -103,6 +103,21 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// Range-checked buffer stores: a store whose byte offset is out of the
+// resource's range (e.g. -1) is dropped by the hardware — predication without an
+// exec-mask branch.  dword3 0x00020000: raw 32-bit buffer on gfx9 (gfx950).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void bstore_f32(float v, __amdgpu_buffer_rsrc_t r, int off_bytes) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off_bytes, 0, 0);
+}
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void bstore_f32x4(f32x4 v, __amdgpu_buffer_rsrc_t r, int off_bytes) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, off_bytes, 0, 0);
+}
+
 // u8 -> fp32 decode, bit-identical to (float)u / 255.0f (IEEE divide), which is
 // the oracle's input convention u8.float()/255.0.  q = u*(1/255)
 // is wrong for 126 of the 256 codes; one residual FMA correction makes all 256

@@ -770,7 +770,9 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restri
 #pragma unroll
     for (int p = 0; p < 3; ++p)
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
-  const float bv = bias[co];
+  // epilogue in the swapped orientation (weights as the MFMA A operand): lane
+  // (i16, g) holds pixel 16 t + i16, channels 16 nt + 4g .. +3 — one 16-B store
+  const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
   wait_vm0();
   // unit index of this lane's A fragment per row tile, tap (0, 0); a tap adds toff
   int qrow[MT];
@@ -843,7 +845,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restri
           a[u].l = *reinterpret_cast<const bf16x8*>(q + 16 * PLU);
         }
 #define PPO_PART(X, Y) \
-  _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(a[u].X, w.Y, acc[t0 + u]);
+  _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(w.Y, a[u].X, acc[t0 + u]);
         PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       }
@@ -857,19 +859,22 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restri
     if (b + 2 * G < B) fetch(b + 2 * G);
     __syncthreads();   // B: partials and the next image are in LDS
     if (kh == 0) {
-      float* o = out + (size_t)b * (81 * 64) + co;
+      const auto rs = make_rsrc(out + (size_t)b * (81 * 64), 81 * 64 * 4);
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         const f32x4 v = acc[t] + R[nt][t][lane];
+        const int m = 16 * t + i16;
+        f32x4 y;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = 16 * t + 4 * g + r;
-          const float y = fmaxf(v[r] + bv, 0.f);
-          if (m < 81) o[m * 64] = y;
-          if constexpr (MASK) {   // ReLU mask bits: lane (g, i16) -> pixel m, channel 16 nt + i16
-            const uint64_t bal = __builtin_amdgcn_ballot_w64(y > 0.f);
-            if (i16 == 0 && m < 81) mbits[((size_t)b * 81 + m) * 4 + nt] = (uint16_t)(bal >> (16 * g));
-          }
+        for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
+        bstore_f32x4(y, rs, m < 81 ? 4 * (m * 64 + 16 * nt + 4 * g) : -1);
+        if constexpr (MASK) {   // ReLU mask bits of pixel m, channels 16 nt .. +15: 4 lanes' nibbles
+          int nib = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) nib |= (y[r] > 0.f ? 1 : 0) << r;
+          const int w16 = nib | (__shfl_down(nib, 16, 64) << 4) | (__shfl_down(nib, 32, 64) << 8) |
+                          (__shfl_down(nib, 48, 64) << 12);
+          if (g == 0 && m < 81) mbits[((size_t)b * 81 + m) * 4 + nt] = (uint16_t)w16;
         }
       }
     }
@@ -1209,7 +1214,7 @@ template <int NP, bool BITS = false>
 __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __restrict__ dz3, int B,
                                                             const uint16_t* __restrict__ wpl,
                                                             const float* __restrict__ a2,
-                                                            float* __restrict__ dz2) {
+                                                            float* __restrict__ dz2, int stagger) {
   constexpr int GW = 25, CS = 288, PLU = 4 * CS, KS = 9, WN = 64 * 288;
   constexpr int DU = 49 * 4, MC = 81 * 64 / 4, MPER = (MC + 511) / 512;
   __shared__ __attribute__((aligned(16))) uint16_t S[2][3 * PLU * 8];
@@ -1288,9 +1293,15 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
     if (b + G < B) fetch(b + G);
   }
   __syncthreads();
+  // stagger: waves 4-7 (the second wave of every SIMD) stage the next image
+  // after their compute instead of before it, so each SIMD's matrix pipe has
+  // one computing wave while the other splits and stores
+  const bool late = stagger && wave >= 4;
   for (; b < B; b += G) {
-    if (b + G < B) put(cur ^ 1);
-    if (b + 2 * G < B) fetch(b + 2 * G);
+    if (!late) {
+      if (b + G < B) put(cur ^ 1);
+      if (b + 2 * G < B) fetch(b + 2 * G);
+    }
     const uint16_t* Sc = S[cur];
     f32x4 acc[3];
 #pragma unroll
@@ -1313,7 +1324,7 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
           a[u].l = *reinterpret_cast<const bf16x8*>(q + 16 * PLU);
         }
 #define PPO_PART(X, Y) \
-  _Pragma("unroll") for (int u = 0; u < 3; ++u) if ((msk[u] >> s) & 1u) acc[u] = mma(a[u].X, w.Y, acc[u]);
+  _Pragma("unroll") for (int u = 0; u < 3; ++u) if ((msk[u] >> s) & 1u) acc[u] = mma(w.Y, a[u].X, acc[u]);
         PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       }
@@ -1326,18 +1337,27 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
       compute(integral_constant<unsigned, 0x03F>{}, integral_constant<unsigned, 0x1FF>{},
               integral_constant<unsigned, 0x1F8>{});
     // epilogue: C row 4g + r of tile t is input pixel m; ReLU mask of a2
+    // swapped orientation (weights as the MFMA A operand): lane (i16, g) holds
+    // pixel 16 tl + i16, channels c0 = 16 nt + 4g .. +3 — one 16-B store per tile
     const uint8_t* mk = reinterpret_cast<const uint8_t*>(Mk[cur]);
-    float* o = dz2 + (size_t)b * 5184 + ci;
+    const auto rs = make_rsrc(dz2 + (size_t)b * 5184, 5184 * 4);
+    const int c0 = 16 * nt + 4 * g;
 #pragma unroll
-    for (int t = 0; t < 3; ++t)
+    for (int t = 0; t < 3; ++t) {
+      const int m = 16 * tl[t] + i16, mm = min(m, 80);
+      const uint32_t mw = Mk[cur][2 * mm + (c0 >> 5)] >> (c0 & 31);
+      f32x4 y;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = 16 * tl[t] + 4 * g + r;
-        if (m < 81) {
-          const bool keep = BITS ? ((Mk[cur][2 * m + (ci >> 5)] >> (ci & 31)) & 1u) != 0 : mk[m * 64 + ci] != 0;
-          o[m * 64] = keep ? acc[t][r] : 0.f;
-        }
+        const bool keep = BITS ? ((mw >> r) & 1u) != 0 : mk[mm * 64 + c0 + r] != 0;
+        y[r] = keep ? acc[t][r] : 0.f;
       }
+      bstore_f32x4(y, rs, m < 81 ? 4 * (m * 64 + c0) : -1);
+    }
+    if (late) {
+      if (b + G < B) put(cur ^ 1);
+      if (b + 2 * G < B) fetch(b + 2 * G);
+    }
     __syncthreads();   // every wave is done with stage cur; stage cur ^ 1 is complete
     cur ^= 1;
   }
@@ -1358,7 +1378,7 @@ template <int NP>
 __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restrict__ a2, int B,
                                                           const uint16_t* __restrict__ wpl,
                                                           const float* __restrict__ bias,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out, int stagger) {
   constexpr int NPX = 84, PL = NPX * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, UPER = (UNITS + 511) / 512;
   __shared__ __attribute__((aligned(16))) uint16_t S[2][3 * PL];
   __shared__ __attribute__((aligned(16))) f32x4 R[2][2][2][2][64];   // [stage][co tile][row half][tile][lane]
@@ -1370,7 +1390,9 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
 #pragma unroll
     for (int p = 0; p < 3; ++p)
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 576 + (9 * kh + s) * 32 + 8 * g);
-  const float bv = bias[co];
+  // swapped orientation (weights as the MFMA A operand): lane (i16, g) holds
+  // row 16 t + i16, channels 16 nt + 4g .. +3 — one 16-B store per tile
+  const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
   wait_vm0();
   for (int i = tid; i < 2 * 3 * PL / 8; i += 512) reinterpret_cast<uint4*>(&S[0][0])[i] = uint4{0, 0, 0, 0};
   f32x4 stg[UPER][2];
@@ -1407,9 +1429,12 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
     if (b + G < B) fetch(b + G);
   }
   __syncthreads();
+  const bool late = stagger && mh == 1;   // waves 4-7 stage after their compute (see conv3 dgrad)
   for (; b < B; b += G) {
-    if (b + G < B) put(cur ^ 1);
-    if (b + 2 * G < B) fetch(b + 2 * G);
+    if (!late) {
+      if (b + G < B) put(cur ^ 1);
+      if (b + 2 * G < B) fetch(b + 2 * G);
+    }
     const uint16_t* Sc = S[cur];
     f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
@@ -1426,7 +1451,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
         a[u].l = *reinterpret_cast<const bf16x8*>(q + 2 * PL);
       }
 #define PPO_PART(X, Y) \
-  _Pragma("unroll") for (int u = 0; u < 2; ++u) acc[u] = mma(a[u].X, w.Y, acc[u]);
+  _Pragma("unroll") for (int u = 0; u < 2; ++u) acc[u] = mma(w.Y, a[u].X, acc[u]);
       PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
     }
@@ -1434,17 +1459,21 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
       R[cur][nt][mh][0][lane] = acc[0];
       R[cur][nt][mh][1][lane] = acc[1];
     }
+    if (late) {
+      if (b + G < B) put(cur ^ 1);
+      if (b + 2 * G < B) fetch(b + 2 * G);
+    }
     __syncthreads();   // stage cur consumed, stage cur ^ 1 complete, partials in R[cur]
     if (kh == 0) {
-      float* o = out + (size_t)b * (49 * 32) + co;
+      const auto rs = make_rsrc(out + (size_t)b * (49 * 32), 49 * 32 * 4);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const f32x4 v = acc[u] + R[cur][nt][mh][u][lane];
+        const int m = 16 * (2 * mh + u) + i16, oy = m / 9, ox = m - 9 * oy;
+        f32x4 y;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = 16 * (2 * mh + u) + 4 * g + r, oy = m / 9, ox = m - 9 * oy;
-          if (ox < 7 && oy < 7) o[(7 * oy + ox) * 32] = fmaxf(v[r] + bv, 0.f);
-        }
+        for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
+        bstore_f32x4(y, rs, (ox < 7 && oy < 7) ? 4 * ((7 * oy + ox) * 32 + 16 * nt + 4 * g) : -1);
       }
     }
     cur ^= 1;
@@ -1628,11 +1657,11 @@ __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __rest
 // ppo_conv1_fwd_mask, 1.6 KB per image) instead of the fp32 activations
 // (51.2 KB per image): 40 % less HBM traffic, 12 % less time (measured with the
 // mask loads removed: 2.14 vs 2.43 ms at the c3 minibatch).
-template <int NP, bool BITS = false>
+template <int NP, bool BITS = false, bool DEFER = false>
 __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __restrict__ dz2, int B,
                                                             const uint16_t* __restrict__ wpl,
                                                             const float* __restrict__ a1,
-                                                            float* __restrict__ dz1) {
+                                                            float* __restrict__ dz1, int stagger) {
   constexpr int HO = 9, CO = 64, GW = 11, GP = 12 * GW, ROW = CO, PL = GP * ROW, MT = 7, KS = 8;
   constexpr int CH = HO * HO * CO / 8, PER = (CH + 511) / 512, WN = 128 * 256;
   __shared__ __attribute__((aligned(16))) uint16_t S[2][3][PL];
@@ -1725,9 +1754,30 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
     if (b + G < B) fetch(b + G);
   }
   __syncthreads();
+  const bool late = (stagger & 1) && wave >= 4;   // waves 4-7 stage after their compute (see conv3 dgrad)
+  // timing anatomy only (tools/kbench.py --tune stagger=...; wrong results):
+  // 16 skips the MFMAs, 32 the epilogue stores, 64 the staging of the next image
+  const bool no_mma = stagger & 16, no_epi = stagger & 32, no_stage = stagger & 64;
+  // DEFER: the stores of image b are issued during image b + G's k-steps (one
+  // row tile per k-step) from registers masked at the end of image b, instead of
+  // all waves storing 51.2 KB per image at once before the barrier; dummy rows
+  // get an out-of-range buffer offset (the store is dropped) instead of a branch
+  // DEFER also swaps the MFMA operands (weights as A, pixels as B): lane (i16, g)
+  // then holds grid row 16 t + i16 and the 4 consecutive channels 4g .. 4g+3 of
+  // its n tile — one 16-B store per tile instead of four scattered dwords.
+  f32x4 eacc[DEFER ? MT : 1];
+  int bprev = -1;
+  const int cbs = (ph >> 1) * 640 + (ph & 1) * 32 + 16 * (wave & 1) + 4 * g;
+  auto store_tile = [&](int t, const f32x4& v, int bp) {
+    const int eo = etab[16 * t + i16];
+    const auto rs = make_rsrc(dz1 + (size_t)bp * 12800, 12800 * 4);
+    bstore_f32x4(v, rs, eo >= 0 ? 4 * (eo + cbs) : -1);
+  };
   for (; b < B; b += G) {
-    if (b + G < B) put(cur ^ 1);
-    if (b + 2 * G < B) fetch(b + 2 * G);
+    if (!late && !no_stage) {
+      if (b + G < B) put(cur ^ 1);
+      if (b + 2 * G < B) fetch(b + 2 * G);
+    }
     const char* Sb = reinterpret_cast<const char*>(S[cur][0]);
     f32x4 acc[MT];
 #pragma unroll
@@ -1737,9 +1787,10 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
       const char* As = Sb + (abase ^ (16 * s));
       const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
       // two groups of row tiles (4 + 3: register budget); within a group the
-      // nine part products, smallest first, go round the tiles
+      // part products, smallest first, go round the tiles
 #pragma unroll
       for (int t0 = 0; t0 < MT; t0 += 4) {
+        if (no_mma) break;
         constexpr int TG = 4;
         Frag3 a[TG];
 #pragma unroll
@@ -1751,29 +1802,54 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
             a[u].l = *reinterpret_cast<const bf16x8*>(q + 4 * PL);
           }
 #define PPO_PART(X, Y)                                                  \
-  _Pragma("unroll") for (int u = 0; u < TG; ++u) if (t0 + u < MT) acc[t0 + u] = mma(a[u].X, w.Y, acc[t0 + u]);
+  _Pragma("unroll") for (int u = 0; u < TG; ++u) if (t0 + u < MT)       \
+    acc[t0 + u] = DEFER ? mma(w.Y, a[u].X, acc[t0 + u]) : mma(a[u].X, w.Y, acc[t0 + u]);
         PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       }
+      if constexpr (DEFER)
+        if (s < MT && bprev >= 0 && !no_epi) store_tile(s, eacc[s], bprev);
     }
     // epilogue: C row 4g + r of tile t is grid row m = 16t + 4g + r; ReLU mask of a1
     const uint8_t* mk = reinterpret_cast<const uint8_t*>(Mk[cur]);
-    float* dm = dz1 + (size_t)b * 12800;
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
+      if constexpr (DEFER) {
+        const int i = max(etab[16 * t + i16], 0) + cbs;   // element (pixel i >> 5, channels (i & 31) + r)
+        const uint32_t mw = Mk[cur][i >> 5] >> (i & 31);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool keep = BITS ? ((mw >> r) & 1u) != 0 : mk[i + r] != 0;
+          eacc[t][r] = keep ? acc[t][r] : 0.f;
+        }
+        continue;
+      }
       const int4 e = *reinterpret_cast<const int4*>(&etab[16 * t + 4 * g]);
       const int eo[4] = {e.x, e.y, e.z, e.w};
+      if (!no_epi) {
+        float* dm = dz1 + (size_t)b * 12800;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (eo[r] >= 0) {
-          const int i = eo[r] + cb;   // element (pixel i >> 5, channel i & 31)
-          const bool keep = BITS ? ((Mk[cur][i >> 5] >> (i & 31)) & 1u) != 0 : mk[i] != 0;
-          dm[i] = keep ? acc[t][r] : 0.f;
-        }
+        for (int r = 0; r < 4; ++r)
+          if (eo[r] >= 0) {
+            const int i = eo[r] + cb;
+            const bool keep = BITS ? ((Mk[cur][i >> 5] >> (i & 31)) & 1u) != 0 : mk[i] != 0;
+            dm[i] = keep ? acc[t][r] : 0.f;
+          }
+      }
+    }
+    bprev = b;
+    if (late && !no_stage) {
+      if (b + G < B) put(cur ^ 1);
+      if (b + 2 * G < B) fetch(b + 2 * G);
     }
     __syncthreads();   // every wave is done with S[cur]; S[cur ^ 1] is complete
     cur ^= 1;
   }
+  if constexpr (DEFER)
+    if (bprev >= 0 && !no_epi) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t) store_tile(t, eacc[t], bprev);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1936,9 +2012,16 @@ enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRA
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
                                          "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad", "fc_dgrad", "fc_wgrad"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
+// stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
+// next image after their compute (conv2 / conv3 dgrad, conv3 forward)
+static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measured best
 static int g_tune[TK_N] = {0, 8, 8, 8, 1, 0, 8, 1, 8, 8, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
+  if (strcmp(key, "stagger") == 0) {
+    g_stagger = value;
+    return 0;
+  }
   if (strcmp(key, "products") == 0) {
     PPO_REQUIRE(value == 1 || value == 6 || value == 9, "ppo_tune_set: products must be 1, 6 or 9, got %d", value);
     g_products = value;
@@ -1954,6 +2037,7 @@ PPO_API int ppo_tune_set(const char* key, int value) {
 }
 
 PPO_API int ppo_tune_get(const char* key) {
+  if (strcmp(key, "stagger") == 0) return g_stagger;
   if (strcmp(key, "products") == 0) return g_products;
   for (int i = 0; i < TK_N; ++i)
     if (strcmp(key, g_tune_names[i]) == 0) return g_tune[i];
@@ -2162,7 +2246,7 @@ PPO_API int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const f
 
 static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float* b2, float* out, uint16_t* mbits,
                           void* stream) {
-  if (mbits && g_tune[TK_CONV2_FWD] != 8) {   // no fused mask epilogue: the conv, then the mask
+  if (mbits && g_tune[TK_CONV2_FWD] != 8) {   // no fused mask epilogue
     const int rc = conv2_fwd_impl(a1, B, w2p, b2, out, nullptr, stream);
     if (rc != 0 || B <= 0) return rc;
     const long long halves = (long long)B * 81 * 4;
@@ -2221,7 +2305,8 @@ PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float*
     const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
     int slot;
     const bool prof = ppo_prof_begin("conv3_fwd", as_stream(stream), &slot);
-    PPO_LAUNCH_NP(conv3_fwd_x9_kernel, nb, 512, as_stream(stream), a2, B, planes_of(w3p, 32 * 576), b3, out);
+    PPO_LAUNCH_NP(conv3_fwd_x9_kernel, nb, 512, as_stream(stream), a2, B, planes_of(w3p, 32 * 576), b3, out,
+                  g_stagger);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
     PPO_LAUNCH_CHECK("conv3_fwd_x9_kernel");
     return 0;
@@ -2394,9 +2479,9 @@ static int conv3_dgrad_img(const float* dz3, int B, const float* w3d, const floa
   int slot;
   const bool prof = ppo_prof_begin("conv3_dgrad", as_stream(stream), &slot);
   const uint16_t* wpl = planes_of(w3d, 64 * 288);
-  if (g_products == 9) conv3_dgrad_x9_kernel<9, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2);
-  else if (g_products == 1) conv3_dgrad_x9_kernel<1, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2);
-  else conv3_dgrad_x9_kernel<6, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2);
+  if (g_products == 9) conv3_dgrad_x9_kernel<9, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2, g_stagger);
+  else if (g_products == 1) conv3_dgrad_x9_kernel<1, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2, g_stagger);
+  else conv3_dgrad_x9_kernel<6, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz3, B, wpl, mask, dz2, g_stagger);
   if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
   PPO_LAUNCH_CHECK("conv3_dgrad_x9_kernel");
   return 0;
@@ -2435,9 +2520,12 @@ static int conv2_dgrad_img(const float* dz2, int B, const float* w2d, const floa
   int slot;
   const bool prof = ppo_prof_begin("conv2_dgrad", as_stream(stream), &slot);
   const uint16_t* wpl = planes_of(w2d, 128 * 256);
-  if (g_products == 9) conv2_dgrad_x9_kernel<9, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1);
-  else if (g_products == 1) conv2_dgrad_x9_kernel<1, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1);
-  else conv2_dgrad_x9_kernel<6, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1);
+  const int sg = g_stagger & ~2;
+  if (g_products == 9) conv2_dgrad_x9_kernel<9, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
+  else if (g_products == 1) conv2_dgrad_x9_kernel<1, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
+  else if (g_stagger & 2)
+    conv2_dgrad_x9_kernel<6, BITS, true><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
+  else conv2_dgrad_x9_kernel<6, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
   if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
   PPO_LAUNCH_CHECK("conv2_dgrad_x9_kernel");
   return 0;

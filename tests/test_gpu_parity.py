@@ -892,7 +892,8 @@ def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu, conv2_variant):
 @pytest.mark.parametrize("variant", [0, 8, 10])
 def test_conv2_fwd_variants_vs_torch(gpu, variant):
     """conv2 forward (4x4 stride 2, 20x20x32 -> 9x9x64, bias + ReLU): the split-bf16
-    tile GEMM (0) and the image-resident kernel (8) vs torch float64:
+    tile GEMM (0), the image-resident kernels (8: register-staged, 10: LDS-DMA
+    staged) vs torch float64:
     max |err| <= 1e-5 * max |ref|.  B = 300 > the persistent grid."""
     Hh = _hip()
     B = 300
@@ -1029,6 +1030,47 @@ def test_conv3_fwd_variants_vs_torch(gpu, variant):
     ref = torch.relu(F.conv2d(a2.double().permute(0, 3, 1, 2), w["w3"].double(), b3.double())).permute(0, 2, 3, 1)
     err = (out.cpu().double() - ref).abs().max().item()
     assert err <= 1e-5 * ref.abs().max().item(), err
+
+
+def test_stagger_bit_identical(gpu):
+    """ppo_tune_set("stagger", 1) only moves waves 4-7's staging of the next image
+    behind their compute (conv2 / conv3 dgrad, conv3 forward); bit 2 defers conv2
+    dgrad's stores into the next image's k-steps: every output is
+    bit-identical to the unstaggered kernels, on B = 300 (> the persistent grid:
+    blocks walk several images, both stage parities)."""
+    Hh = _hip()
+    B = 300
+    _, packed, pk = _packed(gpu, 64, 61)
+    g = torch.Generator().manual_seed(62)
+    dz2 = torch.randn(B, 9, 9, 64, generator=g).cuda()
+    dz3 = torch.randn(B, 7, 7, 32, generator=g).cuda()
+    a1 = torch.randn(B, 20, 20, 32, generator=g).cuda()
+    a2 = torch.relu(torch.randn(B, 9, 9, 64, generator=g)).cuda()
+    b3 = (torch.randn(32, generator=g) * 0.1).cuda()
+
+    def run():
+        o = [torch.full((B, 20, 20, 32), float("nan"), device=gpu), torch.full((B, 9, 9, 64), float("nan"), device=gpu),
+             torch.full((B, 7, 7, 32), float("nan"), device=gpu)]
+        Hh.call("ppo_conv2_dgrad", dz2.data_ptr(), B, pk[5], a1.data_ptr(), o[0].data_ptr(), _s())
+        Hh.call("ppo_conv3_dgrad", dz3.data_ptr(), B, pk[4], a2.data_ptr(), o[1].data_ptr(), _s())
+        Hh.call("ppo_conv3_fwd", a2.data_ptr(), B, pk[1], b3.data_ptr(), o[2].data_ptr(), _s())
+        torch.cuda.synchronize()
+        return o
+
+    old = Hh.call("ppo_tune_get", b"stagger")
+    try:
+        Hh.call("ppo_tune_set", b"stagger", 0)
+        ref = run()
+        got = []
+        for v in (1, 2, 3):
+            Hh.call("ppo_tune_set", b"stagger", v)
+            got.append(run())
+    finally:
+        Hh.call("ppo_tune_set", b"stagger", old)
+    for g_ in got:
+        for r, x in zip(ref, g_):
+            assert not torch.isnan(r).any()
+            assert torch.equal(r, x)
 
 
 @pytest.mark.parametrize("variant", [0, 8])

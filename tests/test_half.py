@@ -11,6 +11,7 @@ import torch
 
 from oracle import ppo_oracle as O
 from oracle import torch_ref as TR
+from helpers.gradcheck import check_grads
 
 pytestmark = pytest.mark.gpu
 
@@ -72,15 +73,18 @@ def test_half_minibatch_gradient_vs_float64(gpu, obs_dtype):
         print(f"{name:28s} half-mode relative Frobenius error {fro:.2e}", flush=True)
         assert fro <= BF16_TOL, (name, fro)
     np.testing.assert_allclose(loss[:3].cpu().numpy(), losses, rtol=BF16_TOL, atol=1e-4)
-    # back to fp32 arithmetic: the same minibatch at the fp32 tolerance of test_full_size
+    # back to fp32 arithmetic: the same minibatch at test_full_size's fp32 bar
+    # (float64 error no more than 2x that of torch's own fp32 autograd)
     pol.float()
     cap32 = _GradCapture()
     eng.train_minibatch(st, adv, idx, HP, loss, cap32)
     torch.cuda.synchronize()
-    g32 = O.unflatten(cap32.grad.cpu().numpy(), O.cnn_param_shapes(H))
-    for (name, _), ref in zip(O.cnn_param_shapes(H), grads):
-        ref = ref.cpu().numpy()
-        assert np.linalg.norm(g32[name] - ref) / max(np.linalg.norm(ref), 1e-12) <= 3e-5, name
+    p32 = TR.unflatten(flat0, H, dtype=torch.float32, device=gpu, requires_grad=True)
+    g32, _ = TR.minibatch_grads(p32, obs_u8, fl(st.actions), fl(st.action_log_probs), adv.reshape(-1),
+                                fl(st.value_preds), fl(st.returns), idx=idx, clip=HP["clip"],
+                                value_coef=HP["value_coef"], entropy_coef=HP["entropy_coef"])
+    g32 = torch.cat([t.reshape(-1) for t in g32]).cpu().numpy()
+    check_grads(cap32.grad.cpu().numpy(), grads, O.cnn_param_shapes(H), fp32_flat=g32)
 
 
 def test_half_precision_run_py_flow(gpu):

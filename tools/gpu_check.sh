@@ -22,8 +22,13 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench 900 python bench.py --no-cpu-baseline --steps 2 --warmup 1 ;;
+    half) run pytest_half 600 python -u -m pytest tests/test_half.py -m gpu -v --timeout 300 --timeout-method thread ;;
+    c5bench) run bench_c5 900 python bench.py --recurrent --num-steps 256 --no-cpu-baseline --no-gae-roofline --no-boundary ;;
+    halfbench) run bench_half 900 python bench.py --half-precision --no-cpu-baseline --no-gae-roofline --no-boundary ;;
+    c5prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+          run rocprof_c5 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5 -o run -- python3 bench.py --recurrent --num-steps 256 --no-cpu-baseline --no-gae-roofline --no-boundary --steps 2 --warmup 1 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-          run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --no-gae-roofline --steps 2 --warmup 1 ;;
+          run rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --no-gae-roofline --steps 2 --warmup 1 ;;
   esac
 done
 echo "== all done"

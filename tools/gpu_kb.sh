@@ -1,0 +1,15 @@
+#!/bin/bash
+# kbench A/B of tune variants: KB="name:tune[,tune]|..." entries, B sizes in BS
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+BS="${BS:-65536 4096}"
+IFS='|' read -ra ENTRIES <<< "$KB"
+for B in $BS; do
+  for e in "${ENTRIES[@]}"; do
+    only=${e%%:*}; tune=${e#*:}
+    echo "--- B=$B only=$only tune=$tune"
+    timeout -k 10 120 python tools/kbench.py --B $B --reps 10 --only "$only" --tune "$tune"
+    rc=$?; if [ $rc -ne 0 ]; then echo "!! rc=$rc"; exit $rc; fi
+  done
+done
