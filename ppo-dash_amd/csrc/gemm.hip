@@ -322,8 +322,11 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
                                                                  const uint8_t* __restrict__ obs,
                                                                  const int64_t* __restrict__ idx, long long row0,
                                                                  int B, float* __restrict__ slab,
-                                                                 float* __restrict__ slab_bias) {
+                                                                 float* __restrict__ slab_bias, int dbg) {
   static_assert(C == 4, "LDS budget sized for 4 input channels");
+  // timing anatomy only (kbench --tune stagger=16*dbg; wrong results): dbg 1 skips
+  // the MFMAs, 2 the staging (put), 4 the dz split, 8 the B-fragment reads
+  const bool no_mma = dbg & 1, no_put = dbg & 2, no_split = dbg & 4, no_rd = dbg & 8;
   constexpr int EROW = 162, NE = C * IMG * EROW, DZL = 416, NPX = 400, KS = 25, NT = 512;
   // float offset of pixel px (multiple of 4) in dzT row co: chunk px/4 XOR SW(co)
   auto dzo = [](int co, int px) {
@@ -418,7 +421,7 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
   int b = blockIdx.x;
   if (b < B) fetch(b);
   for (; b < B; b += gridDim.x) {
-    put();
+    if (!no_put) put();
     __syncthreads();
     if (b + (int)gridDim.x < B) fetch(b + gridDim.x);
     // k-steps kg, kg + 4, ...: the fragments of step s + 4 are read while the
@@ -428,13 +431,14 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
     if (kg < KS) rd(kg, xa0, xa1, bq);
     for (int st = kg; st < KS; st += 4) {
       Frag3 fa;
-      split8(xa0, xa1, fa, false);
+      split8(xa0, xa1, fa, no_split);
+      if (no_split) fa.m = fa.l = fa.h;
       bf16x8 bc[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) bc[t] = bq[t];
-      if (st + 4 < KS) rd(st + 4, xa0, xa1, bq);
+      if (st + 4 < KS && !no_rd) rd(st + 4, xa0, xa1, bq);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
+      for (int t = 0; t < 4 && !no_mma; ++t) {
         if constexpr (NPD == 3) {
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.l, bc[t], acc[t], 0, 0, 0);
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.m, bc[t], acc[t], 0, 0, 0);
@@ -476,164 +480,6 @@ __global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __
     float t = 0.f;
     for (int j = 7 - c8; j < NT; j += 8) t += bred[j * 4 + q];   // threads with cq = c8
     slab_bias[(size_t)blockIdx.x * 32 + tid] = t;
-  }
-}
-
-// conv1 weight gradient, variant with one k-group per wave (ppo_tune_set
-// ("conv1_wgrad", 2)): 4 waves (one per SIMD, room for 8 accumulator tiles),
-// wave w covers all 256 (c, ky, kx) columns for k-steps w, w + 4, ... — each dz
-// fragment is split once (the 8-wave kernel above splits every fragment in both
-// column halves) and feeds 24 MFMAs; the four k-group partials go to the
-// split-K slab as four entries per block (Z = 4 x grid).  Measured slower than
-// the 8-wave kernel (2.17 vs 2.01 ms at the c3 minibatch): one wave per SIMD
-// leaves the E-expansion and split VALU work without a second wave to overlap.
-template <int C>
-__global__ __launch_bounds__(256) void conv1_wgrad_k8_kernel(const float* __restrict__ dz1,
-                                                                 const uint8_t* __restrict__ obs,
-                                                                 const int64_t* __restrict__ idx, long long row0,
-                                                                 int B, float* __restrict__ slab,
-                                                                 float* __restrict__ slab_bias) {
-  static_assert(C == 4, "LDS budget sized for 4 input channels");
-  constexpr int EROW = 162, NE = C * IMG * EROW, DZL = 416, NPX = 400, KS = 25, NT = 256, KG = 4;
-  // float offset of pixel px (multiple of 4) in dzT row co: chunk px/4 XOR SW(co)
-  auto dzo = [](int co, int px) {
-    constexpr unsigned long long SWLO = 0x312423067232146ull, SWHI = 0x1601706435575475ull;
-    const int sw = (int)(((co < 16 ? SWLO >> (4 * co) : SWHI >> (4 * (co - 16)))) & 7);
-    return co * DZL + 4 * ((px >> 2) ^ sw);
-  };
-  __shared__ __attribute__((aligned(16))) uint16_t E[NE];
-  __shared__ __attribute__((aligned(16))) float dzT[32 * DZL];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kg = __builtin_amdgcn_readfirstlane(wave);   // k-steps kg, kg + 4, ...
-  const int l32 = lane & 31, h = lane >> 5;
-  int ecol[8];   // lane's B column n = 32 t + l32 -> (c, ky, kx)
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int n = 32 * t + l32, c = n >> 6, ky = (n >> 3) & 7, kx = n & 7;
-    ecol[t] = (c * IMG + ky) * EROW + kx * 20;   // + 4 oy * EROW + ox0 per quad
-  }
-  f32x16 acc[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  const int cq = tid & 7;                 // dz staging: channel quad of this thread
-  float bsum[4] = {0.f, 0.f, 0.f, 0.f};   // bias partial of channels 4 cq .. +3
-
-  f32x4 dzr[4][4];        // up to 4 units of 4 pixels x 4 channels
-  uint32_t imr[2][21];    // up to two image rows (84 bytes each)
-  auto fetch = [&](int b) {
-    const float* dzb = dz1 + (size_t)b * NPX * 32;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int u = tid + NT * i;
-      if (u < 800) {
-        const int p4 = u >> 3;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dzr[i][r] = *reinterpret_cast<const f32x4*>(dzb + (4 * p4 + r) * 32 + 4 * cq);
-      }
-    }
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      const int cy = tid + NT * rr;
-      if (cy < C * IMG) {
-        const uint32_t* row =
-            reinterpret_cast<const uint32_t*>(obs + obs_row(idx, row0, b) * (long long)(C * IMG2) + cy * IMG);
-#pragma unroll
-        for (int j = 0; j < 21; ++j) imr[rr][j] = row[j];
-      }
-    }
-  };
-  auto put = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int u = tid + NT * i;
-      if (u < 800) {
-        const int p4 = u >> 3;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x4 v = f32x4{dzr[i][0][q], dzr[i][1][q], dzr[i][2][q], dzr[i][3][q]};
-          *reinterpret_cast<f32x4*>(dzT + dzo(4 * cq + q, 4 * p4)) = v;
-          bsum[q] += (v[0] + v[1]) + (v[2] + v[3]);
-        }
-      }
-    }
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
-      const int cy = tid + NT * rr;
-      if (cy < C * IMG) {
-#pragma unroll
-        for (int kx = 0; kx < 8; ++kx) {   // E[cy][kx][ox] = byte (kx & 3) of dword ox + (kx >> 2)
-          const int kh = kx >> 2, kk = kx & 3;
-          uint32_t* dst = reinterpret_cast<uint32_t*>(E + cy * EROW + kx * 20);
-#pragma unroll
-          for (int q = 0; q < 10; ++q) {
-            const uint32_t w0 = imr[rr][2 * q + kh], w1 = imr[rr][2 * q + 1 + kh];
-            const float f0 = (float)((w0 >> (8 * kk)) & 255u), f1 = (float)((w1 >> (8 * kk)) & 255u);
-            dst[q] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
-          }
-        }
-      }
-    }
-  };
-  auto rd = [&](int st, f32x4& x0, f32x4& x1, bf16x8 (&bb)[8]) {
-    const int px = 16 * st + 8 * h;   // this lane half's 8 pixels: quads px/4, px/4 + 1
-    x0 = *reinterpret_cast<const f32x4*>(dzT + dzo(l32, px));
-    x1 = *reinterpret_cast<const f32x4*>(dzT + dzo(l32, px + 4));
-    const int q1 = px >> 2, q2 = q1 + 1;
-    const int e1 = (q1 / 5) * (4 * EROW) + 4 * (q1 % 5), e2 = (q2 / 5) * (4 * EROW) + 4 * (q2 % 5);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {   // 40-B kx rows: quads only 4-byte aligned -> dword reads
-      const uint32_t* p1 = reinterpret_cast<const uint32_t*>(E + ecol[t] + e1);
-      const uint32_t* p2 = reinterpret_cast<const uint32_t*>(E + ecol[t] + e2);
-      bb[t] = __builtin_bit_cast(bf16x8, uint4{p1[0], p1[1], p2[0], p2[1]});
-    }
-  };
-
-  int b = blockIdx.x;
-  if (b < B) fetch(b);
-  for (; b < B; b += gridDim.x) {
-    put();
-    __syncthreads();
-    if (b + (int)gridDim.x < B) fetch(b + gridDim.x);
-    // k-steps kg, kg + 4, ...: one dz split per step feeds 24 MFMAs (8 n tiles x 3)
-    for (int st = kg; st < KS; st += KG) {
-      f32x4 xa0, xa1;
-      bf16x8 bc[8];
-      rd(st, xa0, xa1, bc);
-      Frag3 fa;
-      split8(xa0, xa1, fa, false);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.l, bc[t], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.m, bc[t], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.h, bc[t], acc[t], 0, 0, 0);
-      }
-    }
-    __syncthreads();   // before the next image overwrites E / dzT
-  }
-  // ---- each wave's partial is its own split-K slab entry (blockIdx * KG + wave):
-  // ppo_wgrad_reduce sums all of them in a fixed order ----
-  float* out = slab + ((size_t)blockIdx.x * KG + wave) * 32 * 256;
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = (r & 3) + 8 * (r >> 2) + 4 * h, n = 32 * t + l32;
-      out[co * 256 + n] = acc[t][r];
-    }
-  __syncthreads();
-  float* bred = dzT;   // [NT threads][4]
-#pragma unroll
-  for (int q = 0; q < 4; ++q) bred[tid * 4 + q] = bsum[q];
-  __syncthreads();
-  if (tid < 32) {   // channel tid: the 64 threads of its quad, fixed order
-    const int q = tid & 3, c8 = tid >> 2;
-    float t = 0.f;
-    for (int j = c8; j < NT; j += 8) t += bred[j * 4 + q];
-    slab_bias[(size_t)blockIdx.x * KG * 32 + tid] = t;
-  } else if (tid < KG * 32) {
-    slab_bias[(size_t)blockIdx.x * KG * 32 + tid] = 0.f;   // the block's other KG - 1 entries
   }
 }
 
@@ -2590,26 +2436,16 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
   const long long R = (long long)B * 400;
   PPO_REQUIRE(R < 0x7fffffffLL, "ppo_conv1_wgrad: B too large");
   const double fl = 2.0 * R * 32 * C * 64;
-  if (obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] == 2 && Z % 4 == 0) {
-    if (B <= 0 || Z <= 0) return 0;
-    int slot;
-    const bool prof = ppo_prof_begin("conv1_wgrad_u8", as_stream(stream), &slot);
-    conv1_wgrad_k8_kernel<4><<<Z / 4, 256, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
-                                                                  slab_bias);
-    if (prof) ppo_prof_end(slot, as_stream(stream), fl);
-    PPO_LAUNCH_CHECK("conv1_wgrad_k8_kernel");
-    return 0;
-  }
   if (obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] != 9) {
     if (B <= 0 || Z <= 0) return 0;
     int slot;
     const bool prof = ppo_prof_begin("conv1_wgrad_u8", as_stream(stream), &slot);
     if (g_products == 1)   // half-precision mode: bf16 dz
       conv1_wgrad_bf16x3_kernel<4, 1><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
-                                                                        slab, slab_bias);
+                                                                        slab, slab_bias, g_stagger >> 4);
     else
       conv1_wgrad_bf16x3_kernel<4><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
-                                                                     slab_bias);
+                                                                     slab_bias, g_stagger >> 4);
     if (prof) ppo_prof_end(slot, as_stream(stream), fl);
     PPO_LAUNCH_CHECK("conv1_wgrad_bf16x3_kernel");
     return 0;

@@ -1215,11 +1215,11 @@ def test_gru_step_kernels_vs_float64(gpu, M, H):
             assert err <= 2e-5 * max(v.abs().max().item(), 1.0), (variant, k, err)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 9])
 def test_conv1_wgrad_variants_vs_torch(gpu, variant):
     """conv1 weight + bias gradient from u8 observations gathered by index (the
-    minibatch path): the 8-wave kernel (1, default) and the one-k-group-per-wave
-    kernel (2) vs torch float64 on (u8 / 255): max |err| <= 1e-5 * max |ref|.
+    minibatch path): the image-resident bf16x3 kernel (1, default) and the fp32
+    tile GEMM (9) vs torch float64 on (u8 / 255): max |err| <= 1e-5 * max |ref|.
     B = 300 images, rows gathered out of order."""
     Hh = _hip()
     B, rows = 300, 420
