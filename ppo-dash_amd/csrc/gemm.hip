@@ -278,6 +278,204 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
   }
 }
 
+// conv1 weight gradient, part-pipelined (ppo_tune_set("conv1_wgrad", 3)): the
+// GEMM of conv1_wgrad_bf16x3_kernel (dW[co][(c,ky,kx)] = Σ_px dz1[px][co] ·
+// u[c][4oy+ky][4ox+kx], u8 pixels exact in bf16, dz = hi + mid + lo exactly:
+// three v_mfma_f32_32x32x16_bf16 per block pair), restaged so that the staging
+// overlaps the MFMAs:
+//   * an image is processed in 5 parts of 4 output rows (80 pixels = 5 k-steps);
+//     a part's operands are 42,496 B of LDS — two stages (85 KB) instead of one
+//     whole-image stage that fills the LDS;
+//       E   [c][20 rows][40 quad slots][4 px] bf16: row yr = input row 16p + yr,
+//           slot Q*8 + kx holds u[c][y][16Q + 4j + kx], j = 0..3 (the 4 pixels of
+//           an output-row quad for one kx); slot kx bits XOR ((item >> 1) & 7),
+//           item = row * 5 + Q, so the staging ds_write_b64 of 16 consecutive
+//           items and the B-fragment ds_read_b64 of 32 lanes (4 ky x 8 kx) are
+//           both conflict-free
+//       dzP [3 planes][32 co][88] bf16: dz of the part split once (no per-wave
+//           re-split), 176-B rows: conflict-free ds_read_b128 A fragments
+//   * wave w owns one 32-column tile (c = w >> 1, ky = 4 (w & 1) + .., all kx)
+//     for every k-step: no k-group partials to combine;
+//   * staggered: waves 0-3 stage part i+1 then compute part i, waves 4-7 the
+//     other way round, so each SIMD pairs one staging (VALU) wave with one
+//     computing (MFMA) wave; the loads of part i+2 are in flight meanwhile.
+// One barrier per part.  Output: the split-K slab [Z][32][256] (u8 integers: the
+// reduce applies 1/255) and bias partials [Z][32], as the other variants.
+template <int NPD = 3>   // NPD: dz parts summed (3 exact; 1 half-precision mode)
+__global__ __launch_bounds__(512) void conv1_wgrad_parts_kernel(const float* __restrict__ dz1,
+                                                                const uint8_t* __restrict__ obs,
+                                                                const int64_t* __restrict__ idx, long long row0,
+                                                                int B, float* __restrict__ slab,
+                                                                float* __restrict__ slab_bias, int dbg) {
+  // timing anatomy only (kbench --tune stagger=16*dbg; wrong results): 1 skips the
+  // MFMAs, 2 the staging (put), 4 the DMAs, 8 the stagger
+  const bool no_mma = dbg & 1, no_put = dbg & 2, no_dma = dbg & 4;
+  constexpr int C = 4, NPART = 5, ER = 20, SLOTS = 40, DZS = 88, MAXIMG = 512;
+  constexpr int E_BF = C * ER * SLOTS * 4, DZ_BF = 32 * DZS, STG = E_BF + 3 * DZ_BF;   // bf16 elements
+  // raw part, as 16-B LDS-DMA pieces: the 4 channels' 20 input rows (4 x 1,680 B =
+  // 420 pieces, 16-B aligned in the u8 storage row; 7 wave-instructions, padded to
+  // 448) then dz of the part's 80 pixels (10,240 B contiguous = 640 pieces)
+  constexpr int EPC = 105, EPIECE = 448, DPIECE = 640, RAWP = EPIECE + DPIECE;
+  __shared__ __attribute__((aligned(16))) uint16_t L[2 * STG];           // 84,992 B: two part stages
+  __shared__ __attribute__((aligned(16))) uint4 RAW[3][RAWP];            // 52,224 B: raw parts, 3-slot ring
+  __shared__ long long rowtab[MAXIMG];                                    // storage row of the block's images
+  __shared__ float bred[512];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int G = gridDim.x;
+  const int nimg = blockIdx.x < B ? (B - 1 - (int)blockIdx.x) / G + 1 : 0, nit = NPART * nimg;
+  for (int k = tid; k < nimg; k += 512) rowtab[k] = obs_row(idx, row0, (int)blockIdx.x + k * G);
+  // B column of this lane: n = 32 wave + l32 -> (c, ky, kx)
+  const int bc = wave >> 1, bky = 4 * (wave & 1) + (l32 >> 3), bkx = l32 & 7;
+  int qoff[5][2];   // E element offset of the lane's quads for local k-step ls
+#pragma unroll
+  for (int ls = 0; ls < 5; ++ls)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ql = 4 * ls + 2 * h + j, oyl = ql / 5, Q = ql - 5 * oyl;
+      const int r = bc * ER + 4 * oyl + bky, item = r * 5 + Q;
+      qoff[ls][j] = (r * SLOTS + Q * 8 + (bkx ^ ((item >> 1) & 7))) * 4;
+    }
+  const int aoff = E_BF + l32 * DZS + 8 * h;   // + plane * DZ_BF + 16 ls
+  // staging items: E item tid < 400 (row r = tid / 5 = c * 20 + yr, quad Q = tid % 5);
+  // dz item tid < 320 (co = tid & 31, pixel octet oc = tid >> 5).  Threads without
+  // an item DMA item 0's addresses (harmless duplicates) so every wave issues the
+  // same DMA count.
+  const bool e_on = tid < 400, d_on = tid < 320;
+  const int eit = e_on ? tid : 0, dit = d_on ? tid : 0;
+  const int er = eit / 5, eQ = eit - 5 * er, ec = er / ER, eyr = er - ER * ec, ef = (eit >> 1) & 7;
+  const int dco = dit & 31, doc = dit >> 5;
+  float bacc = 0.f;
+  // DMA of item j's raw part into RAW[j & 1]: wave w moves pieces 64 w + lane of
+  // the image rows (waves 0-6) and of dz (pieces 64 (w + 8 i) + lane, i = 0, 1)
+  auto dma = [&](int j) {
+    if (no_dma) return;
+    const int jj = j < nit ? j : nit - 1, k = jj / NPART, p = jj - NPART * k, b = (int)blockIdx.x + k * G;
+    uint4* dst = RAW[jj % 3];
+    if (wave < 7) {
+      const int piece = min(64 * wave + lane, C * EPC - 1), c = piece / EPC, r = piece - EPC * c;
+      const uint8_t* src = obs + rowtab[k] * (long long)(C * IMG2) + c * IMG2 + p * (16 * IMG) + 16 * r;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                       reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                           reinterpret_cast<uintptr_t>(dst + 64 * wave)), 16, 0, 0);
+    }
+    const char* dsrc = reinterpret_cast<const char*>(dz1 + (size_t)b * 12800 + p * 80 * 32);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int blk = wave + 8 * i;   // wave-uniform
+      if (blk < DPIECE / 64)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc + 16 * (64 * blk + lane)),
+                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                             reinterpret_cast<uintptr_t>(dst + EPIECE + 64 * blk)), 16, 0, 0);
+    }
+  };
+  auto put = [&](int j, int st) {   // item j: RAW[j % 3] -> stage st
+    if (no_put) return;
+    const uint32_t* R = reinterpret_cast<const uint32_t*>(RAW[j % 3]);
+    uint32_t ew[5];
+    float dv[8];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) ew[q] = R[(ec * 1680 + eyr * IMG + 16 * eQ) / 4 + q];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) dv[q] = __uint_as_float(R[4 * EPIECE + (8 * doc + q) * 32 + dco]);
+    uint16_t* S = L + st * STG;
+    if (e_on) {
+#pragma unroll
+      for (int kx = 0; kx < 8; ++kx) {   // u[16Q + 4i + kx] = byte (kx & 3) of dword i + (kx >> 2)
+        const int o = kx >> 2, sh = 8 * (kx & 3);
+        float f[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) f[i] = (float)((ew[i + o] >> sh) & 255u);
+        const uint2 q = {__builtin_amdgcn_perm(__float_as_uint(f[1]), __float_as_uint(f[0]), 0x07060302u),
+                         __builtin_amdgcn_perm(__float_as_uint(f[3]), __float_as_uint(f[2]), 0x07060302u)};
+        *reinterpret_cast<uint2*>(S + (er * SLOTS + eQ * 8 + (kx ^ ef)) * 4) = q;
+      }
+    }
+    if (d_on) {
+      Frag3 fr;
+      split8(f32x4{dv[0], dv[1], dv[2], dv[3]}, f32x4{dv[4], dv[5], dv[6], dv[7]}, fr, NPD == 1);
+      uint16_t* d = S + E_BF + dco * DZS + 8 * doc;
+      *reinterpret_cast<bf16x8*>(d) = fr.h;
+      if constexpr (NPD == 3) {
+        *reinterpret_cast<bf16x8*>(d + DZ_BF) = fr.m;
+        *reinterpret_cast<bf16x8*>(d + 2 * DZ_BF) = fr.l;
+      }
+      bacc += ((dv[0] + dv[1]) + (dv[2] + dv[3])) + ((dv[4] + dv[5]) + (dv[6] + dv[7]));
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  auto compute = [&](int st) {
+    if (no_mma) return;
+    const uint16_t* S = L + st * STG;
+#pragma unroll
+    for (int ls = 0; ls < 5; ++ls) {
+      const uint2 q1 = *reinterpret_cast<const uint2*>(S + qoff[ls][0]);
+      const uint2 q2 = *reinterpret_cast<const uint2*>(S + qoff[ls][1]);
+      const bf16x8 bq = __builtin_bit_cast(bf16x8, uint4{q1.x, q1.y, q2.x, q2.y});
+      const uint16_t* A = S + aoff + 16 * ls;
+      if constexpr (NPD == 3) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(A + 2 * DZ_BF), bq, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(A + DZ_BF), bq, acc, 0, 0, 0);
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(A), bq, acc, 0, 0, 0);
+    }
+  };
+  // pipeline: item j's pieces are DMA'd into RAW[j % 3] at item j - 3 (by every
+  // wave, a share each); at the end of item j - 2 every wave waits for its own
+  // share (vmcnt = one item's DMA count: item j + 1's may stay in flight) and the
+  // barrier publishes the slot; item j - 1 stages it (put) into LDS stage j & 1.
+  const int nops = (wave < 7 ? 1 : 0) + 1 + (wave + 8 < DPIECE / 64 ? 1 : 0);
+  auto wait_raw = [&]() {   // all but the youngest item's DMAs retired
+    if (nops == 3) __builtin_amdgcn_s_waitcnt(0x0F73);        // vmcnt(3)
+    else if (nops == 2) __builtin_amdgcn_s_waitcnt(0x0F72);   // vmcnt(2)
+    else __builtin_amdgcn_s_waitcnt(0x0F71);                  // vmcnt(1)
+  };
+  // block barrier that does not drain the in-flight DMAs (__syncthreads' release
+  // fence would wait for them: vmcnt(0)); LDS stores are retired by lgkmcnt(0),
+  // and the memory clobber keeps the compiler from moving LDS accesses across it
+  auto part_barrier = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  __syncthreads();   // rowtab
+  if (nit > 0) {
+    dma(0);
+    dma(1);
+    dma(2);
+    if (nops == 3) __builtin_amdgcn_s_waitcnt(0x0F76);        // vmcnt(6): item 0 retired
+    else if (nops == 2) __builtin_amdgcn_s_waitcnt(0x0F74);   // vmcnt(4)
+    else __builtin_amdgcn_s_waitcnt(0x0F72);                  // vmcnt(2)
+    part_barrier();
+    put(0, 0);
+    wait_raw();   // item 1 retired (item 2 may be in flight)
+  }
+  part_barrier();
+  const bool late = wave >= 4 && !(dbg & 8);
+  for (int i = 0; i < nit; ++i) {
+    const int st = i & 1;
+    const bool more = i + 1 < nit;
+    if (!late && more) put(i + 1, st ^ 1);
+    if (more) dma(i + 3);   // into RAW[i % 3]: item i was staged before the last barrier
+    compute(st);
+    if (late && more) put(i + 1, st ^ 1);
+    wait_raw();   // item i + 2 retired (item i + 3 may be in flight)
+    part_barrier();
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // drain the clamped tail DMAs before the block exits
+  float* out = slab + (size_t)blockIdx.x * 32 * 256;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int co = (r & 3) + 8 * (r >> 2) + 4 * h, n = 32 * wave + l32;
+    out[co * 256 + n] = acc[r];
+  }
+  bred[tid] = d_on ? bacc : 0.f;
+  __syncthreads();
+  if (tid < 32) {   // channel tid: its 10 pixel octets, fixed order
+    float t = 0.f;
+#pragma unroll
+    for (int o = 0; o < 10; ++o) t += bred[32 * o + tid];
+    slab_bias[(size_t)blockIdx.x * 32 + tid] = t;
+  }
+}
+
 // ReLU mask bits of a conv1 output [B][400][32]: bit c of word p = (a1[p][c] > 0),
 // for the conv1 paths without the fused epilogue (one thread per half pixel).
 __global__ __launch_bounds__(256) void relu_bits_kernel(const float* __restrict__ a1, long long halves,
@@ -1861,7 +2059,7 @@ static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad"
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
 static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measured best
-static int g_tune[TK_N] = {0, 8, 8, 8, 1, 0, 8, 1, 8, 8, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 8, 8, 8, 3, 0, 8, 1, 8, 8, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   if (strcmp(key, "stagger") == 0) {
@@ -2436,6 +2634,21 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
   const long long R = (long long)B * 400;
   PPO_REQUIRE(R < 0x7fffffffLL, "ppo_conv1_wgrad: B too large");
   const double fl = 2.0 * R * 32 * C * 64;
+  if (obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] == 3) {   // part-pipelined
+    if (B <= 0 || Z <= 0) return 0;
+    PPO_REQUIRE((B + Z - 1) / Z <= 512, "ppo_conv1_wgrad: %d images over %d blocks (at most 512 per block)", B, Z);
+    int slot;
+    const bool prof = ppo_prof_begin("conv1_wgrad_u8", as_stream(stream), &slot);
+    if (g_products == 1)   // half-precision mode: bf16 dz
+      conv1_wgrad_parts_kernel<1><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
+                                                                    slab_bias, 0);
+    else
+      conv1_wgrad_parts_kernel<3><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
+                                                                    slab_bias, g_stagger >> 4);
+    if (prof) ppo_prof_end(slot, as_stream(stream), fl);
+    PPO_LAUNCH_CHECK("conv1_wgrad_parts_kernel");
+    return 0;
+  }
   if (obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] != 9) {
     if (B <= 0 || Z <= 0) return 0;
     int slot;

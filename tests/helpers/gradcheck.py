@@ -7,11 +7,13 @@ import torch
 from oracle import ppo_oracle as O
 
 
-def check_grads(got_flat, ref_list, shapes, fp32_flat=None, fro_tol=3e-5, max_tol=1e-4):
+def check_grads(got_flat, ref_list, shapes, fp32_flat=None, fro_tol=3e-5, max_tol=1e-4, ratio=2.0, floor=1e-6):
     """Per tensor, against the float64 reference: relative Frobenius error
     ||err||/||ref|| <= fro_tol and max |err| <= max_tol * max|ref|; and, where the
     same gradient computed by torch's own fp32 autograd is given (fp32_flat: the
-    reference's precision), our Frobenius error <= 2x torch fp32's (+1e-7).
+    reference's precision), our Frobenius error <= ratio x torch fp32's + floor
+    (floor: 1e-6 relative, ~16 fp32 ulps — where torch's own error happens to be
+    far below that, e.g. a bias summed over few terms, the ratio alone is noise).
 
     Why not 1e-5 of max|ref| element-wise at these sizes: a weight gradient here
     sums 16 k - 26 M products (conv1 at 65,536 rows: 26 M per element) and a few
@@ -35,7 +37,7 @@ def check_grads(got_flat, ref_list, shapes, fp32_flat=None, fro_tol=3e-5, max_to
             e32 = f32[name] - ref
             mx32, fro32 = np.abs(e32).max() / scale, np.linalg.norm(e32) / norm
             line += f"  | torch-fp32 max {mx32:.2e} fro {fro32:.2e}"
-            ok = ok and fro <= 2.0 * fro32 + 1e-7
+            ok = ok and fro <= ratio * fro32 + floor
         print(line, flush=True)
         if not ok:
             bad.append(line)

@@ -1215,11 +1215,12 @@ def test_gru_step_kernels_vs_float64(gpu, M, H):
             assert err <= 2e-5 * max(v.abs().max().item(), 1.0), (variant, k, err)
 
 
-@pytest.mark.parametrize("variant", [1, 9])
+@pytest.mark.parametrize("variant", [1, 3, 9])
 def test_conv1_wgrad_variants_vs_torch(gpu, variant):
     """conv1 weight + bias gradient from u8 observations gathered by index (the
-    minibatch path): the image-resident bf16x3 kernel (1, default) and the fp32
-    tile GEMM (9) vs torch float64 on (u8 / 255): max |err| <= 1e-5 * max |ref|.
+    minibatch path): the image-resident bf16x3 kernel (1), the part-pipelined
+    kernel (3) and the fp32 tile GEMM (9) vs torch float64 on (u8 / 255):
+    max |err| <= 1e-5 * max |ref|.
     B = 300 images, rows gathered out of order."""
     Hh = _hip()
     B, rows = 300, 420
@@ -1233,6 +1234,7 @@ def test_conv1_wgrad_variants_vs_torch(gpu, variant):
     slab_b = torch.empty(Z * 32, device=gpu)
     gw = torch.empty(32 * 256, device=gpu)
     gb = torch.empty(32, device=gpu)
+    old = Hh.call("ppo_tune_get", b"conv1_wgrad")
     Hh.call("ppo_tune_set", b"conv1_wgrad", variant)
     try:
         Hh.call("ppo_conv1_wgrad", dz1_d.data_ptr(), obs_d.data_ptr(), 1, idx_d.data_ptr(), 0, 4, B, Z,
@@ -1241,7 +1243,7 @@ def test_conv1_wgrad_variants_vs_torch(gpu, variant):
                 gb.data_ptr(), 1.0 / 255, 0, _s())
         torch.cuda.synchronize()
     finally:
-        Hh.call("ppo_tune_set", b"conv1_wgrad", 1)
+        Hh.call("ppo_tune_set", b"conv1_wgrad", old)
     x = obs[idx].double() / 255.0
     dy = dz1.double().permute(0, 3, 1, 2)
     ref_w = torch.nn.grad.conv2d_weight(x, (32, 4, 8, 8), dy, stride=4)
