@@ -110,6 +110,20 @@ def profiled(products):
 TIMED = ("conv2_fwd", "conv2_dgrad", "conv2_wgrad", "conv3_fwd", "conv3_dgrad", "conv3_wgrad", "conv1_wgrad_u8",
          "conv1_fwd_u8")
 PROFILED = profiled(6)
+# compulsory HBM bytes per image of the image-resident conv kernels (fp32 NHWC
+# activations, u8 observations, ReLU mask bits) and the layer's MACs per image:
+# these kernels are MFMA- and HBM-heavy at once (conv1 wgrad reads 79 KB per
+# image for 3.3 M MACs), so both rooflines are reported
+CONV_HBM = {
+    "conv1_fwd_u8": (3276800, 28224 + 51200),
+    "conv1_wgrad_u8": (3276800, 51200 + 28224),          # dz1 + u8 image
+    "conv2_fwd": (2654208, 51200 + 20736),               # a1 + a2 (+ 648 B mask bits, training)
+    "conv2_dgrad": (2654208, 20736 + 1600 + 51200),      # dz2 + conv1 mask bits + dz1
+    "conv2_wgrad": (2654208, 20736 + 51200),             # dz2 + a1
+    "conv3_fwd": (903168, 20736 + 6272),
+    "conv3_dgrad": (903168, 6272 + 648 + 20736),
+    "conv3_wgrad": (903168, 6272 + 20736),
+}
 CONV1_FWD_BYTES_PER_FLOP = 79424.0 / (2.0 * 400 * 32 * 256)
 
 
@@ -329,7 +343,7 @@ def pmc_traffic(kernel, workload):
 PMC_SYMBOL = {"conv2_fwd": "conv2_fwd_x9_kernel<", "conv2_dgrad": "conv2_dgrad_x9_kernel<",
               "conv2_wgrad": "conv2_wgrad_x9_kernel<", "conv3_fwd": "conv3_fwd_x9_kernel<",
               "conv3_dgrad": "conv3_dgrad_x9_kernel<", "conv3_wgrad": "conv3_wgrad_x9_kernel<",
-              "conv1_wgrad_u8": "conv1_wgrad_bf16x3_kernel<", "conv1_fwd_u8": "conv1_fwd_bf16x3_kernel<"}
+              "conv1_wgrad_u8": "conv1_wgrad_parts_kernel<", "conv1_fwd_u8": "conv1_fwd_bf16x3_kernel<"}
 
 
 def pmc_mfma(workload):
@@ -455,6 +469,11 @@ def kernel_entry(name, launches, ms_total, work, products, where):
          "avg_launch_ms": round(ms_total / launches, 4), "instructions": how, "timed_in": where}
     if unit_kind != "bytes":
         e["fp32_tflops"] = round(work / (ms_total * 1e-3) / 1e12, 2)
+    if name in CONV_HBM:   # the same launches against HBM: compulsory bytes per image
+        macs, nbytes = CONV_HBM[name]
+        gbps = work / (2.0 * macs) * nbytes / (ms_total * 1e-3) / 1e9
+        e["hbm_view"] = {"bytes_per_image": nbytes, "achieved_gbps": round(gbps, 1),
+                         "frac_of_hbm_peak": round(gbps / PEAK_HBM_GBPS, 4)}
     return e
 
 
