@@ -925,6 +925,184 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restri
   }
 }
 
+// conv2 forward with two LDS stages (ppo_tune_set("conv2_fwd", 12)): the waves,
+// K halves and arithmetic of conv2_fwd_x9_kernel (bit-identical outputs), with
+// the next image's split staged into the second stage *during* the current
+// image's k-steps instead of in a phase of its own.
+//   * Compact parity layout, 400 16-B units per 8-channel chunk: pixel (y, x) at
+//     P = 100 (2 (y & 1) + (x & 1)) + 10 (y >> 1) + (x >> 1), so tap (ky, kx) of
+//     output pixel (oy, ox) reads v + toff(ky, kx), v = 10 oy + ox.  Row i of row
+//     tile t is the t-th pixel (by v) with v ≡ i (mod 16) (≤ 6 per residue: 6
+//     tiles; a missing one is a dummy row reading pixel v = i): the 16 lanes of
+//     a ds_read_b128 group read 16 distinct residues, conflict-free.  Two stages
+//     x 3 planes x 4 chunks x 400 x 16 B = 153,600 B.
+//   * The K-half partials (24,576 B) are handed over in the lo plane of the stage
+//     the image has just left: kh 1 writes them after barrier A, kh 0 reads them
+//     after barrier B; the next image's hi / mid parts are staged into that
+//     stage's planes 0-1 during k-steps 0-3, its lo parts held in registers
+//     until a mid-image barrier (after k-step 5) has retired the partial reads,
+//     then written during k-steps 6-7.  The image after next is fetched into
+//     registers from k-step 4 on.
+//   * Epilogue in the swapped MFMA orientation (weights as A): one 16-B store of
+//     four consecutive channels per tile, dummy rows dropped by buffer range.
+template <int NP, bool MASK = false>
+__global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restrict__ a1, int B,
+                                                           const uint16_t* __restrict__ wpl,
+                                                           const float* __restrict__ bias,
+                                                           float* __restrict__ out,
+                                                           uint16_t* __restrict__ mbits) {
+  constexpr int U = 400, PLN = 4 * U, STG = 3 * PLN, MT = 6, KS = 8, WN = 64 * 512;
+  constexpr int UNITS = 4 * U, UPER = (UNITS + 511) / 512;   // 4 units per thread (the 4th: wave 0)
+  __shared__ __attribute__((aligned(16))) bf16x8 S[2 * STG];
+  __shared__ int vtab[MT][16];
+  __shared__ int otab[MT][16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int nt = wave & 3, kh = wave >> 2, co = 16 * nt + i16;
+  if (tid < 16) {
+    int t = 0;
+    for (int v = tid; v <= 88; v += 16)
+      if (v % 10 != 9) {
+        vtab[t][tid] = v;
+        otab[t][tid] = 9 * (v / 10) + v % 10;
+        ++t;
+      }
+    for (; t < MT; ++t) {
+      vtab[t][tid] = tid;
+      otab[t][tid] = -1;
+    }
+  }
+  bf16x8 bw[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
+  const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
+  wait_vm0();
+  // staging unit u = tid + 512 j: chunk c = (u >> 3) & 3 of the pixel at compact
+  // position rho = 8 (u >> 5) + (u & 7): 8 consecutive lanes write 8 consecutive
+  // units (conflict-free ds_write_b128) and 4 lanes read one pixel's 128-B line
+  int usrc[UPER], udst[UPER];
+#pragma unroll
+  for (int j = 0; j < UPER; ++j) {
+    const int u = min(tid + 512 * j, UNITS - 1), rho = 8 * (u >> 5) + (u & 7), c = (u >> 3) & 3;
+    const int par = rho / 100, rem = rho - 100 * par, yh = rem / 10, xh = rem - 10 * yh;
+    const int y = 2 * yh + (par >> 1), x = 2 * xh + (par & 1);
+    usrc[j] = (y * 20 + x) * 8 + 2 * c;
+    udst[j] = c * U + rho;
+  }
+  const bool has_last = tid + 512 * (UPER - 1) < UNITS;
+  f32x4 stg[UPER][2];
+  bf16x8 lo[UPER];
+  auto fetch = [&](int b) {   // unconditional loads (the 4th unit of waves 1-7 reloads unit 1599)
+    const f32x4* src = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
+#pragma unroll
+    for (int j = 0; j < UPER; ++j) {
+      stg[j][0] = src[usrc[j]];
+      stg[j][1] = src[usrc[j] + 1];
+    }
+  };
+  auto put_hm = [&](int j, int st) {   // hi / mid parts now, lo part held
+    Frag3 f;
+    split8(stg[j][0], stg[j][1], f, NP == 1);
+    lo[j] = f.l;
+    if (j < UPER - 1 || has_last) {
+      bf16x8* d = S + st * STG + udst[j];
+      d[0] = f.h;
+      if constexpr (NP > 1) d[PLN] = f.m;
+    }
+  };
+  auto put_l = [&](int j, int st) {
+    if constexpr (NP > 1)
+      if (j < UPER - 1 || has_last) S[st * STG + 2 * PLN + udst[j]] = lo[j];
+  };
+  // block barrier that leaves the image prefetch in flight (__syncthreads' fence
+  // would drain every outstanding load): LDS ops retired, compiler fence
+  auto lds_barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  __syncthreads();   // vtab / otab
+  int vrow[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) vrow[t] = vtab[t][i16] + g * U;
+  const int G = gridDim.x;
+  int b = blockIdx.x, cur = 0;
+  if (b < B) {
+    fetch(b);
+#pragma unroll
+    for (int j = 0; j < UPER; ++j) {
+      put_hm(j, 0);
+      put_l(j, 0);
+    }
+    if (b + G < B) fetch(b + G);
+  }
+  __syncthreads();
+  for (; b < B; b += G) {
+    const bool nxt = b + G < B, nn = b + 2 * G < B;
+    const bf16x8* Sc = S + cur * STG;
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = zero4();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int tap = 8 * kh + s, ky = tap >> 2, kx = tap & 3;
+      const int toff = 100 * (2 * (ky & 1) + (kx & 1)) + 10 * (ky >> 1) + (kx >> 1);
+      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+#pragma unroll
+      for (int t0 = 0; t0 < MT; t0 += 3) {
+        Frag3 a[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const bf16x8* q = Sc + vrow[t0 + u] + toff;
+          a[u].h = q[0];
+          if constexpr (NP > 1) {
+            a[u].m = q[PLN];
+            a[u].l = q[2 * PLN];
+          }
+        }
+#define PPO_PART(X, Y) \
+  _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(w.Y, a[u].X, acc[t0 + u]);
+        PPO_PRODUCTS(NP, PPO_PART)
+#undef PPO_PART
+      }
+      if (s < UPER && nxt) put_hm(s, cur ^ 1);
+      if (s == UPER && nn) fetch(b + 2 * G);
+      if (s == 5) lds_barrier();   // mid-image: the previous image's partials (lo plane of stage cur ^ 1) are read
+      if (s >= 6 && nxt) {
+#pragma unroll
+        for (int j = 0; j < UPER; ++j)
+          if ((j & 1) == s - 6) put_l(j, cur ^ 1);
+      }
+    }
+    lds_barrier();   // A: stage cur consumed; stage cur ^ 1 complete
+    f32x4* R = reinterpret_cast<f32x4*>(S + cur * STG + 2 * PLN);   // partials in the lo plane just left
+    if (kh == 1) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t) R[(nt * MT + t) * 64 + lane] = acc[t];
+    }
+    lds_barrier();   // B: partials in LDS
+    if (kh == 0) {
+      const auto rs = make_rsrc(out + (size_t)b * (81 * 64), 81 * 64 * 4);
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const f32x4 v = acc[t] + R[(nt * MT + t) * 64 + lane];
+        const int m = otab[t][i16];
+        f32x4 y;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
+        bstore_f32x4(y, rs, m >= 0 ? 4 * (m * 64 + 16 * nt + 4 * g) : -1);
+        if constexpr (MASK) {   // ReLU mask bits of pixel m, channels 16 nt .. +15: 4 lanes' nibbles
+          int nib = 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) nib |= (y[r] > 0.f ? 1 : 0) << r;
+          const int w16 = nib | (__shfl_down(nib, 16, 64) << 4) | (__shfl_down(nib, 32, 64) << 8) |
+                          (__shfl_down(nib, 48, 64) << 12);
+          if (g == 0 && m >= 0) mbits[((size_t)b * 81 + m) * 4 + nt] = (uint16_t)w16;
+        }
+      }
+    }
+    cur ^= 1;
+  }
+}
+
 // conv2 forward, LDS-DMA staged variant of conv2_fwd_x9_kernel (same layout,
 // same math, bit-identical results).  The register-staged kernel loses ~45 % of
 // its time in the per-image staging phase: the next image's global loads sit
@@ -2059,7 +2237,7 @@ static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad"
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
 static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measured best
-static int g_tune[TK_N] = {0, 8, 8, 8, 3, 0, 8, 1, 8, 8, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 8, 8, 8, 3, 0, 12, 1, 8, 8, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   if (strcmp(key, "stagger") == 0) {
@@ -2290,13 +2468,29 @@ PPO_API int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const f
 
 static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float* b2, float* out, uint16_t* mbits,
                           void* stream) {
-  if (mbits && g_tune[TK_CONV2_FWD] != 8) {   // no fused mask epilogue
+  if (mbits && g_tune[TK_CONV2_FWD] != 8 && g_tune[TK_CONV2_FWD] != 12) {   // no fused mask epilogue
     const int rc = conv2_fwd_impl(a1, B, w2p, b2, out, nullptr, stream);
     if (rc != 0 || B <= 0) return rc;
     const long long halves = (long long)B * 81 * 4;
     const long long nb = (halves + 255) / 256;
     relu_bits_kernel<<<(unsigned)(nb < 8192 ? nb : 8192), 256, 0, as_stream(stream)>>>(out, halves, mbits);
     PPO_LAUNCH_CHECK("relu_bits_kernel");
+    return 0;
+  }
+  if (g_tune[TK_CONV2_FWD] == 12) {   // two LDS stages, staging inside the k-steps
+    if (B <= 0) return 0;
+    const int n_cu = device_cus();
+    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+    int slot;
+    const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
+    const uint16_t* wpl = planes_of(w2p, 64 * 512);
+    hipStream_t st = as_stream(stream);
+    if (mbits && g_products == 9) conv2_fwd_x9c_kernel<9, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+    else if (mbits && g_products == 1) conv2_fwd_x9c_kernel<1, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+    else if (mbits) conv2_fwd_x9c_kernel<6, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+    else PPO_LAUNCH_NP(conv2_fwd_x9c_kernel, nb, 512, st, a1, B, wpl, b2, out, nullptr);
+    if (prof) ppo_prof_end(slot, st, 2.0 * B * 81 * 64 * 512);
+    PPO_LAUNCH_CHECK("conv2_fwd_x9c_kernel");
     return 0;
   }
   if (g_tune[TK_CONV2_FWD] == 10) {   // LDS-DMA staged

@@ -795,12 +795,13 @@ def test_conv2_dgrad_variants_vs_torch(gpu, variant):
     a1 = torch.randn(B, 20, 20, 32, generator=g)
     dz1 = torch.full((B, 20, 20, 32), float("nan"), device=gpu)
     dz2_d, a1_d = dz2.cuda(), a1.cuda()
+    old_tune = Hh.call("ppo_tune_get", b"conv2_dgrad")
     Hh.call("ppo_tune_set", b"conv2_dgrad", variant)
     try:
         Hh.call("ppo_conv2_dgrad", dz2_d.data_ptr(), B, pk[5], a1_d.data_ptr(), dz1.data_ptr(), _s())
         torch.cuda.synchronize()
     finally:
-        Hh.call("ppo_tune_set", b"conv2_dgrad", 8)
+        Hh.call("ppo_tune_set", b"conv2_dgrad", old_tune)
     ref = F.conv_transpose2d(dz2.double().permute(0, 3, 1, 2), w["w2"].double(), stride=2).permute(0, 2, 3, 1)
     ref = torch.where(a1 > 0, ref, torch.zeros((), dtype=torch.float64))
     err = (dz1.cpu().double() - ref).abs().max().item()
@@ -824,6 +825,7 @@ def test_conv1_mask_bits_and_conv2_dgrad_bits(gpu, conv1_variant):
     a1 = torch.full((B, 20, 20, 32), float("nan"), device=gpu)
     a1m = torch.full_like(a1, float("nan"))
     bits = torch.zeros(B * 400, dtype=torch.int32, device=gpu)
+    old_tune = Hh.call("ppo_tune_get", b"conv1_fwd")
     Hh.call("ppo_tune_set", b"conv1_fwd", conv1_variant)
     try:
         Hh.call("ppo_conv1_fwd", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, w1.data_ptr(), b1.data_ptr(),
@@ -832,7 +834,7 @@ def test_conv1_mask_bits_and_conv2_dgrad_bits(gpu, conv1_variant):
                 a1m.data_ptr(), bits.data_ptr(), _s())
         torch.cuda.synchronize()
     finally:
-        Hh.call("ppo_tune_set", b"conv1_fwd", 0)
+        Hh.call("ppo_tune_set", b"conv1_fwd", old_tune)
     assert torch.equal(a1, a1m)
     live = (a1 > 0).reshape(B * 400, 32).cpu().to(torch.int64)
     want = (live << torch.arange(32, dtype=torch.int64)).sum(1)
@@ -850,7 +852,7 @@ def test_conv1_mask_bits_and_conv2_dgrad_bits(gpu, conv1_variant):
     assert torch.equal(d_ref, d_bits)
 
 
-@pytest.mark.parametrize("conv2_variant", [8, 0])
+@pytest.mark.parametrize("conv2_variant", [8, 0, 12])
 def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu, conv2_variant):
     """ppo_conv2_fwd_mask (fused ballot epilogue: variant 8; conv + relu_bits
     kernel: variant 0) writes bit c of word p = (a2[p][c] > 0) of its own fp32
@@ -865,13 +867,14 @@ def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu, conv2_variant):
     a2 = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
     a2m = torch.full_like(a2, float("nan"))
     bits = torch.zeros(B * 81, dtype=torch.int64, device=gpu)
+    old = Hh.call("ppo_tune_get", b"conv2_fwd")
     Hh.call("ppo_tune_set", b"conv2_fwd", conv2_variant)
     try:
         Hh.call("ppo_conv2_fwd", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2.data_ptr(), _s())
         Hh.call("ppo_conv2_fwd_mask", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2m.data_ptr(), bits.data_ptr(), _s())
         torch.cuda.synchronize()
     finally:
-        Hh.call("ppo_tune_set", b"conv2_fwd", 8)
+        Hh.call("ppo_tune_set", b"conv2_fwd", old)
     assert torch.equal(a2, a2m)
     live = (a2 > 0).reshape(B * 81, 64).cpu()
     got = bits.cpu()
@@ -889,11 +892,11 @@ def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu, conv2_variant):
     assert torch.equal(d_ref, d_bits)
 
 
-@pytest.mark.parametrize("variant", [0, 8, 10])
+@pytest.mark.parametrize("variant", [0, 8, 10, 12])
 def test_conv2_fwd_variants_vs_torch(gpu, variant):
     """conv2 forward (4x4 stride 2, 20x20x32 -> 9x9x64, bias + ReLU): the split-bf16
     tile GEMM (0), the image-resident kernels (8: register-staged, 10: LDS-DMA
-    staged) vs torch float64:
+    staged, 12: two stages, staging inside the k-steps) vs torch float64:
     max |err| <= 1e-5 * max |ref|.  B = 300 > the persistent grid."""
     Hh = _hip()
     B = 300
@@ -903,7 +906,7 @@ def test_conv2_fwd_variants_vs_torch(gpu, variant):
     b2 = torch.randn(64, generator=g) * 0.1
     a1_d, b2_d = a1.cuda(), b2.cuda()
     out = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
-    old = 8   # the default
+    old = Hh.call("ppo_tune_get", b"conv2_fwd")
     Hh.call("ppo_tune_set", b"conv2_fwd", variant)
     try:
         Hh.call("ppo_conv2_fwd", a1_d.data_ptr(), B, pk[0], b2_d.data_ptr(), out.data_ptr(), _s())
@@ -932,6 +935,7 @@ def test_conv2_wgrad_variants_vs_torch(gpu, variant):
     slab_b = torch.empty(Z * 64, device=gpu)
     gw = torch.empty(64 * 512, device=gpu)
     gb = torch.empty(64, device=gpu)
+    old_tune = Hh.call("ppo_tune_get", b"conv2_wgrad")
     Hh.call("ppo_tune_set", b"conv2_wgrad", variant)
     try:
         Hh.call("ppo_conv2_wgrad", dz2_d.data_ptr(), a1_d.data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), _s())
@@ -939,7 +943,7 @@ def test_conv2_wgrad_variants_vs_torch(gpu, variant):
                 gb.data_ptr(), 1.0, 0, _s())
         torch.cuda.synchronize()
     finally:
-        Hh.call("ppo_tune_set", b"conv2_wgrad", 8)
+        Hh.call("ppo_tune_set", b"conv2_wgrad", old_tune)
     x, dy = a1.double().permute(0, 3, 1, 2), dz2.double().permute(0, 3, 1, 2)
     ref_w = torch.nn.grad.conv2d_weight(x, (64, 32, 4, 4), dy, stride=2)
     ref_b = dy.sum((0, 2, 3))
@@ -996,12 +1000,13 @@ def test_conv3_dgrad_variants_vs_torch(gpu, variant):
     a2 = torch.randn(B, 9, 9, 64, generator=g)
     dz3_d, a2_d = dz3.cuda(), a2.cuda()
     dz2 = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
+    old_tune = Hh.call("ppo_tune_get", b"conv3_dgrad")
     Hh.call("ppo_tune_set", b"conv3_dgrad", variant)
     try:
         Hh.call("ppo_conv3_dgrad", dz3_d.data_ptr(), B, pk[4], a2_d.data_ptr(), dz2.data_ptr(), _s())
         torch.cuda.synchronize()
     finally:
-        Hh.call("ppo_tune_set", b"conv3_dgrad", 8)
+        Hh.call("ppo_tune_set", b"conv3_dgrad", old_tune)
     ref = F.conv_transpose2d(dz3.double().permute(0, 3, 1, 2), w["w3"].double()).permute(0, 2, 3, 1)
     ref = torch.where(a2 > 0, ref, torch.zeros((), dtype=torch.float64))
     err = (dz2.cpu().double() - ref).abs().max().item()
@@ -1021,15 +1026,44 @@ def test_conv3_fwd_variants_vs_torch(gpu, variant):
     b3 = torch.randn(32, generator=g) * 0.1
     a2_d, b3_d = a2.cuda(), b3.cuda()
     out = torch.full((B, 7, 7, 32), float("nan"), device=gpu)
+    old_tune = Hh.call("ppo_tune_get", b"conv3_fwd")
     Hh.call("ppo_tune_set", b"conv3_fwd", variant)
     try:
         Hh.call("ppo_conv3_fwd", a2_d.data_ptr(), B, pk[1], b3_d.data_ptr(), out.data_ptr(), _s())
         torch.cuda.synchronize()
     finally:
-        Hh.call("ppo_tune_set", b"conv3_fwd", 8)
+        Hh.call("ppo_tune_set", b"conv3_fwd", old_tune)
     ref = torch.relu(F.conv2d(a2.double().permute(0, 3, 1, 2), w["w3"].double(), b3.double())).permute(0, 2, 3, 1)
     err = (out.cpu().double() - ref).abs().max().item()
     assert err <= 1e-5 * ref.abs().max().item(), err
+
+
+def test_conv2_fwd_two_stage_bit_identical(gpu):
+    """conv2 forward variant 12 (two compact LDS stages, staging inside the
+    k-steps, partials handed over in the vacated stage) computes exactly the
+    products and sums of variant 8: outputs and ReLU mask bits bit-identical,
+    B = 300 and the rollout-like B = 7 (fewer images than blocks)."""
+    Hh = _hip()
+    _, packed, pk = _packed(gpu, 64, 71)
+    g = torch.Generator().manual_seed(72)
+    old = Hh.call("ppo_tune_get", b"conv2_fwd")
+    try:
+        for B in (300, 7):
+            a1 = torch.relu(torch.randn(B, 20, 20, 32, generator=g)).cuda()
+            b2 = (torch.randn(64, generator=g) * 0.1).cuda()
+            res = []
+            for v in (8, 12):
+                Hh.call("ppo_tune_set", b"conv2_fwd", v)
+                o = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
+                bits = torch.zeros(B * 81, dtype=torch.int64, device=gpu)
+                Hh.call("ppo_conv2_fwd_mask", a1.data_ptr(), B, pk[0], b2.data_ptr(), o.data_ptr(), bits.data_ptr(),
+                        _s())
+                torch.cuda.synchronize()
+                res.append((o, bits))
+            assert not torch.isnan(res[0][0]).any()
+            assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    finally:
+        Hh.call("ppo_tune_set", b"conv2_fwd", old)
 
 
 def test_stagger_bit_identical(gpu):
@@ -1089,6 +1123,7 @@ def test_conv3_wgrad_variants_vs_torch(gpu, variant):
     slab_b = torch.empty(Z * 32, device=gpu)
     gw = torch.empty(32 * 576, device=gpu)
     gb = torch.empty(32, device=gpu)
+    old_tune = Hh.call("ppo_tune_get", b"conv3_wgrad")
     Hh.call("ppo_tune_set", b"conv3_wgrad", variant)
     try:
         Hh.call("ppo_conv3_wgrad", dz3_d.data_ptr(), a2_d.data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), _s())
@@ -1096,7 +1131,7 @@ def test_conv3_wgrad_variants_vs_torch(gpu, variant):
                 gb.data_ptr(), 1.0, 0, _s())
         torch.cuda.synchronize()
     finally:
-        Hh.call("ppo_tune_set", b"conv3_wgrad", 8)
+        Hh.call("ppo_tune_set", b"conv3_wgrad", old_tune)
     x, dy = a2.double().permute(0, 3, 1, 2), dz3.double().permute(0, 3, 1, 2)
     ref_w = torch.nn.grad.conv2d_weight(x, (32, 64, 3, 3), dy)
     ref_b = dy.sum((0, 2, 3))
