@@ -1861,60 +1861,73 @@ __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __rest
 // conv2 dgrad, image-resident on the bf16 matrix cores (exact split, DESIGN.md
 // §3): the phase-merged GEMM of Conv2Dgrad (n = (phase, ci), k = (tap, co)),
 // one persistent block (8 waves) per CU walking images.  Per image the LDS holds
-// dz2 already split into three bf16 planes, as a zero-padded 12 x 11 pixel grid
-// (dz2 pixel (oy, ox) at (oy + 1, ox + 1)): 2 stages x 50,688 B, the next image
-// in flight into registers, so the k loop has no staging, no barrier and no
-// range tests.  GEMM rows run over the padded grid too: m = 11 yy + xx (xx = 10 is
-// a dummy column, 110 rows in 7 tiles of 16 — the padding 100 rows would need
-// anyway), so row m's tap (ty, tx) is grid pixel m + 12 - (11 ty + tx).
-//   k order: k-step s takes co 8s .. 8s+7 of all four taps, lane group g = tap
-//   (ty, tx) = (g >> 1, g & 1): the A fragment of lane (row i, g) is one 16-B
-//   read per plane, and a 16-lane ds_read_b128 group reads 16 consecutive grid
-//   pixels — conflict-free with chunk c of pixel p stored at c ^ ((p >> 1) & 7)
-//   (128-B pixel rows: slot = 8 (p & 1) + chunk).  W2d [128][(tap, co)] needs no
-//   repacking: lane (n, g) of k-step s reads W2d[n][64 g + 8 s .. +7].
+// dz2 already split into three bf16 planes, as a zero-padded 12 x 10 pixel grid
+// (dz2 pixel (oy, ox) at (oy + 1, ox + 1); column 10 of a row is column 0 of the
+// next, also zero): 2 stages x 51,840 B, the next image in flight into registers,
+// so the k loop has no staging, no barrier and no range tests.  GEMM row m =
+// 10 yy + xx is the dz1 phase pixel (yy, xx); its tap (ty, tx) is grid pixel
+// m + 11 - (10 ty + tx).  A pixel is 144 B (64 co + 8 pad): 16 consecutive
+// pixels start on 16 distinct 16-B bank slots (36 p mod 64, 9 odd), so the
+// fragment reads are conflict-free without a swizzle and every (tile, k-step)
+// offset is an immediate.
+//   Border taps skipped: the rows run in 7 tiles — top row yy = 0 (10 pixels),
+// five interior tiles (m = 10 .. 89, exact), bottom row yy = 9.  k-step s takes
+// tap row ty = s & 1, lane group g = (tx = g & 1, co 16 (s >> 1) + 8 (g >> 1)):
+// the top tile (ty = 1 reads only zero padding there) runs the even k-steps, the
+// bottom tile (ty = 0) the odd ones: 48 tile-k-steps per image instead of 56 —
+// 6 tiles every k-step (7 -> 1.87 ms per 65,536-image minibatch from 2.03).
+// The k loop is software-pipelined over half k-steps (two groups of 3 tiles:
+// the next group's fragments are read while the current group's MFMAs run;
+// compute alone 1.41 -> 1.36 ms).  W2d [128][(ty, tx, co)] as packed: lane (n, g) of
+// k-step s reads W2d[n][128 ty + 64 tx + 16 (s >> 1) + 8 (g >> 1) .. +7].
 // Wave w owns n tile w (phase w >> 1, ci 16 (w & 1) + [0, 16)) for all of K,
 // its weight fragments (pre-split planes, 8 k-steps x 3) in 96 VGPRs.
+// Swapped operands (weights as A, pixels as B): lane (i16, g) holds row
+// mrow(t) + i16 and the 4 consecutive channels 4g .. 4g+3 of its n tile — one
+// 16-B store per tile; dummy rows get an out-of-range buffer offset (the store
+// is dropped) instead of a branch.  The stores of image b are issued during
+// image b + G's k-steps (one row tile per k-step) from registers masked at the
+// end of image b, instead of all waves storing 51.2 KB at once before the barrier.
 // BITS: the ReLU mask comes as bits (a1 points at u32 words [B][400] from
 // ppo_conv1_fwd_mask, 1.6 KB per image) instead of the fp32 activations
-// (51.2 KB per image): 40 % less HBM traffic, 12 % less time (measured with the
-// mask loads removed: 2.14 vs 2.43 ms at the c3 minibatch).
-template <int NP, bool BITS = false, bool DEFER = false>
+// (51.2 KB per image): 40 % less HBM traffic, 12 % less time.
+template <int NP, bool BITS = false>
 __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __restrict__ dz2, int B,
                                                             const uint16_t* __restrict__ wpl,
                                                             const float* __restrict__ a1,
                                                             float* __restrict__ dz1, int stagger) {
-  constexpr int HO = 9, CO = 64, GW = 11, GP = 12 * GW, ROW = CO, PL = GP * ROW, MT = 7, KS = 8;
+  constexpr int HO = 9, CO = 64, GW = 10, GP = 12 * GW, PS = 72, PL = GP * PS, MT = 7, KS = 8;
   constexpr int CH = HO * HO * CO / 8, PER = (CH + 511) / 512, WN = 128 * 256;
   __shared__ __attribute__((aligned(16))) uint16_t S[2][3][PL];
-  __shared__ int etab[16 * MT];   // row m -> output offset yy*1280 + xx*64 (or -1: dummy row)
-  // ReLU mask of a1 (conv1's output) for the image: one byte per element,
-  // staged like dz2 (coalesced 16-B loads one image ahead, in registers)
-  constexpr int MC = 400 * 32 / 4, MPER = (MC + 511) / 512;
+  __shared__ int etab[16 * MT];   // row (t, i16) -> output offset yy*1280 + xx*64 (or -1: dummy row)
+  // ReLU mask of a1 (conv1's output) for the image: bits, or one byte per
+  // element, staged like dz2 (coalesced 16-B loads one image ahead, in registers)
+  constexpr int MC = BITS ? 400 : 400 * 32 / 4, MPER = (MC + 511) / 512;
   __shared__ __attribute__((aligned(16))) uint32_t Mk[2][MC];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
-  const int n = 16 * wave + i16, ph = wave >> 1, ci = 16 * (wave & 1) + i16;
+  const int n = 16 * wave + i16, ph = wave >> 1;
+  constexpr auto mrow = [](int t) { return t == 0 ? 0 : t == MT - 1 ? 90 : 16 * t - 6; };
   bf16x8 bw[KS][3];
 #pragma unroll
   for (int s = 0; s < KS; ++s)
 #pragma unroll
     for (int p = 0; p < 3; ++p)
-      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + n * 256 + 64 * g + 8 * s);
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + n * 256 + 128 * (s & 1) + 64 * (g & 1) +
+                                                  16 * (s >> 1) + 8 * (g >> 1));
   wait_vm0();
   // zero the pad pixels of both stages (staging only ever writes the 81 real ones)
-  for (int i = tid; i < 2 * 3 * GP * 8; i += 512) {
-    const int c = i % (GP * 8), p = c >> 3, py = p / GW, px = p - GW * py;
-    if (py == 0 || py >= 10 || px == 0 || px == 10)
-      *reinterpret_cast<uint4*>(&S[i / (3 * GP * 8)][(i / (GP * 8)) % 3][8 * c]) = uint4{0, 0, 0, 0};
+  for (int i = tid; i < 2 * 3 * GP * 9; i += 512) {
+    const int c = i % (GP * 9), p = c / 9, py = p / GW, px = p - GW * py;
+    if (py == 0 || py >= 10 || px == 0)
+      *reinterpret_cast<uint4*>(&S[i / (3 * GP * 9)][(i / (GP * 9)) % 3][8 * c]) = uint4{0, 0, 0, 0};
   }
   if (tid < 16 * MT) {
-    const int yy = tid / GW, xx = tid - GW * yy;
-    etab[tid] = (yy < 10 && xx < 10) ? yy * 1280 + xx * 64 : -1;
+    const int t = tid >> 4, r = tid & 15, m = mrow(t) + r;
+    etab[tid] = ((t == 0 || t == MT - 1) && r >= 10) ? -1 : (m / 10) * 1280 + (m % 10) * 64;
   }
-  // byte offset of this lane's A fragment, row tile 0, k-step 0 (tile t adds 16
-  // pixels = 2048 B, k-step s XORs 16 s — both leave the swizzle term unchanged)
-  const int pa = i16 + 12 - (11 * (g >> 1) + (g & 1));
-  const int abase = pa * 128 + 16 * ((pa >> 1) & 7);
+  // byte offset of this lane's fragment at row 0, ty 0, k-step 0; (tile t, k-step
+  // s) adds 144 (mrow(t) - 10 (s & 1)) + 32 (s >> 1): an immediate
+  const int abase = (i16 + 11 - (g & 1)) * (2 * PS) + 16 * (g >> 1);
   f32x4 stg[PER][2];
   f32x4 mst[BITS ? 1 : MPER];
   uint4 mbv;
@@ -1955,7 +1968,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
       const int c = tid + 512 * j;
       if (c < CH) {
         const int r = c >> 3, oy = r / HO, p = (oy + 1) * GW + (r - HO * oy) + 1;
-        const int off = p * ROW + 8 * ((c & 7) ^ ((p >> 1) & 7));
+        const int off = p * PS + 8 * (c & 7);
         Frag3 f;
         split8(stg[j][0], stg[j][1], f, false);
         *reinterpret_cast<bf16x8*>(&S[buf][0][off]) = f.h;
@@ -1966,10 +1979,6 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
   };
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
-  // (Tried: a software-pipelined epilogue — image b's stores issued after image
-  // b+1's loads, through a range-checked buffer resource — measured neutral,
-  // 2.454 vs 2.467 ms at the c3 minibatch; it is in the history, commit 3585bac.)
-  const int cb = (ph >> 1) * 640 + (ph & 1) * 32 + ci;
   if (b < B) {
     fetch(b);
     put(0);
@@ -1980,14 +1989,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
   // timing anatomy only (tools/kbench.py --tune stagger=...; wrong results):
   // 16 skips the MFMAs, 32 the epilogue stores, 64 the staging of the next image
   const bool no_mma = stagger & 16, no_epi = stagger & 32, no_stage = stagger & 64;
-  // DEFER: the stores of image b are issued during image b + G's k-steps (one
-  // row tile per k-step) from registers masked at the end of image b, instead of
-  // all waves storing 51.2 KB per image at once before the barrier; dummy rows
-  // get an out-of-range buffer offset (the store is dropped) instead of a branch
-  // DEFER also swaps the MFMA operands (weights as A, pixels as B): lane (i16, g)
-  // then holds grid row 16 t + i16 and the 4 consecutive channels 4g .. 4g+3 of
-  // its n tile — one 16-B store per tile instead of four scattered dwords.
-  f32x4 eacc[DEFER ? MT : 1];
+  f32x4 eacc[MT];
   int bprev = -1;
   const int cbs = (ph >> 1) * 640 + (ph & 1) * 32 + 16 * (wave & 1) + 4 * g;
   auto store_tile = [&](int t, const f32x4& v, int bp) {
@@ -2000,63 +2002,67 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
       if (b + G < B) put(cur ^ 1);
       if (b + 2 * G < B) fetch(b + 2 * G);
     }
-    const char* Sb = reinterpret_cast<const char*>(S[cur][0]);
+    const char* Sb = reinterpret_cast<const char*>(S[cur][0]) + abase;
     f32x4 acc[MT];
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = zero4();
+    if (no_mma) {   // anatomy only
+      if (bprev >= 0 && !no_epi)
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const char* As = Sb + (abase ^ (16 * s));
-      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
-      // two groups of row tiles (4 + 3: register budget); within a group the
-      // part products, smallest first, go round the tiles
+        for (int t = 0; t < MT; ++t) store_tile(t, eacc[t], bprev);
+    } else {
+      // software pipeline over half k-steps: group 0 = {border tile of the tap
+      // row, tiles 1, 2}, group 1 = tiles 3-5; the fragments of the next group
+      // are read while the current one's MFMAs run (2 x 36 VGPRs)
+      Frag3 fr[2][3];
+      auto tile_of = [](int s, int grp, int u) {
+        return grp == 0 ? (u == 0 ? ((s & 1) ? MT - 1 : 0) : u) : 3 + u;
+      };
+      auto ld = [&](int s, int grp) {
 #pragma unroll
-      for (int t0 = 0; t0 < MT; t0 += 4) {
-        if (no_mma) break;
-        constexpr int TG = 4;
-        Frag3 a[TG];
-#pragma unroll
-        for (int u = 0; u < TG; ++u)
-          if (t0 + u < MT) {
-            const char* q = As + 2048 * (t0 + u);
-            a[u].h = *reinterpret_cast<const bf16x8*>(q);
-            a[u].m = *reinterpret_cast<const bf16x8*>(q + 2 * PL);
-            a[u].l = *reinterpret_cast<const bf16x8*>(q + 4 * PL);
-          }
-#define PPO_PART(X, Y)                                                  \
-  _Pragma("unroll") for (int u = 0; u < TG; ++u) if (t0 + u < MT)       \
-    acc[t0 + u] = DEFER ? mma(w.Y, a[u].X, acc[t0 + u]) : mma(a[u].X, w.Y, acc[t0 + u]);
+        for (int u = 0; u < 3; ++u) {
+          const int t = tile_of(s, grp, u);
+          const char* q = Sb + 2 * PS * (mrow(t) - 10 * (s & 1)) + 32 * (s >> 1);
+          fr[grp][u].h = *reinterpret_cast<const bf16x8*>(q);
+          fr[grp][u].m = *reinterpret_cast<const bf16x8*>(q + 2 * PL);
+          fr[grp][u].l = *reinterpret_cast<const bf16x8*>(q + 4 * PL);
+        }
+      };
+      auto mm = [&](int s, int grp) {
+        const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+#define PPO_PART(X, Y)                                                                \
+  _Pragma("unroll") for (int u = 0; u < 3; ++u) {                                     \
+    const int t = tile_of(s, grp, u);                                                 \
+    acc[t] = mma(w.Y, fr[grp][u].X, acc[t]);                                          \
+  }
         PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
-      }
-      if constexpr (DEFER)
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        ld(s, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(s, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 < KS) ld(s + 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(s, 1);
         if (s < MT && bprev >= 0 && !no_epi) store_tile(s, eacc[s], bprev);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
-    // epilogue: C row 4g + r of tile t is grid row m = 16t + 4g + r; ReLU mask of a1
-    const uint8_t* mk = reinterpret_cast<const uint8_t*>(Mk[cur]);
+    // masked results of this image, stored during the next one's k-steps:
+    // C row 4g + r of the swapped tile is channel 4g + r of pixel row (t, i16)
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
-      if constexpr (DEFER) {
-        const int i = max(etab[16 * t + i16], 0) + cbs;   // element (pixel i >> 5, channels (i & 31) + r)
-        const uint32_t mw = Mk[cur][i >> 5] >> (i & 31);
+      const int i = max(etab[16 * t + i16], 0) + cbs;   // element (pixel i >> 5, channels (i & 31) + r)
+      const uint32_t mw = Mk[cur][i >> 5] >> (i & 31);
+      const uint8_t* mk = reinterpret_cast<const uint8_t*>(Mk[cur]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool keep = BITS ? ((mw >> r) & 1u) != 0 : mk[i + r] != 0;
-          eacc[t][r] = keep ? acc[t][r] : 0.f;
-        }
-        continue;
-      }
-      const int4 e = *reinterpret_cast<const int4*>(&etab[16 * t + 4 * g]);
-      const int eo[4] = {e.x, e.y, e.z, e.w};
-      if (!no_epi) {
-        float* dm = dz1 + (size_t)b * 12800;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (eo[r] >= 0) {
-            const int i = eo[r] + cb;
-            const bool keep = BITS ? ((Mk[cur][i >> 5] >> (i & 31)) & 1u) != 0 : mk[i] != 0;
-            dm[i] = keep ? acc[t][r] : 0.f;
-          }
+      for (int r = 0; r < 4; ++r) {
+        const bool keep = BITS ? ((mw >> r) & 1u) != 0 : mk[i + r] != 0;
+        eacc[t][r] = keep ? acc[t][r] : 0.f;
       }
     }
     bprev = b;
@@ -2067,11 +2073,10 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
     __syncthreads();   // every wave is done with S[cur]; S[cur ^ 1] is complete
     cur ^= 1;
   }
-  if constexpr (DEFER)
-    if (bprev >= 0 && !no_epi) {
+  if (bprev >= 0 && !no_epi) {
 #pragma unroll
-      for (int t = 0; t < MT; ++t) store_tile(t, eacc[t], bprev);
-    }
+    for (int t = 0; t < MT; ++t) store_tile(t, eacc[t], bprev);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2761,8 +2766,6 @@ static int conv2_dgrad_img(const float* dz2, int B, const float* w2d, const floa
   const int sg = g_stagger & ~2;
   if (g_products == 9) conv2_dgrad_x9_kernel<9, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
   else if (g_products == 1) conv2_dgrad_x9_kernel<1, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
-  else if (g_stagger & 2)
-    conv2_dgrad_x9_kernel<6, BITS, true><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
   else conv2_dgrad_x9_kernel<6, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
   if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
   PPO_LAUNCH_CHECK("conv2_dgrad_x9_kernel");

@@ -10,7 +10,7 @@ for B in $BS; do
   for e in "${ENTRIES[@]}"; do
     only=${e%%:*}; tune=${e#*:}
     for L in $LIBS; do
-      if [ "$L" = base ]; then export PPO_HIP_LIB=ppo-dash_amd/lib/libppo_hip_base.so; else unset PPO_HIP_LIB; fi
+      if [ "$L" = cur ]; then unset PPO_HIP_LIB; else export PPO_HIP_LIB=ppo-dash_amd/lib/libppo_hip_$L.so; fi
       echo "--- B=$B lib=$L only=$only tune=$tune"
       timeout -k 10 120 python tools/kbench.py --B $B --reps 10 --only "$only" --tune "$tune"
       rc=$?; if [ $rc -ne 0 ]; then echo "!! rc=$rc"; exit $rc; fi
