@@ -2038,18 +2038,26 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
         PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       };
-      ld(0, 0);
+      // (the fp32-mask variant holds 28 more VGPRs of mask staging: no pipeline)
+      if constexpr (BITS) ld(0, 0);
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        ld(s, 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(s, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (s + 1 < KS) ld(s + 1, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(s, 1);
+        if constexpr (BITS) {
+          ld(s, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          mm(s, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (s + 1 < KS) ld(s + 1, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          mm(s, 1);
+        } else {
+          ld(s, 0);
+          mm(s, 0);
+          ld(s, 1);
+          mm(s, 1);
+        }
         if (s < MT && bprev >= 0 && !no_epi) store_tile(s, eacc[s], bprev);
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (BITS) __builtin_amdgcn_sched_barrier(0);
       }
     }
     // masked results of this image, stored during the next one's k-steps:
