@@ -239,6 +239,21 @@ __global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict
       b[gt][s] = v[0]; b[gt][s + 1] = v[1]; b[gt][s + 2] = v[2]; b[gt][s + 3] = v[3];
     }
   }
+  // the epilogue's operands (gi, bias, mask, h) are loaded here, in flight during
+  // the MFMAs, instead of a second dependent round trip after the K-quarter sum
+  float pg[2][3], pb[2][3], pm[2], ph[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int p = tid + 256 * e, m = min(m0 + (p >> 4), M - 1), j = j0 + (p & 15);
+    const float* gr = gi + (size_t)m * 3 * H;
+#pragma unroll
+    for (int gt = 0; gt < 3; ++gt) {
+      pg[e][gt] = gr[gt * H + j];
+      pb[e][gt] = bhh[gt * H + j];
+    }
+    pm[e] = masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
+    ph[e] = hprev[(size_t)m * H + j];
+  }
   f32x4 acc[2][3];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
@@ -267,13 +282,11 @@ __global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict
     for (int gt = 0; gt < 3; ++gt)
       v[gt] = ((P[0][rt * 3 + gt][ln][rg] + P[1][rt * 3 + gt][ln][rg]) + P[2][rt * 3 + gt][ln][rg]) +
               P[3][rt * 3 + gt][ln][rg];
-    const float* gr = gi + (size_t)m * 3 * H;
-    const float ghr = v[0] + bhh[j], ghz = v[1] + bhh[H + j], ghn = v[2] + bhh[2 * H + j];
-    const float r = sigm(gr[j] + ghr);
-    const float z = sigm(gr[H + j] + ghz);
-    const float n = tanhf(gr[2 * H + j] + r * ghn);
-    const float mk = masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
-    const float hin = hprev[(size_t)m * H + j] * mk;
+    const float ghr = v[0] + pb[e][0], ghz = v[1] + pb[e][1], ghn = v[2] + pb[e][2];
+    const float r = sigm(pg[e][0] + ghr);
+    const float z = sigm(pg[e][1] + ghz);
+    const float n = tanhf(pg[e][2] + r * ghn);
+    const float hin = ph[e] * pm[e];
     const size_t o = (size_t)m * H + j;
     hout[o] = (1.0f - z) * n + z * hin;
     if (sr) {
@@ -310,6 +323,19 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
   const int k0 = q * 4 * KW + g * KW;
+  // epilogue operands prefetched (in flight during the MFMAs)
+  float pd[2], pm[2], pc[2][6];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int p = tid + 256 * e, m = min(m0 + (p >> 4), M - 1), j = j0 + (p & 15);
+    const size_t o = (size_t)m * H + j;
+    pd[e] = dhz[o];
+    pm[e] = masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
+    if (cp.dout) {
+      pc[e][0] = cp.dout[o]; pc[e][1] = cp.r[o]; pc[e][2] = cp.z[o];
+      pc[e][3] = cp.n[o]; pc[e][4] = cp.ghn[o]; pc[e][5] = cp.hin[o];
+    }
+  }
   f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
   for (int half = 0; half < NH; ++half) {
@@ -346,12 +372,11 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
     if (m >= M) continue;
     const int rt = ml >> 4, ir = ml & 15, ln = jl + 16 * (ir >> 2), rg = ir & 3;
     const float v = ((P[0][rt][ln][rg] + P[1][rt][ln][rg]) + P[2][rt][ln][rg]) + P[3][rt][ln][rg];
-    const float mk = masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
     const size_t o = (size_t)m * H + j;
-    const float cv = (v + dhz[o]) * mk;
+    const float cv = (v + pd[e]) * pm[e];
     carry[o] = cv;
     if (cp.dout)   // the previous step's cell backward for this element (gru_cell_bwd_kernel, fused)
-      gru_cell_bwd_elem(cp.dout[o] + cv, cp.r[o], cp.z[o], cp.n[o], cp.ghn[o], cp.hin[o], o,
+      gru_cell_bwd_elem(pc[e][0] + cv, pc[e][1], pc[e][2], pc[e][3], pc[e][4], pc[e][5], o,
                         (size_t)m * 3 * H + j, H, cp.dgi, cp.dgh, const_cast<float*>(dhz));
   }
 }
