@@ -143,6 +143,8 @@ def parse():
                    help="kernels event-timed inside the timed region; the one with the most time is the roofline kernel")
     p.add_argument("--no-profile-pass", action="store_true",
                    help="skip the profiled iteration after the timed region (per-kernel breakdown)")
+    p.add_argument("--gru-persist", type=int, default=1, choices=(0, 1),
+                   help="recurrent: whole-sequence GRU forward as one persistent launch (1) or per-step launches (0)")
     p.add_argument("--products", type=int, default=6, choices=(6, 9),
                    help="part products per fp32 product in the split-bf16 GEMMs (9 = every product exact)")
     p.add_argument("--half-precision", action="store_true",
@@ -521,6 +523,7 @@ def main():
     from a2c_ppo_acktr.synthetic import SyntheticVecEnv
 
     _hip.call("ppo_tune_set", b"products", args.products)
+    _hip.call("ppo_gru_persist_set", args.gru_persist)
     N, T, E, M = args.envs, args.num_steps, args.ppo_epoch, args.num_mini_batch
     H = args.hidden or (256 if args.recurrent else 512)
     V = args.vec_len if args.recurrent else 0

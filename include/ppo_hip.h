@@ -216,6 +216,15 @@ int ppo_gru_variant_get(void);
 int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* idx, const float* whh, const float* bhh,
                     const float* gi, int T, int n, int H, float* hout, float* save_r, float* save_z, float* save_n,
                     float* save_ghn, float* save_hin, void* stream);
+/* ppo_gru_seq_fwd runs as ONE persistent launch when ceil(n/32)·H/16 blocks fit
+ * one per CU (H in {64,128,256,512}, variant 0): row groups synchronise through
+ * agent-scope release/acquire counters, bounded waits; bit-identical to the
+ * step launches.  persist 0 forces the step launches. */
+int ppo_gru_persist_set(int v);
+int ppo_gru_persist_get(void);
+/* 1 if a persistent launch's bounded wait timed out since the last call (its
+ * results are invalid); synchronises the device and clears the flag */
+int ppo_gru_persist_timeouts(void);
 int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float* save_z, const float* save_n,
                     const float* save_ghn, const float* save_hin, const float* masks, const int64_t* idx,
                     const float* whhT, int T, int n, int H, float* dgi, float* dgh, float* dhz, float* carry,

@@ -161,6 +161,9 @@ class PPO():
         _dist.allreduce_losses(self._loss_acc)
         num_updates = self.ppo_epoch * self.num_mini_batch        # ppo.py:90 (not the drop_last count)
         acc = self._loss_acc.tolist()                              # one D2H per update
+        if self.actor_critic.is_recurrent and call("ppo_gru_persist_timeouts"):
+            # a persistent GRU sequence kernel gave up a bounded wait: its outputs are invalid
+            raise RuntimeError("PPO.update: persistent GRU kernel timed out (ppo_gru_persist_set(0) disables it)")
         if acc[3] > 0:
             # the reference's log_probs gather (distributions.py:22) raises on such an index
             raise IndexError("PPO.update: {:.0f} stored action(s) outside [0, {}) in the rollout".format(

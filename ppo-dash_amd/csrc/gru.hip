@@ -202,22 +202,23 @@ using CfgGruB = Cfg<64, 64, 2, 2, true, true>;
 // MFMA maps (16x16x4 f32): A[l&15][k=l>>4], B[k=l>>4][l&15], D col=l&15, row=4(l>>4)+r.
 
 // forward: gh = h_in · W_hhᵀ for the (r, z, n) rows of the block's 16 units, then
-// the GRU cell (as GruStep::store_tile)
-template <int H>
-__global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict__ hprev,
-                                                         const float* __restrict__ masks,
-                                                         const int64_t* __restrict__ mask_idx,
-                                                         const float* __restrict__ whh, const float* __restrict__ bhh,
-                                                         const float* __restrict__ gi, int M, float* __restrict__ hout,
-                                                         float* __restrict__ sr, float* __restrict__ sz,
-                                                         float* __restrict__ sn, float* __restrict__ sghn,
-                                                         float* __restrict__ shin) {
+// the GRU cell (as GruStep::store_tile).  The block's W_hh slice (b) is loaded by
+// the caller: once per launch (step kernel) or once per sequence (persistent).
+// PUB (persistent kernel): h is handed between blocks inside the launch — its
+// stores are write-through (sc1) and every load of h is an sc1 load (the R1 form
+// of cdna_hip_programming.md §6 G16: no release / acquire fence needed)
+template <int H, bool PUB = false>
+__device__ __forceinline__ void gru_fwd_tile(int m0, int j0, const float* __restrict__ hprev,
+                                             const float* __restrict__ masks, const int64_t* __restrict__ mask_idx,
+                                             const float (&b)[3][H / 16], const float* __restrict__ bhh,
+                                             const float* __restrict__ gi, int M, float* __restrict__ hout,
+                                             float* __restrict__ sr, float* __restrict__ sz, float* __restrict__ sn,
+                                             float* __restrict__ sghn, float* __restrict__ shin,
+                                             f32x4 (&P)[4][6][64]) {
   constexpr int KW = H / 16;   // k per lane group and wave (4 groups x 4 waves x KW = H)
-  __shared__ f32x4 P[4][6][64];
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
-  const int m0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
   const int k0 = q * 4 * KW + g * KW;
-  float a[2][KW], b[3][KW];
+  float a[2][KW];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     const int m = m0 + 16 * rt + c;
@@ -226,17 +227,14 @@ __global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict
     const float* src = hprev + (size_t)(ok ? m : 0) * H + k0;
 #pragma unroll
     for (int s = 0; s < KW; s += 4) {
-      const f32x4 v = ok ? *reinterpret_cast<const f32x4*>(src + s) * mk : zero4();
+      f32x4 v;
+      if constexpr (PUB)
+        v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          make_rsrc(hprev, (uint32_t)M * H * 4), ((ok ? m : 0) * H + k0 + s) * 4, 0, 16));
+      else
+        v = *reinterpret_cast<const f32x4*>(src + s);
+      v = ok ? v * mk : zero4();
       a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
-    }
-  }
-#pragma unroll
-  for (int gt = 0; gt < 3; ++gt) {
-    const float* src = whh + ((size_t)gt * H + j0 + c) * H + k0;
-#pragma unroll
-    for (int s = 0; s < KW; s += 4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(src + s);
-      b[gt][s] = v[0]; b[gt][s + 1] = v[1]; b[gt][s + 2] = v[2]; b[gt][s + 3] = v[3];
     }
   }
   // the epilogue's operands (gi, bias, mask, h) are loaded here, in flight during
@@ -252,7 +250,11 @@ __global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict
       pb[e][gt] = bhh[gt * H + j];
     }
     pm[e] = masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
-    ph[e] = hprev[(size_t)m * H + j];
+    if constexpr (PUB)
+      ph[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(hprev, (uint32_t)M * H * 4),
+                                                                             (m * H + j) * 4, 0, 16));
+    else
+      ph[e] = hprev[(size_t)m * H + j];
   }
   f32x4 acc[2][3];
 #pragma unroll
@@ -288,13 +290,101 @@ __global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict
     const float n = tanhf(pg[e][2] + r * ghn);
     const float hin = ph[e] * pm[e];
     const size_t o = (size_t)m * H + j;
-    hout[o] = (1.0f - z) * n + z * hin;
+    const float hv = __fmaf_rn(z, hin, (1.0f - z) * n);   // explicit: same rounding in every instantiation
+    if constexpr (PUB)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, hv), make_rsrc(hout, (uint32_t)M * H * 4),
+                                            (int)o * 4, 0, 16);
+    else
+      hout[o] = hv;
     if (sr) {
       sr[o] = r;
       sz[o] = z;
       sn[o] = n;
       sghn[o] = ghn;
       shin[o] = hin;
+    }
+  }
+}
+
+template <int H>
+__device__ __forceinline__ void gru_load_whh(const float* __restrict__ whh, int j0, float (&b)[3][H / 16]) {
+  constexpr int KW = H / 16;
+  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
+  const int k0 = q * 4 * KW + g * KW;
+#pragma unroll
+  for (int gt = 0; gt < 3; ++gt) {
+    const float* src = whh + ((size_t)gt * H + j0 + c) * H + k0;
+#pragma unroll
+    for (int s = 0; s < KW; s += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + s);
+      b[gt][s] = v[0]; b[gt][s + 1] = v[1]; b[gt][s + 2] = v[2]; b[gt][s + 3] = v[3];
+    }
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict__ hprev,
+                                                         const float* __restrict__ masks,
+                                                         const int64_t* __restrict__ mask_idx,
+                                                         const float* __restrict__ whh, const float* __restrict__ bhh,
+                                                         const float* __restrict__ gi, int M, float* __restrict__ hout,
+                                                         float* __restrict__ sr, float* __restrict__ sz,
+                                                         float* __restrict__ sn, float* __restrict__ sghn,
+                                                         float* __restrict__ shin) {
+  __shared__ f32x4 P[4][6][64];
+  float b[3][H / 16];
+  gru_load_whh<H>(whh, blockIdx.y * 16, b);
+  gru_fwd_tile<H>(blockIdx.x * 32, blockIdx.y * 16, hprev, masks, mask_idx, b, bhh, gi, M, hout, sr, sz, sn, sghn,
+                  shin, P);
+}
+
+// Persistent whole-sequence forward: the step kernel's blocks stay resident for
+// all T steps, each with its W_hh slice in registers (loaded once).  Step t of row
+// group x needs h(t-1) of its 32 rows from all H/16 unit blocks of the group, so
+// the groups synchronise separately (no grid-wide barrier): a block publishes its
+// h(t) tile (write-through sc1 stores drained by every wave, then one relaxed
+// agent-scope counter increment of its group) and waits for the group's count
+// before step t + 1 (relaxed polls), reading h only with sc1 loads — the R1
+// hand-off of cdna_hip_programming.md §6 G16, correct wherever the blocks run.  The grid (<= one block per CU) is
+// resident by its size; every wait is bounded and a timeout sets *err.
+template <int H>
+__global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict__ h0, const float* __restrict__ masks,
+                                                        const int64_t* __restrict__ idx, const float* __restrict__ whh,
+                                                        const float* __restrict__ bhh, const float* __restrict__ gi,
+                                                        int T, int n, float* __restrict__ hout, float* __restrict__ sr,
+                                                        float* __restrict__ sz, float* __restrict__ sn,
+                                                        float* __restrict__ sghn, float* __restrict__ shin,
+                                                        int* __restrict__ cnt, int* __restrict__ err) {
+  __shared__ f32x4 P[4][6][64];
+  const int j0 = blockIdx.y * 16, m0 = blockIdx.x * 32, grp = blockIdx.x, need = H / 16;
+  float b[3][H / 16];
+  gru_load_whh<H>(whh, j0, b);
+  const bool sv = sr != nullptr;
+  for (int t = 0; t < T; ++t) {
+    const size_t o = (size_t)t * n * H;
+    if (t > 0) {   // h(t-1) of the group's rows complete (all its unit blocks published)
+      if (threadIdx.x == 0) {
+        const int target = need * t;
+        int it = 0;
+        while (__hip_atomic_load(cnt + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          if (++it > (1 << 21)) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: h loads stay below the poll
+      __syncthreads();
+    }
+    const float* mk = masks && !idx ? masks + (size_t)t * n : masks;
+    gru_fwd_tile<H, true>(m0, j0, t == 0 ? h0 : hout + o - (size_t)n * H, mk, idx ? idx + (size_t)t * n : nullptr, b, bhh,
+                    gi + 3 * o, n, hout + o, sv ? sr + o : nullptr, sv ? sz + o : nullptr, sv ? sn + o : nullptr,
+                    sv ? sghn + o : nullptr, sv ? shin + o : nullptr, P);
+    if (t + 1 < T) {   // publish h(t) of this tile
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its sc1 h stores done
+      __syncthreads();   // also: every wave has read P before the next step rewrites it
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -383,6 +473,52 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
 
 // 0: register-tiled step kernels where H allows; 1: the tile-GEMM steps (A/B)
 static int g_gru_variant = 0;
+// whole-sequence forward as one persistent launch (gru_seq16_kernel) where its
+// grid fits one block per CU; 0: one step kernel per step
+static int g_gru_persist = 1;
+
+// group counters + timeout word of the persistent kernels (one stream at a time)
+static int* persist_words(int groups) {
+  static int* buf = nullptr;
+  static int cap = 0;
+  if (groups + 1 > cap) {
+    if (buf) (void)hipFree(buf);
+    cap = groups + 1 > 4096 ? groups + 1 : 4096;
+    if (hipMalloc(&buf, (size_t)cap * sizeof(int)) != hipSuccess) {
+      buf = nullptr;
+      cap = 0;
+      return nullptr;
+    }
+    if (hipMemset(buf, 0, (size_t)cap * sizeof(int)) != hipSuccess) return nullptr;
+  }
+  return buf;
+}
+
+static int gru_cus() {
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    n_cu = v;
+  }
+  return n_cu;
+}
+
+template <int H>
+int launch_seq16(const float* h0, const float* masks, const int64_t* idx, const float* whh, const float* bhh,
+                 const float* gi, int T, int n, float* hout, float* sr, float* sz, float* sn, float* sghn,
+                 float* shin, hipStream_t st) {
+  const int groups = ceil_div(n, 32);
+  int* w = persist_words(groups);
+  PPO_REQUIRE(w != nullptr, "ppo_gru_seq_fwd: counter allocation failed");
+  PPO_HIP_CHECK(hipMemsetAsync(w + 1, 0, (size_t)groups * sizeof(int), st), "ppo_gru_seq_fwd: counter reset");
+  dim3 grid((unsigned)groups, H / 16);
+  gru_seq16_kernel<H><<<grid, 256, 0, st>>>(h0, masks, idx, whh, bhh, gi, T, n, hout, sr, sz, sn, sghn, shin, w + 1, w);
+  PPO_LAUNCH_CHECK("gru_seq16_kernel");
+  return 0;
+}
 
 template <int H>
 int launch_step16(const float* hprev, const float* masks, const int64_t* mask_idx, const float* whh,
@@ -495,6 +631,15 @@ PPO_API int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* 
                             float* save_z, float* save_n, float* save_ghn, float* save_hin, void* stream) {
   PPO_REQUIRE(T >= 0 && n >= 0 && H > 0 && H % 32 == 0, "ppo_gru_seq_fwd: T=%d n=%d H=%d", T, n, H);
   ProfScope prof("gru_seq_fwd", as_stream(stream), 2.0 * T * n * 3.0 * H * H);
+  if (T > 0 && n > 0 && g_gru_variant == 0 && g_gru_persist && (long long)ceil_div(n, 32) * (H / 16) <= gru_cus()) {
+    hipStream_t st = as_stream(stream);
+    switch (H) {
+      case 64: return launch_seq16<64>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, st);
+      case 128: return launch_seq16<128>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, st);
+      case 256: return launch_seq16<256>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, st);
+      case 512: return launch_seq16<512>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, st);
+    }
+  }
   const bool sv = save_r != nullptr;
   for (int t = 0; t < T; ++t) {
     const size_t o = (size_t)t * n * H;
@@ -533,6 +678,26 @@ PPO_API int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float*
     if (rc) return rc;
   }
   return 0;
+}
+
+// persistent whole-sequence kernels on (1) / off (0)
+PPO_API int ppo_gru_persist_set(int v) {
+  PPO_REQUIRE(v == 0 || v == 1, "ppo_gru_persist_set: %d", v);
+  g_gru_persist = v;
+  return 0;
+}
+PPO_API int ppo_gru_persist_get(void) { return g_gru_persist; }
+
+// 1 if a persistent kernel's bounded wait has timed out since the last call
+// (results of that launch are invalid); synchronises the device; clears the word
+PPO_API int ppo_gru_persist_timeouts(void) {
+  int* w = persist_words(0);
+  PPO_REQUIRE(w != nullptr, "ppo_gru_persist_timeouts: no counter buffer");
+  int v = 0;
+  PPO_HIP_CHECK(hipDeviceSynchronize(), "ppo_gru_persist_timeouts");
+  PPO_HIP_CHECK(hipMemcpy(&v, w, sizeof(int), hipMemcpyDeviceToHost), "ppo_gru_persist_timeouts");
+  if (v) PPO_HIP_CHECK(hipMemset(w, 0, sizeof(int)), "ppo_gru_persist_timeouts");
+  return v;
 }
 
 // A/B switch for the step kernels (0 register-tiled, 1 tile GEMM)

@@ -1250,6 +1250,45 @@ def test_gru_step_kernels_vs_float64(gpu, M, H):
             assert err <= 2e-5 * max(v.abs().max().item(), 1.0), (variant, k, err)
 
 
+@pytest.mark.parametrize("T,n,H,use_idx", [(24, 512, 256, True), (9, 37, 64, False), (5, 100, 128, True),
+                                            (3, 16, 512, False)])
+def test_gru_persistent_sequence_equals_steps(gpu, T, n, H, use_idx):
+    """ppo_gru_seq_fwd as one persistent launch (row groups synchronised by
+    release/acquire counters, W_hh slices resident) equals the step-by-step
+    launches bit for bit — hout and every saved gate over all T steps — with masks
+    direct ([T][n]) or through the minibatch index, and no bounded wait timed out."""
+    Hh = _hip()
+    g = torch.Generator().manual_seed(T * n + H)
+    N = 3 * n
+    h0 = torch.randn(n, H, generator=g).cuda()
+    whh = (torch.randn(3 * H, H, generator=g) / H ** 0.5).cuda()
+    bhh = (torch.randn(3 * H, generator=g) * 0.1).cuda()
+    gi = torch.randn(T * n, 3 * H, generator=g).cuda()
+    if use_idx:
+        masks = (torch.rand(T * N, generator=g) > 0.1).float().cuda()
+        idx = torch.randint(0, T * N, (T * n,), generator=g).cuda()
+    else:
+        masks = (torch.rand(T * n, generator=g) > 0.1).float().cuda()
+        idx = None
+    outs = {}
+    for persist in (0, 1):
+        o = {k: torch.full((T * n, H), float("nan"), device=gpu) for k in ("h", "r", "z", "n", "ghn", "hin")}
+        Hh.call("ppo_gru_persist_set", persist)
+        try:
+            Hh.call("ppo_gru_seq_fwd", h0.data_ptr(), masks.data_ptr(), None if idx is None else idx.data_ptr(),
+                    whh.data_ptr(), bhh.data_ptr(), gi.data_ptr(), T, n, H, o["h"].data_ptr(), o["r"].data_ptr(),
+                    o["z"].data_ptr(), o["n"].data_ptr(), o["ghn"].data_ptr(), o["hin"].data_ptr(), _s())
+            torch.cuda.synchronize()
+        finally:
+            Hh.call("ppo_gru_persist_set", 1)
+        outs[persist] = o
+    assert Hh.call("ppo_gru_persist_timeouts") == 0
+    for k in outs[0]:
+        assert torch.isfinite(outs[1][k]).all(), k
+        assert torch.equal(outs[0][k], outs[1][k]), (k, (outs[0][k] - outs[1][k]).abs().max().item(),
+                                                      (outs[0][k] != outs[1][k]).sum().item())
+
+
 @pytest.mark.parametrize("variant", [1, 3, 9])
 def test_conv1_wgrad_variants_vs_torch(gpu, variant):
     """conv1 weight + bias gradient from u8 observations gathered by index (the
