@@ -342,7 +342,7 @@ def pmc_traffic(kernel, workload):
 
 
 # bench kernel name -> the kernel symbol in the rocprofv3 PMC summaries
-PMC_SYMBOL = {"conv2_fwd": "conv2_fwd_x9_kernel<", "conv2_dgrad": "conv2_dgrad_x9_kernel<",
+PMC_SYMBOL = {"conv2_fwd": "conv2_fwd_x9c_kernel<", "conv2_dgrad": "conv2_dgrad_x9_kernel<",
               "conv2_wgrad": "conv2_wgrad_x9_kernel<", "conv3_fwd": "conv3_fwd_x9_kernel<",
               "conv3_dgrad": "conv3_dgrad_x9_kernel<", "conv3_wgrad": "conv3_wgrad_x9_kernel<",
               "conv1_wgrad_u8": "conv1_wgrad_parts_kernel<", "conv1_fwd_u8": "conv1_fwd_bf16x3_kernel<"}

@@ -278,11 +278,13 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
   }
 }
 
-// conv1 weight gradient, part-pipelined (ppo_tune_set("conv1_wgrad", 3)): the
-// GEMM of conv1_wgrad_bf16x3_kernel (dW[co][(c,ky,kx)] = Σ_px dz1[px][co] ·
-// u[c][4oy+ky][4ox+kx], u8 pixels exact in bf16, dz = hi + mid + lo exactly:
-// three v_mfma_f32_32x32x16_bf16 per block pair), restaged so that the staging
-// overlaps the MFMAs:
+// conv1 weight gradient on the bf16 matrix cores, exact, part-pipelined
+// (ppo_tune_set("conv1_wgrad", 3), default): dW[co][(c,ky,kx)] = Σ_px dz1[px][co] ·
+// u[c][4oy+ky][4ox+kx]; the u8 pixels are exact in bf16 and dz = hi + mid + lo
+// exactly, so three v_mfma_f32_32x32x16_bf16 per block pair give exact products
+// with fp32 accumulation.  Staged so that the staging overlaps
+// the MFMAs (a whole-image-stage kernel that filled the LDS measured 2.03-2.10
+// ms per minibatch against 1.92-2.01 for this one and was removed):
 //   * an image is processed in 5 parts of 4 output rows (80 pixels = 5 k-steps);
 //     a part's operands are 42,496 B of LDS — two stages (85 KB) instead of one
 //     whole-image stage that fills the LDS;
@@ -493,194 +495,6 @@ __global__ __launch_bounds__(256) void relu_bits_kernel(const float* __restrict_
   }
 }
 
-// conv1 weight gradient on the bf16 matrix cores, exact (u8 observations,
-// C = 4): dW[co][(c,ky,kx)] = Σ_pixels dz1[px][co] · u[c][4oy+ky][4ox+kx].  The
-// pixel is exact in bf16 and dz = dz_hi + dz_mid + dz_lo exactly, so three
-// v_mfma_f32_32x32x16_bf16 per block pair give exact products with fp32
-// accumulation.  A block (8 waves, 2 per SIMD) walks its images;
-// per image the LDS holds
-//   E  [c][y][kx][ox]  bf16  the image "kx-expanded" (E = u[c][y][4ox+kx]), so
-//                           the 4 pixels of an output-row quad are 4 adjacent
-//                           elements for every (c, ky, kx); the 8 kx rows of
-//                           one (c, y) take 81 dwords (odd: the staging stores
-//                           of 32 lanes hit 32 banks)                   108,864 B
-//   dzT[co][416]       f32   dz1 transposed; the 16-B chunk k of row co sits at
-//                           chunk k ^ SW(co) (a searched 3-bit table): the staging
-//                           ds_write_b128 of 8 lanes (rows 4cq + q) and the fragment
-//                           ds_read_b128 of each 16-lane group both conflict-free 53,248 B
-// and the next image is in flight into registers.  The reduction runs over
-// pixels in natural order: k-step s covers pixels 16s .. 16s+15, lane half h the
-// 8 pixels 16s + 8h .. +7 (two output-row quads 4Q .. 4Q+3).  Wave w: n tiles
-// 4 (w & 1) .. +3 (128 of the 256 (c,ky,kx) columns), k-steps s ≡ (w >> 1) mod 4;
-// the k-groups' partial sums are combined in a fixed order at the end.
-// Output: the usual split-K slab [Z][32][256] (u8 integers: the reduce applies
-// 1/255) and bias partials [Z][32].
-template <int C, int NPD = 3>   // NPD: dz parts summed (3 exact; 1 half-precision mode)
-__global__ __launch_bounds__(512) void conv1_wgrad_bf16x3_kernel(const float* __restrict__ dz1,
-                                                                 const uint8_t* __restrict__ obs,
-                                                                 const int64_t* __restrict__ idx, long long row0,
-                                                                 int B, float* __restrict__ slab,
-                                                                 float* __restrict__ slab_bias, int dbg) {
-  static_assert(C == 4, "LDS budget sized for 4 input channels");
-  // timing anatomy only (kbench --tune stagger=16*dbg; wrong results): dbg 1 skips
-  // the MFMAs, 2 the staging (put), 4 the dz split, 8 the B-fragment reads
-  const bool no_mma = dbg & 1, no_put = dbg & 2, no_split = dbg & 4, no_rd = dbg & 8;
-  constexpr int EROW = 162, NE = C * IMG * EROW, DZL = 416, NPX = 400, KS = 25, NT = 512;
-  // float offset of pixel px (multiple of 4) in dzT row co: chunk px/4 XOR SW(co)
-  auto dzo = [](int co, int px) {
-    constexpr unsigned long long SWLO = 0x312423067232146ull, SWHI = 0x1601706435575475ull;
-    const int sw = (int)(((co < 16 ? SWLO >> (4 * co) : SWHI >> (4 * (co - 16)))) & 7);
-    return co * DZL + 4 * ((px >> 2) ^ sw);
-  };
-  __shared__ __attribute__((aligned(16))) uint16_t E[NE];
-  __shared__ __attribute__((aligned(16))) float dzT[32 * DZL];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ng = __builtin_amdgcn_readfirstlane(wave & 1), kg = __builtin_amdgcn_readfirstlane(wave >> 1);
-  const int l32 = lane & 31, h = lane >> 5;
-  int ecol[4];   // lane's B column n = 128 ng + 32 t + l32 -> (c, ky, kx)
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int n = 128 * ng + 32 * t + l32, c = n >> 6, ky = (n >> 3) & 7, kx = n & 7;
-    ecol[t] = (c * IMG + ky) * EROW + kx * 20;   // + 4 oy * EROW + ox0 per quad
-  }
-  f32x16 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  // dz staging runs from the top thread down (u = NT - 1 - tid + NT i): the waves
-  // that expand the image (tid < 336) get the fewer dz units
-  const int rt = NT - 1 - tid;
-  const int cq = rt & 7;                  // dz staging: channel quad of this thread
-  float bsum[4] = {0.f, 0.f, 0.f, 0.f};   // bias partial of channels 4 cq .. +3
-
-  f32x4 dzr[2][4];        // up to 2 units of 4 pixels x 4 channels
-  uint32_t imr[21];       // one image row (84 bytes)
-  auto fetch = [&](int b) {
-    const float* dzb = dz1 + (size_t)b * NPX * 32;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int u = rt + NT * i;
-      if (u < 800) {
-        const int p4 = u >> 3;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dzr[i][r] = *reinterpret_cast<const f32x4*>(dzb + (4 * p4 + r) * 32 + 4 * cq);
-      }
-    }
-    if (tid < C * IMG) {
-      const uint32_t* row =
-          reinterpret_cast<const uint32_t*>(obs + obs_row(idx, row0, b) * (long long)(C * IMG2) + tid * IMG);
-#pragma unroll
-      for (int j = 0; j < 21; ++j) imr[j] = row[j];
-    }
-  };
-  auto put = [&]() {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int u = rt + NT * i;
-      if (u < 800) {
-        const int p4 = u >> 3;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x4 v = f32x4{dzr[i][0][q], dzr[i][1][q], dzr[i][2][q], dzr[i][3][q]};
-          *reinterpret_cast<f32x4*>(dzT + dzo(4 * cq + q, 4 * p4)) = v;
-          bsum[q] += (v[0] + v[1]) + (v[2] + v[3]);
-        }
-      }
-    }
-    if (tid < C * IMG) {
-#pragma unroll
-      for (int kx = 0; kx < 8; ++kx) {   // E[cy][kx][ox] = byte (kx & 3) of dword ox + (kx >> 2)
-        const int kh = kx >> 2, kk = kx & 3;
-        uint32_t* dst = reinterpret_cast<uint32_t*>(E + tid * EROW + kx * 20);
-#pragma unroll
-        for (int q = 0; q < 10; ++q) {
-          const uint32_t w0 = imr[2 * q + kh], w1 = imr[2 * q + 1 + kh];
-          const float f0 = (float)((w0 >> (8 * kk)) & 255u), f1 = (float)((w1 >> (8 * kk)) & 255u);
-          dst[q] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
-        }
-      }
-    }
-  };
-  auto rd = [&](int st, f32x4& x0, f32x4& x1, bf16x8 (&bb)[4]) {
-    const int px = 16 * st + 8 * h;   // this lane half's 8 pixels: quads px/4, px/4 + 1
-    x0 = *reinterpret_cast<const f32x4*>(dzT + dzo(l32, px));
-    x1 = *reinterpret_cast<const f32x4*>(dzT + dzo(l32, px + 4));
-    const int q1 = px >> 2, q2 = q1 + 1;
-    const int e1 = (q1 / 5) * (4 * EROW) + 4 * (q1 % 5), e2 = (q2 / 5) * (4 * EROW) + 4 * (q2 % 5);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {   // 40-B kx rows: quads only 4-byte aligned -> dword reads
-      const uint32_t* p1 = reinterpret_cast<const uint32_t*>(E + ecol[t] + e1);
-      const uint32_t* p2 = reinterpret_cast<const uint32_t*>(E + ecol[t] + e2);
-      bb[t] = __builtin_bit_cast(bf16x8, uint4{p1[0], p1[1], p2[0], p2[1]});
-    }
-  };
-
-  int b = blockIdx.x;
-  if (b < B) fetch(b);
-  for (; b < B; b += gridDim.x) {
-    if (!no_put) put();
-    __syncthreads();
-    if (b + (int)gridDim.x < B) fetch(b + gridDim.x);
-    // k-steps kg, kg + 4, ...: the fragments of step s + 4 are read while the
-    // 12 MFMAs of step s run
-    f32x4 xa0, xa1;
-    bf16x8 bq[4];
-    if (kg < KS) rd(kg, xa0, xa1, bq);
-    for (int st = kg; st < KS; st += 4) {
-      Frag3 fa;
-      split8(xa0, xa1, fa, no_split);
-      if (no_split) fa.m = fa.l = fa.h;
-      bf16x8 bc[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) bc[t] = bq[t];
-      if (st + 4 < KS && !no_rd) rd(st + 4, xa0, xa1, bq);
-#pragma unroll
-      for (int t = 0; t < 4 && !no_mma; ++t) {
-        if constexpr (NPD == 3) {
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.l, bc[t], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.m, bc[t], acc[t], 0, 0, 0);
-        }
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.h, bc[t], acc[t], 0, 0, 0);
-      }
-    }
-    __syncthreads();   // before the next image overwrites E / dzT
-  }
-  // ---- combine the four k-groups (fixed order), write the slab ----
-  float* red = reinterpret_cast<float*>(E);   // [k-group 1..3][ng][t][r][lane]: 98,304 B <= 108,864
-  if (kg > 0) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) red[((((kg - 1) * 2 + ng) * 4 + t) * 16 + r) * 64 + lane] = acc[t][r];
-  }
-  __syncthreads();
-  float* out = slab + (size_t)blockIdx.x * 32 * 256;
-  if (kg == 0) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = acc[t][r];
-#pragma unroll
-        for (int g = 0; g < 3; ++g) v += red[(((g * 2 + ng) * 4 + t) * 16 + r) * 64 + lane];
-        const int co = (r & 3) + 8 * (r >> 2) + 4 * h, n = 128 * ng + 32 * t + l32;
-        out[co * 256 + n] = v;
-      }
-  }
-  __syncthreads();
-  float* bred = dzT;   // [512 threads][4]
-#pragma unroll
-  for (int q = 0; q < 4; ++q) bred[tid * 4 + q] = bsum[q];
-  __syncthreads();
-  if (tid < 32) {   // channel tid: the 64 threads of its quad, fixed order
-    const int q = tid & 3, c8 = tid >> 2;
-    float t = 0.f;
-    for (int j = 7 - c8; j < NT; j += 8) t += bred[j * 4 + q];   // threads with cq = c8
-    slab_bias[(size_t)blockIdx.x * 32 + tid] = t;
-  }
-}
-
 // NHWC conv (conv2, conv3): k = (ky, kx, ci), weights packed [COUT][K]
 template <int HIN, int CIN, int KS, int ST, int HOUT, int COUT, class C_>
 struct ConvFwd : C_ {
@@ -783,152 +597,15 @@ struct Conv2Dgrad : C_ {
 };
 
 // conv2 forward, image-resident on the bf16 matrix cores (exact split, DESIGN.md
-// §3): a2[b][m][co] = relu(b2[co] + Σ_k im2col(a1)[m][k] W2p[co][k]), m = (oy, ox)
-// (81 rows in 6 tiles of 16), k = (ky, kx, ci).  One persistent block (8 waves)
-// per CU walks images; the image sits in LDS split into three bf16 planes, the
-// next one in flight into registers (stored between the compute phases).
-//   LDS layout: 16-B units (8 ci) of pixel (y, x) at unit index
-//     c * CS + (y & 1) * 250 + (y >> 1) * 25 + (x & 1) * 10 + (x >> 1)
-//   (c = ci >> 3, CS = 544): with y and x parities split out, the pixel a row
-//   m = 9 oy + ox reads for tap (ky, kx) is oy * 25 + ox + const ≡ m + const
-//   (mod 16), so the 16 rows of a tile hit 16 distinct 16-B slots whatever their
-//   ci chunk — ds_read_b128 without bank conflicts.
-//   Wave w: n tile w & 3 (16 co), taps 8 (w >> 2) .. +7 (ky rows 0-1 / 2-3);
-//   its weight fragments (pre-split planes) in 96 VGPRs.  The two K halves are
-//   summed through LDS (half 1 writes, half 0 adds and stores).
-template <int NP, bool MASK = false>   // MASK: also write the ReLU mask bits (training forward)
-__global__ __launch_bounds__(512) void conv2_fwd_x9_kernel(const float* __restrict__ a1, int B,
-                                                          const uint16_t* __restrict__ wpl,
-                                                          const float* __restrict__ bias,
-                                                          float* __restrict__ out,
-                                                          uint16_t* __restrict__ mbits) {
-  constexpr int CS = 544, PLU = 4 * CS, MT = 6, KS = 8, UNITS = 400 * 4, UPER = (UNITS + 511) / 512;
-  constexpr int WN = 64 * 512;
-  __shared__ __attribute__((aligned(16))) uint16_t S[3 * PLU * 8];   // 3 planes x 4 chunks x CS units x 8 bf16
-  __shared__ __attribute__((aligned(16))) f32x4 R[4][MT][64];        // K-half-1 partial sums
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
-  const int nt = wave & 3, kh = wave >> 2, co = 16 * nt + i16;
-  bf16x8 bw[KS][3];
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
-  // epilogue in the swapped orientation (weights as the MFMA A operand): lane
-  // (i16, g) holds pixel 16 t + i16, channels 16 nt + 4g .. +3 — one 16-B store
-  const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
-  wait_vm0();
-  // unit index of this lane's A fragment per row tile, tap (0, 0); a tap adds toff
-  int qrow[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) {
-    const int m = 16 * t + i16, oy = m / 9, ox = m - 9 * oy;
-    qrow[t] = g * CS + oy * 25 + ox;
-  }
-  // staging: unit u -> chunk (u >> 3) & 3 of the pixel at LDS-order position
-  // rho = 8 (u >> 5) + (u & 7), rho = 20 y + 10 (x & 1) + (x >> 1): the 8 lanes of a
-  // ds_write_b128 pass store 8 consecutive units (no bank conflicts), and the 4
-  // chunks of a pixel are read by one load instruction (whole 128-B lines)
-  int upx[UPER], uq[UPER];
-#pragma unroll
-  for (int j = 0; j < UPER; ++j) {
-    const int u = tid + 512 * j, rho = 8 * (u >> 5) + (u & 7), c = (u >> 3) & 3;
-    const int y = rho / 20, r = rho - 20 * y, x = r < 10 ? 2 * r : 2 * (r - 10) + 1;
-    upx[j] = (y * 20 + x) * 4 + c;
-    uq[j] = c * CS + (y & 1) * 250 + (y >> 1) * 25 + r;
-  }
-  float4 stg[UPER][2];
-  auto fetch = [&](int b) {
-    const float4* src = reinterpret_cast<const float4*>(a1 + (size_t)b * 12800);
-#pragma unroll
-    for (int j = 0; j < UPER; ++j) {
-      const int u = tid + 512 * j;
-      if (u < UNITS) { stg[j][0] = src[2 * upx[j]]; stg[j][1] = src[2 * upx[j] + 1]; }
-    }
-  };
-  auto put = [&]() {
-#pragma unroll
-    for (int j = 0; j < UPER; ++j) {
-      const int u = tid + 512 * j;
-      if (u < UNITS) {
-        const int q = uq[j];
-        Frag3 f;
-        split8(f32x4{stg[j][0].x, stg[j][0].y, stg[j][0].z, stg[j][0].w},
-               f32x4{stg[j][1].x, stg[j][1].y, stg[j][1].z, stg[j][1].w}, f, false);
-        *reinterpret_cast<bf16x8*>(&S[8 * q]) = f.h;
-        *reinterpret_cast<bf16x8*>(&S[8 * (PLU + q)]) = f.m;
-        *reinterpret_cast<bf16x8*>(&S[8 * (2 * PLU + q)]) = f.l;
-      }
-    }
-  };
-  const int G = gridDim.x;
-  int b = blockIdx.x;
-  if (b < B) {
-    fetch(b);
-    put();
-    if (b + G < B) fetch(b + G);
-  }
-  __syncthreads();
-  for (; b < B; b += G) {
-    f32x4 acc[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t) acc[t] = zero4();
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int tap = 8 * kh + s, ky = tap >> 2, kx = tap & 3;
-      const int toff = (ky & 1) * 250 + (ky >> 1) * 25 + (kx & 1) * 10 + (kx >> 1);
-      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
-#pragma unroll
-      for (int t0 = 0; t0 < MT; t0 += 3) {
-        Frag3 a[3];
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          const uint16_t* q = S + 8 * (qrow[t0 + u] + toff);
-          a[u].h = *reinterpret_cast<const bf16x8*>(q);
-          a[u].m = *reinterpret_cast<const bf16x8*>(q + 8 * PLU);
-          a[u].l = *reinterpret_cast<const bf16x8*>(q + 16 * PLU);
-        }
-#define PPO_PART(X, Y) \
-  _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(w.Y, a[u].X, acc[t0 + u]);
-        PPO_PRODUCTS(NP, PPO_PART)
-#undef PPO_PART
-      }
-    }
-    __syncthreads();   // A: the image is consumed
-    if (kh == 1) {
-#pragma unroll
-      for (int t = 0; t < MT; ++t) R[nt][t][lane] = acc[t];
-    }
-    if (b + G < B) put();
-    if (b + 2 * G < B) fetch(b + 2 * G);
-    __syncthreads();   // B: partials and the next image are in LDS
-    if (kh == 0) {
-      const auto rs = make_rsrc(out + (size_t)b * (81 * 64), 81 * 64 * 4);
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const f32x4 v = acc[t] + R[nt][t][lane];
-        const int m = 16 * t + i16;
-        f32x4 y;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
-        bstore_f32x4(y, rs, m < 81 ? 4 * (m * 64 + 16 * nt + 4 * g) : -1);
-        if constexpr (MASK) {   // ReLU mask bits of pixel m, channels 16 nt .. +15: 4 lanes' nibbles
-          int nib = 0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) nib |= (y[r] > 0.f ? 1 : 0) << r;
-          const int w16 = nib | (__shfl_down(nib, 16, 64) << 4) | (__shfl_down(nib, 32, 64) << 8) |
-                          (__shfl_down(nib, 48, 64) << 12);
-          if (g == 0 && m < 81) mbits[((size_t)b * 81 + m) * 4 + nt] = (uint16_t)w16;
-        }
-      }
-    }
-  }
-}
-
-// conv2 forward with two LDS stages (ppo_tune_set("conv2_fwd", 12)): the waves,
-// K halves and arithmetic of conv2_fwd_x9_kernel (bit-identical outputs), with
-// the next image's split staged into the second stage *during* the current
-// image's k-steps instead of in a phase of its own.
+// §3), two LDS stages (ppo_tune_set("conv2_fwd", 12), default): a2[b][m][co] =
+// relu(b2[co] + Σ_k im2col(a1)[m][k] W2p[co][k]), m = (oy, ox), k = (ky, kx, ci).
+// One persistent block (8 waves) per CU walks images.  Wave w: n tile w & 3 (16
+// co), taps 8 (w >> 2) .. +7 (ky rows 0-1 / 2-3), its weight fragments
+// (pre-split planes) in registers; the two K halves are summed through LDS.  The
+// next image's split is staged into the second stage *during* the current
+// image's k-steps instead of in a phase of its own (the single-stage kernel this
+// replaced, 1.98 ms per minibatch, and an LDS-DMA staged variant, 2.00 ms, were
+// removed; this one is bit-identical to both).
 //   * Compact parity layout, 400 16-B units per 8-channel chunk: pixel (y, x) at
 //     P = 100 (2 (y & 1) + (x & 1)) + 10 (y >> 1) + (x >> 1), so tap (ky, kx) of
 //     output pixel (oy, ox) reads v + toff(ky, kx), v = 10 oy + ox.  Row i of row
@@ -1100,145 +777,6 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
       }
     }
     cur ^= 1;
-  }
-}
-
-// conv2 forward, LDS-DMA staged variant of conv2_fwd_x9_kernel (same layout,
-// same math, bit-identical results).  The register-staged kernel loses ~45 % of
-// its time in the per-image staging phase: the next image's global loads sit
-// at the VGPR cap (254) and the allocator's register shuffles wait on them
-// right after issue, so every image pays an HBM round trip with the MFMAs
-// idle.  Here the next image goes global -> LDS by global_load_lds_dwordx4
-// (no VGPRs; in flight during the whole compute phase) into a raw fp32 buffer
-// (51,200 B, lane-linear in source order), and the split reads it from LDS.
-// LDS (one array): S planes 104,448 B | RAW 51,200 B; the K-half partials
-// alias S once the image is consumed.  Per image: compute -> vmcnt(0) +
-// barrier -> partials -> barrier -> epilogue -> barrier -> split RAW into S ->
-// barrier -> issue the DMA of the image after next.
-// Measured (kbench, c3 minibatch): 2.00 ms vs 1.98 ms for the register-staged
-// kernel — neutral: what remains of the staging phase is the split VALU and
-// the barriers, which no staging path can overlap with the MFMAs while one
-// split image fills two thirds of the LDS.  Kept as ppo_tune_set("conv2_fwd", 10).
-template <int NP>
-__global__ __launch_bounds__(512) void conv2_fwd_dma_kernel(const float* __restrict__ a1, int B,
-                                                           const uint16_t* __restrict__ wpl,
-                                                           const float* __restrict__ bias,
-                                                           float* __restrict__ out) {
-  constexpr int CS = 544, PLU = 4 * CS, MT = 6, KS = 8, UNITS = 400 * 4, UPER = (UNITS + 511) / 512;
-  constexpr int WN = 64 * 512, SBYTES = 3 * PLU * 8 * 2, RAWU = 400 * 8;   // RAW: 3,200 16-B units
-  __shared__ __attribute__((aligned(16))) uint8_t L[SBYTES + RAWU * 16];
-  uint16_t* S = reinterpret_cast<uint16_t*>(L);
-  f32x4* RAW = reinterpret_cast<f32x4*>(L + SBYTES);
-  f32x4(*R)[MT][64] = reinterpret_cast<f32x4(*)[MT][64]>(L);   // [4][MT][64], aliases S
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
-  const int nt = wave & 3, kh = wave >> 2, co = 16 * nt + i16;
-  bf16x8 bw[KS][3];
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
-  const float bv = bias[co];
-  wait_vm0();
-  int qrow[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) {
-    const int m = 16 * t + i16, oy = m / 9, ox = m - 9 * oy;
-    qrow[t] = g * CS + oy * 25 + ox;
-  }
-  int upx[UPER], uq[UPER];
-#pragma unroll
-  for (int j = 0; j < UPER; ++j) {
-    const int u = tid + 512 * j, rho = 8 * (u >> 5) + (u & 7), c = (u >> 3) & 3;
-    const int y = rho / 20, r = rho - 20 * y, x = r < 10 ? 2 * r : 2 * (r - 10) + 1;
-    upx[j] = (y * 20 + x) * 4 + c;
-    uq[j] = c * CS + (y & 1) * 250 + (y >> 1) * 25 + r;
-  }
-  // DMA of image b into RAW: wave w's instruction i moves units (8 i + w) * 64 + lane
-  auto dma = [&](int b) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
-#pragma unroll
-    for (int i = 0; i < (RAWU + 511) / 512; ++i) {
-      const int base = (8 * i + wave) * 64;   // wave-uniform
-      if (base < RAWU)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + base + lane),
-                                         reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                             reinterpret_cast<uintptr_t>(RAW + base)),
-                                         16, 0, 0);
-    }
-  };
-  auto put = [&]() {
-#pragma unroll
-    for (int j = 0; j < UPER; ++j) {
-      const int u = tid + 512 * j;
-      if (u < UNITS) {
-        const int q = uq[j];
-        Frag3 f;
-        split8(RAW[2 * upx[j]], RAW[2 * upx[j] + 1], f, false);
-        *reinterpret_cast<bf16x8*>(&S[8 * q]) = f.h;
-        *reinterpret_cast<bf16x8*>(&S[8 * (PLU + q)]) = f.m;
-        *reinterpret_cast<bf16x8*>(&S[8 * (2 * PLU + q)]) = f.l;
-      }
-    }
-  };
-  const int G = gridDim.x;
-  int b = blockIdx.x;
-  if (b < B) {
-    dma(b);
-    wait_vm0();
-    __syncthreads();
-    put();
-    __syncthreads();
-    if (b + G < B) dma(b + G);
-  }
-  for (; b < B; b += G) {
-    f32x4 acc[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t) acc[t] = zero4();
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int tap = 8 * kh + s, ky = tap >> 2, kx = tap & 3;
-      const int toff = (ky & 1) * 250 + (ky >> 1) * 25 + (kx & 1) * 10 + (kx >> 1);
-      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
-#pragma unroll
-      for (int t0 = 0; t0 < MT; t0 += 3) {
-        Frag3 a[3];
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          const uint16_t* q = S + 8 * (qrow[t0 + u] + toff);
-          a[u].h = *reinterpret_cast<const bf16x8*>(q);
-          a[u].m = *reinterpret_cast<const bf16x8*>(q + 8 * PLU);
-          a[u].l = *reinterpret_cast<const bf16x8*>(q + 16 * PLU);
-        }
-#define PPO_PART(X, Y) \
-  _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(a[u].X, w.Y, acc[t0 + u]);
-        PPO_PRODUCTS(NP, PPO_PART)
-#undef PPO_PART
-      }
-    }
-    wait_vm0();        // this wave's part of the next image has landed in RAW
-    __syncthreads();   // A: the image is consumed, RAW complete
-    if (kh == 1) {
-#pragma unroll
-      for (int t = 0; t < MT; ++t) R[nt][t][lane] = acc[t];
-    }
-    __syncthreads();   // B: partials visible
-    if (kh == 0) {
-      float* o = out + (size_t)b * (81 * 64) + co;
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        const f32x4 v = acc[t] + R[nt][t][lane];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = 16 * t + 4 * g + r;
-          if (m < 81) o[m * 64] = fmaxf(v[r] + bv, 0.f);
-        }
-      }
-    }
-    __syncthreads();   // C: partials consumed
-    if (b + G < B) put();
-    __syncthreads();   // D: next image in S, RAW free
-    if (b + 2 * G < B) dma(b + 2 * G);
   }
 }
 
@@ -2279,39 +1817,22 @@ PPO_API int ppo_tune_get(const char* key) {
   return -1;
 }
 
+// fp32-MFMA tile core (x9 = 0 and the generic fallbacks): one tile shape per
+// problem class, the measured best of the round-1 sweep
+// (profiles/r01_kbench_sweep_v2.log); the other shapes were removed.
 // N = 32 output-channel problems (conv1/conv3 fwd, conv2 dgrad)
 using V32_0 = Cfg<256, 32, 4, 1, true, true>;           // 4 waves x 64 rows, 46 KB LDS
-using V32_1 = Cfg<128, 32, 4, 1, true, true>;           // 4 waves x 32 rows, 26 KB
-using V32_2 = Cfg<128, 32, 2, 1, true, true>;           // 2 waves x 64 rows, 26 KB
-using V32_3 = Cfg<128, 32, 4, 1, true, true, false, 32>;  // BK 32, 46 KB
-using V32_4 = Cfg<64, 32, 2, 1, true, true, false, 32>;   // 2 waves x 32 rows, BK 32, 28 KB
 // N = 64 problems (conv2 fwd, conv3 dgrad)
 using V64_0 = Cfg<128, 64, 2, 2, true, true>;
-using V64_1 = Cfg<64, 64, 2, 2, true, true>;
-using V64_2 = Cfg<128, 64, 4, 1, true, true>;
 
-#define PPO_VARIANTS32(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                        \
-  switch (g_tune[tk]) {                                                                           \
-    case 1: { TEMPL(V32_1) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-    case 2: { TEMPL(V32_2) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-    case 3: { TEMPL(V32_3) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-    case 4: { TEMPL(V32_4) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-    default: { TEMPL(V32_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-  }
+#define PPO_VARIANTS32(TEMPL, SETUP, M, N, Z, NAME, FLOPS) \
+  { TEMPL(V32_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }
 
 // N = 128 problems (conv2 dgrad, phases merged)
 using V128_0 = Cfg<128, 128, 2, 2, true, true>;           // 2x2 waves of 64x64, 32 KB
-using V128_1 = Cfg<256, 128, 4, 2, true, true>;           // 8 waves of 64x64, 48 KB
-using V128_2 = Cfg<128, 128, 4, 1, true, true>;           // 4 waves of 32x128, 32 KB
-using V128_3 = Cfg<64, 128, 2, 2, true, true>;            // 2x2 waves of 32x64, 24 KB
 
-#define PPO_VARIANTS128(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                        \
-  switch (g_tune[tk]) {                                                                            \
-    case 1: { TEMPL(V128_1) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-    case 2: { TEMPL(V128_2) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-    case 3: { TEMPL(V128_3) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-    default: { TEMPL(V128_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-  }
+#define PPO_VARIANTS128(TEMPL, SETUP, M, N, Z, NAME, FLOPS) \
+  { TEMPL(V128_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }
 
 // exact-split bf16 core (igemm_x9.h)
 using X32 = CfgX<128, 32, 4, 1, true, true>;          // N = 32: waves of 32x32
@@ -2320,20 +1841,12 @@ using X128 = CfgX<128, 128, 2, 2, true, true>;        // N >= 128: waves of 64x6
 using XW32 = CfgX<32, 128, 1, 4, false, false, true>;   // wgrad, 32 output channels
 using XW64 = CfgX<64, 128, 2, 2, false, false, true>;   // wgrad, 64 output channels
 using XW128 = CfgX<128, 128, 2, 2, false, false, true>; // wgrad, >= 128 output channels
-using XW128w8a = CfgX<128, 128, 4, 2, false, false, true>;  // 8 waves of 32x64
-using XW128w8b = CfgX<128, 128, 2, 4, false, false, true>;  // 8 waves of 64x32
 using XW256x128 = CfgX<256, 128, 4, 2, false, false, true>; // 8 waves of 64x64
 using XP32 = CfgX<128, 32, 4, 1, true, true, false, false, false, true>;    // B from planes, waves 32x32
 using XP64 = CfgX<128, 64, 4, 1, true, true, false, false, false, true>;    // waves 32x64
 using XP128 = CfgX<128, 128, 4, 1, true, true, false, false, false, true>;  // waves 32x128
-using XP64s = CfgX<64, 64, 2, 1, true, true, false, false, false, true>;    // 2 waves of 32x64
-using XP256x128w8 = CfgX<256, 128, 8, 1, true, true, false, false, false, true>;  // 8 waves of 32x128
 using XP128w8 = CfgX<128, 128, 8, 1, true, true, false, false, false, true>;      // 8 waves of 16x128
-using XP256x64w8 = CfgX<256, 64, 8, 1, true, true, false, false, false, true>;    // 8 waves of 32x64
-using XP128x256 = CfgX<128, 256, 4, 1, true, true, false, false, false, true>;    // 4 waves of 32x256
-using XP64x128w4 = CfgX<64, 128, 4, 1, true, true, false, false, false, true>;    // 4 waves of 16x128 (2 blocks/CU)
 using XP128x64w8 = CfgX<128, 64, 8, 1, true, true, false, false, false, true>;    // 8 waves of 16x64 (2 blocks/CU)
-using XP256x128w16 = CfgX<256, 128, 16, 1, true, true, false, false, false, true>; // 16 waves of 16x128
 // x9 = 1: the split-bf16 core where it measured faster (forward GEMMs, fc dgrad); the gather-heavy
 // conv dgrads and the wgrads stay on fp32 MFMA (their split path is VALU-bound); x9 = 2: everywhere
 // compute units of the current device (persistent-kernel grid size)
@@ -2356,41 +1869,14 @@ static inline void set_planes(P& p, const float* seg, long long n, int rows, int
   p.bpl = planes_of(seg, n); p.bps = n; p.bld = K; p.bnr = rows;
 }
 
-// dense-core experiments (fc forward, N multiple of 128; conv2 forward, N = 64)
-using VD_1 = Cfg<128, 128, 2, 2, true, true, false, 32>;  // BK 32
-using VD_2 = Cfg<256, 128, 4, 2, true, true>;             // 8 waves of 64x64
-using VD_3 = Cfg<256, 128, 2, 2, true, true>;             // 4 waves of 128x64
-using VD_4 = Cfg<128, 128, 1, 2, true, true>;             // 2 waves of 128x64
-using VD_5 = Cfg<256, 128, 4, 2, true, true, false, 32>;  // 8 waves, BK 32
-using V64_3 = Cfg<256, 64, 4, 1, true, true>;             // 4 waves of 64x64
-using V64_4 = Cfg<256, 64, 2, 1, true, true>;             // 2 waves of 128x64
-using V64_5 = Cfg<128, 64, 2, 2, true, true, false, 32>;  // BK 32
-using V64_6 = Cfg<256, 64, 4, 2, true, true>;             // 8 waves of 64x32
+// fp32-MFMA core (x9 = 0): fc forward (N multiple of 128), conv2 forward (N = 64)
+#define PPO_VARIANTS_FC(TEMPL, SETUP, M, N, Z, NAME, FLOPS) \
+  { TEMPL(CfgN128) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }
+#define PPO_VARIANTS_C2F(TEMPL, SETUP, M, N, Z, NAME, FLOPS) \
+  { TEMPL(V64_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }
 
-#define PPO_VARIANTS_FC(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                       \
-  switch (g_tune[tk]) {                                                                           \
-    case 1: { TEMPL(VD_1) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
-    case 2: { TEMPL(VD_2) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
-    case 3: { TEMPL(VD_3) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
-    case 4: { TEMPL(VD_4) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
-    case 5: { TEMPL(VD_5) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
-    default: { TEMPL(CfgN128) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-  }
-#define PPO_VARIANTS_C2F(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                       \
-  switch (g_tune[tk]) {                                                                            \
-    case 3: { TEMPL(V64_3) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
-    case 4: { TEMPL(V64_4) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
-    case 5: { TEMPL(V64_5) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
-    case 6: { TEMPL(V64_6) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }  \
-    default: { TEMPL(V64_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-  }
-
-#define PPO_VARIANTS64(TEMPL, SETUP, M, N, Z, NAME, FLOPS)                                        \
-  switch (g_tune[tk]) {                                                                           \
-    case 1: { TEMPL(V64_1) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-    case 2: { TEMPL(V64_2) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-    default: { TEMPL(V64_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); } \
-  }
+#define PPO_VARIANTS64(TEMPL, SETUP, M, N, Z, NAME, FLOPS) \
+  { TEMPL(V64_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }
 
 static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
                           const float* w1, const float* b1, float* out, uint16_t* mbits, void* stream);
@@ -2481,7 +1967,7 @@ PPO_API int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const f
 
 static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float* b2, float* out, uint16_t* mbits,
                           void* stream) {
-  if (mbits && g_tune[TK_CONV2_FWD] != 8 && g_tune[TK_CONV2_FWD] != 12) {   // no fused mask epilogue
+  if (mbits && g_tune[TK_CONV2_FWD] != 12) {   // no fused mask epilogue
     const int rc = conv2_fwd_impl(a1, B, w2p, b2, out, nullptr, stream);
     if (rc != 0 || B <= 0) return rc;
     const long long halves = (long long)B * 81 * 4;
@@ -2506,43 +1992,12 @@ static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float*
     PPO_LAUNCH_CHECK("conv2_fwd_x9c_kernel");
     return 0;
   }
-  if (g_tune[TK_CONV2_FWD] == 10) {   // LDS-DMA staged
-    if (B <= 0) return 0;
-    const int n_cu = device_cus();
-    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
-    int slot;
-    const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
-    PPO_LAUNCH_NP(conv2_fwd_dma_kernel, nb, 512, as_stream(stream), a1, B, planes_of(w2p, 64 * 512), b2, out);
-    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
-    PPO_LAUNCH_CHECK("conv2_fwd_dma_kernel");
-    return 0;
-  }
-  if (g_tune[TK_CONV2_FWD] == 8) {
-    if (B <= 0) return 0;
-    const int n_cu = device_cus();
-    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
-    int slot;
-    const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
-    const uint16_t* wpl = planes_of(w2p, 64 * 512);
-    if (mbits && g_products == 9)
-      conv2_fwd_x9_kernel<9, true><<<nb, 512, 0, as_stream(stream)>>>(a1, B, wpl, b2, out, mbits);
-    else if (mbits && g_products == 1)
-      conv2_fwd_x9_kernel<1, true><<<nb, 512, 0, as_stream(stream)>>>(a1, B, wpl, b2, out, mbits);
-    else if (mbits)
-      conv2_fwd_x9_kernel<6, true><<<nb, 512, 0, as_stream(stream)>>>(a1, B, wpl, b2, out, mbits);
-    else
-      PPO_LAUNCH_NP(conv2_fwd_x9_kernel, nb, 512, as_stream(stream), a1, B, wpl, b2, out, nullptr);
-    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
-    PPO_LAUNCH_CHECK("conv2_fwd_x9_kernel");
-    return 0;
-  }
   if (use_x9()) {
     ConvFwd<20, 32, 4, 2, 9, 64, XP64> p;
     p.in = a1; p.w = w2p; p.bias = b2; p.out = out; p.M = B * 81;
     set_planes(p, w2p, 64 * 512, 64, 512);
     return launch_x9(p, (long long)B * 81, 64, 1, as_stream(stream), "conv2_fwd", 2.0 * B * 81 * 64 * 512);
   }
-  const int tk = TK_CONV2_FWD;
 #define T2(C_) ConvFwd<20, 32, 4, 2, 9, 64, C_>
   PPO_VARIANTS_C2F(T2, (p.in = a1, p.w = w2p, p.bias = b2, p.out = out, p.M = B * 81), (long long)B * 81, 64, 1,
                    "conv2_fwd", 2.0 * B * 81 * 64 * 512)
@@ -2568,7 +2023,6 @@ PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float*
     set_planes(p, w3p, 32 * 576, 32, 576);
     return launch_x9(p, (long long)B * 49, 32, 1, as_stream(stream), "conv3_fwd", 2.0 * B * 49 * 32 * 576);
   }
-  const int tk = TK_CONV3_FWD;
 #define T3(C_) ConvFwd<9, 64, 3, 1, 7, 32, C_>
   PPO_VARIANTS32(T3, (p.in = a2, p.w = w3p, p.bias = b3, p.out = out, p.M = B * 49), (long long)B * 49, 32, 1,
                  "conv3_fwd", 2.0 * B * 49 * 32 * 576)
@@ -2583,7 +2037,7 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
   const int K = 1568;
   if (use_x9()) {
     // rollout-sized M (4096 rows) fills a quarter of the chip with 128 x 128
-    // tiles: narrower tiles there (fc_fwd tune: 0 auto, 1 128x128, 2 128x64, 3 64x64)
+    // tiles: narrower tiles there (fc_fwd tune: 0 auto, 1 128x128, 5 8 waves of 16x64)
     int v = g_tune[TK_FC_FWD];
     if (v == 0) {
       const long long t128 = ((M + 127LL) / 128) * ((H + 127) / 128);
@@ -2596,9 +2050,6 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
     set_planes(p, w4p, (long long)H * K, H, K);                                                      \
     return launch_x9(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);                      \
   }
-    if (v == 2) PPO_FC(XP64)
-    if (v == 3) PPO_FC(XP64s)
-    if (v == 4) PPO_FC(XP128w8)
     if (v == 5) PPO_FC(XP128x64w8)
     PPO_FC(XP128)
 #undef PPO_FC
@@ -2618,7 +2069,6 @@ PPO_API int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, co
     return launch_x9(p, M, N, 1, as_stream(stream), "linear_relu_fwd", 2.0 * M * N * K);
   }
   if (N % 128 == 0) {
-    const int tk = TK_FC_FWD;
 #define TF(C_) DenseReluFwd<C_>
     PPO_VARIANTS_FC(TF, (p.x = x, p.w = w, p.bias = b, p.out = out, p.M = M, p.N = N, p.K = K), M, N, 1,
                     "linear_relu_fwd", 2.0 * M * N * K)
@@ -2705,16 +2155,7 @@ PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt
     set_planes(p, wt, (long long)N * K, N, K);                                      \
     return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K); \
   }
-    switch (g_tune[TK_FC_DGRAD]) {   // tile variants (kbench A/B)
-      case 1: PPO_FCD(XP256x128w8)
-      case 2: PPO_FCD(XP128)
-      case 3: PPO_FCD(XP256x64w8)
-      case 4: PPO_FCD(XP128x256)
-      case 5: PPO_FCD(XP64x128w4)
-      case 6: PPO_FCD(XP128x64w8)
-      case 7: PPO_FCD(XP256x128w16)
-      default: PPO_FCD(XP128w8)   // measured: 0.75 vs 0.87 ms (XP128) at the c3 minibatch
-    }
+    PPO_FCD(XP128w8)   // measured: 0.75 vs 0.87 ms (XP128) at the c3 minibatch
 #undef PPO_FCD
   }
   DenseDgradMask<CfgN128> p;
@@ -2756,7 +2197,6 @@ PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const flo
     set_planes(p, w3d, 64 * 288, 64, 288);
     return launch_x9(p, (long long)B * 81, 64, 1, as_stream(stream), "conv3_dgrad", 2.0 * B * 49 * 32 * 576);
   }
-  const int tk = TK_CONV3_DGRAD;
 #define TD3(C_) ConvDgradS1<9, 64, 3, 7, 32, C_>
   PPO_VARIANTS64(TD3, (p.dy = dz3, p.wd = w3d, p.act = a2, p.dx = dz2, p.M = B * 81), (long long)B * 81, 64, 1,
                  "conv3_dgrad", 2.0 * B * 49 * 32 * 576)
@@ -2798,7 +2238,6 @@ PPO_API int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const flo
     set_planes(p, w2d, 128 * 256, 128, 256);
     return launch_x9(p, (long long)B * 100, 128, 1, as_stream(stream), "conv2_dgrad", 2.0 * B * 81 * 64 * 512);
   }
-  const int tk = TK_CONV2_DGRAD;
 #define TD2(C_) Conv2Dgrad<C_>
   PPO_VARIANTS128(TD2, (p.dy = dz2, p.wd = w2d, p.act = a1, p.dx = dz1, p.M = B * 100), (long long)B * 100, 128, 1,
                   "conv2_dgrad", 2.0 * B * 81 * 64 * 512)
@@ -2854,22 +2293,8 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
     PPO_LAUNCH_CHECK("conv1_wgrad_parts_kernel");
     return 0;
   }
-  if (obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] != 9) {
-    if (B <= 0 || Z <= 0) return 0;
-    int slot;
-    const bool prof = ppo_prof_begin("conv1_wgrad_u8", as_stream(stream), &slot);
-    if (g_products == 1)   // half-precision mode: bf16 dz
-      conv1_wgrad_bf16x3_kernel<4, 1><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
-                                                                        slab, slab_bias, g_stagger >> 4);
-    else
-      conv1_wgrad_bf16x3_kernel<4><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
-                                                                     slab_bias, g_stagger >> 4);
-    if (prof) ppo_prof_end(slot, as_stream(stream), fl);
-    PPO_LAUNCH_CHECK("conv1_wgrad_bf16x3_kernel");
-    return 0;
-  }
   if (obs_is_u8) {
-    if (g_tune[TK_CONV1_WGRAD] == 1 || g_tune[TK_CONV1_WGRAD] == 9) {
+    if (g_tune[TK_CONV1_WGRAD] == 9) {
       Conv1Wgrad<uint8_t, CfgW32n> p;
       set_wgrad(p, dz1, 32, R, Z, slab, slab_bias, C * 64);
       p.obs = (const uint8_t*)obs; p.idx = idx; p.row0 = row0; p.C = C;
@@ -2952,12 +2377,7 @@ PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int 
     p.x = x; p.K = K;                                                               \
     return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K); \
   }
-    switch (g_tune[TK_FC_WGRAD]) {   // tile variants (kbench A/B)
-      case 1: PPO_FCW(XW128w8a)
-      case 2: PPO_FCW(XW128w8b)
-      case 3: PPO_FCW(XW128)
-      default: PPO_FCW(XW256x128)   // measured: 0.79 vs 0.83 ms (XW128) at the c3 minibatch
-    }
+    PPO_FCW(XW256x128)   // measured: 0.79 vs 0.83 ms (XW128) at the c3 minibatch
 #undef PPO_FCW
   }
   DenseWgrad<CfgWfc> p;
