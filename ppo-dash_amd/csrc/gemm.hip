@@ -303,8 +303,19 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
 //     computing (MFMA) wave; the loads of part i+2 are in flight meanwhile.
 // One barrier per part.  Output: the split-K slab [Z][32][256] (u8 integers: the
 // reduce applies 1/255) and bias partials [Z][32], as the other variants.
-template <int NPD = 3>   // NPD: dz parts summed (3 exact; 1 half-precision mode)
-__global__ __launch_bounds__(512) void conv1_wgrad_parts_kernel(const float* __restrict__ dz1,
+// NW = 16 (ppo_tune_set("conv1_wgrad", 4)): four waves per SIMD.  Waves w and
+// w + 8 share column tile w & 7 and split the k-steps by parity (wave w + 8 the
+// odd global k-steps), their accumulators summed in a fixed order at the end;
+// every wave stages at most one item (E items on waves 0-6, dz items on waves
+// 8-12), so per SIMD two waves stage while two compute (waves 4-7 and 12-15
+// compute first).
+// TPW = 2 (NW = 16, ppo_tune_set("conv1_wgrad", 5)): each wave computes two
+// column tiles (2 (w & 3), +1) per A fragment read, k-steps split four ways
+// (k-group w >> 2 takes global k-steps ≡ w >> 2 mod 4): the dz fragments, the
+// same for every tile, are read from LDS half as often (the kernel is LDS-bound:
+// the staging writes and the fragment reads share the LDS with each other).
+template <int NPD = 3, int NW = 8, int TPW = 1>   // NPD: dz parts summed (3 exact; 1 half-precision mode)
+__global__ __launch_bounds__(NW * 64) void conv1_wgrad_parts_kernel(const float* __restrict__ dz1,
                                                                 const uint8_t* __restrict__ obs,
                                                                 const int64_t* __restrict__ idx, long long row0,
                                                                 int B, float* __restrict__ slab,
@@ -321,29 +332,37 @@ __global__ __launch_bounds__(512) void conv1_wgrad_parts_kernel(const float* __r
   __shared__ __attribute__((aligned(16))) uint16_t L[2 * STG];           // 84,992 B: two part stages
   __shared__ __attribute__((aligned(16))) uint4 RAW[3][RAWP];            // 52,224 B: raw parts, 3-slot ring
   __shared__ long long rowtab[MAXIMG];                                    // storage row of the block's images
-  __shared__ float bred[512];
+  __shared__ float bred[320];
+  static_assert(NW == 8 || NW == 16, "8 or 16 waves");
+  static_assert(TPW == 1 || (TPW == 2 && NW == 16), "two tiles per wave with 16 waves");
+  constexpr int NT = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  // column tile(s) tile + t (t < TPW); TPW 1: k-step parity kh (NW = 16); TPW 2: k-group kh (0-3)
+  const int tile = TPW == 2 ? 2 * (wave & 3) : wave & 7, kh = TPW == 2 ? wave >> 2 : wave >> 3;
   const int G = gridDim.x;
   const int nimg = blockIdx.x < B ? (B - 1 - (int)blockIdx.x) / G + 1 : 0, nit = NPART * nimg;
-  for (int k = tid; k < nimg; k += 512) rowtab[k] = obs_row(idx, row0, (int)blockIdx.x + k * G);
-  // B column of this lane: n = 32 wave + l32 -> (c, ky, kx)
-  const int bc = wave >> 1, bky = 4 * (wave & 1) + (l32 >> 3), bkx = l32 & 7;
-  int qoff[5][2];   // E element offset of the lane's quads for local k-step ls
+  for (int k = tid; k < nimg; k += NT) rowtab[k] = obs_row(idx, row0, (int)blockIdx.x + k * G);
+  // B column of this lane: n = 32 (tile + t) + l32 -> (c, ky, kx)
+  int qoff[TPW][5][2];   // E element offset of the lane's quads for local k-step ls
 #pragma unroll
-  for (int ls = 0; ls < 5; ++ls)
+  for (int t = 0; t < TPW; ++t) {
+    const int tt = tile + t, bc = tt >> 1, bky = 4 * (tt & 1) + (l32 >> 3), bkx = l32 & 7;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ql = 4 * ls + 2 * h + j, oyl = ql / 5, Q = ql - 5 * oyl;
-      const int r = bc * ER + 4 * oyl + bky, item = r * 5 + Q;
-      qoff[ls][j] = (r * SLOTS + Q * 8 + (bkx ^ ((item >> 1) & 7))) * 4;
-    }
+    for (int ls = 0; ls < 5; ++ls)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ql = 4 * ls + 2 * h + j, oyl = ql / 5, Q = ql - 5 * oyl;
+        const int r = bc * ER + 4 * oyl + bky, item = r * 5 + Q;
+        qoff[t][ls][j] = (r * SLOTS + Q * 8 + (bkx ^ ((item >> 1) & 7))) * 4;
+      }
+  }
   const int aoff = E_BF + l32 * DZS + 8 * h;   // + plane * DZ_BF + 16 ls
   // staging items: E item tid < 400 (row r = tid / 5 = c * 20 + yr, quad Q = tid % 5);
   // dz item tid < 320 (co = tid & 31, pixel octet oc = tid >> 5).  Threads without
   // an item DMA item 0's addresses (harmless duplicates) so every wave issues the
   // same DMA count.
-  const bool e_on = tid < 400, d_on = tid < 320;
-  const int eit = e_on ? tid : 0, dit = d_on ? tid : 0;
+  const bool e_on = tid < 400, d_on = NW == 8 ? tid < 320 : tid >= 512 && tid < 832;
+  const int eit = e_on ? tid : 0, dit = d_on ? tid - (NW == 8 ? 0 : 512) : 0;
   const int er = eit / 5, eQ = eit - 5 * er, ec = er / ER, eyr = er - ER * ec, ef = (eit >> 1) & 7;
   const int dco = dit & 31, doc = dit >> 5;
   float bacc = 0.f;
@@ -362,9 +381,9 @@ __global__ __launch_bounds__(512) void conv1_wgrad_parts_kernel(const float* __r
     }
     const char* dsrc = reinterpret_cast<const char*>(dz1 + (size_t)b * 12800 + p * 80 * 32);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int blk = wave + 8 * i;   // wave-uniform
-      if (blk < DPIECE / 64)
+    for (int i = 0; i < (NW == 8 ? 2 : 1); ++i) {
+      const int blk = NW == 8 ? wave + 8 * i : wave - 6;   // wave-uniform; NW = 16: waves 6-15
+      if (blk >= 0 && blk < DPIECE / 64)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(dsrc + 16 * (64 * blk + lane)),
                                          reinterpret_cast<__attribute__((address_space(3))) void*>(
                                              reinterpret_cast<uintptr_t>(dst + EPIECE + 64 * blk)), 16, 0, 0);
@@ -375,10 +394,14 @@ __global__ __launch_bounds__(512) void conv1_wgrad_parts_kernel(const float* __r
     const uint32_t* R = reinterpret_cast<const uint32_t*>(RAW[j % 3]);
     uint32_t ew[5];
     float dv[8];
+    if (NW == 8 || e_on) {   // NW = 8: every thread reads both (all loads issued first)
 #pragma unroll
-    for (int q = 0; q < 5; ++q) ew[q] = R[(ec * 1680 + eyr * IMG + 16 * eQ) / 4 + q];
+      for (int q = 0; q < 5; ++q) ew[q] = R[(ec * 1680 + eyr * IMG + 16 * eQ) / 4 + q];
+    }
+    if (NW == 8 || d_on) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dv[q] = __uint_as_float(R[4 * EPIECE + (8 * doc + q) * 32 + dco]);
+      for (int q = 0; q < 8; ++q) dv[q] = __uint_as_float(R[4 * EPIECE + (8 * doc + q) * 32 + dco]);
+    }
     uint16_t* S = L + st * STG;
     if (e_on) {
 #pragma unroll
@@ -404,30 +427,45 @@ __global__ __launch_bounds__(512) void conv1_wgrad_parts_kernel(const float* __r
       bacc += ((dv[0] + dv[1]) + (dv[2] + dv[3])) + ((dv[4] + dv[5]) + (dv[6] + dv[7]));
     }
   };
-  f32x16 acc;
+  f32x16 acc[TPW];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  auto compute = [&](int st) {
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  auto compute = [&](int st, int i) {
     if (no_mma) return;
     const uint16_t* S = L + st * STG;
 #pragma unroll
-    for (int ls = 0; ls < 5; ++ls) {
-      const uint2 q1 = *reinterpret_cast<const uint2*>(S + qoff[ls][0]);
-      const uint2 q2 = *reinterpret_cast<const uint2*>(S + qoff[ls][1]);
-      const bf16x8 bq = __builtin_bit_cast(bf16x8, uint4{q1.x, q1.y, q2.x, q2.y});
+    for (int ls = 0; ls < 5; ++ls) {   // global k-step 5 i + ls; the skips are wave-uniform
+      if (TPW == 2 && ((i + ls) & 3) != kh) continue;
+      if (TPW == 1 && NW == 16 && ((i + ls) & 1) != kh) continue;
+      bf16x8 bq[TPW];
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const uint2 q1 = *reinterpret_cast<const uint2*>(S + qoff[t][ls][0]);
+        const uint2 q2 = *reinterpret_cast<const uint2*>(S + qoff[t][ls][1]);
+        bq[t] = __builtin_bit_cast(bf16x8, uint4{q1.x, q1.y, q2.x, q2.y});
+      }
       const uint16_t* A = S + aoff + 16 * ls;
       if constexpr (NPD == 3) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(A + 2 * DZ_BF), bq, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(A + DZ_BF), bq, acc, 0, 0, 0);
+        const bf16x8 al = *reinterpret_cast<const bf16x8*>(A + 2 * DZ_BF), am = *reinterpret_cast<const bf16x8*>(A + DZ_BF);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bq[t], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bq[t], acc[t], 0, 0, 0);
+        }
       }
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(A), bq, acc, 0, 0, 0);
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(A);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bq[t], acc[t], 0, 0, 0);
     }
   };
   // pipeline: item j's pieces are DMA'd into RAW[j % 3] at item j - 3 (by every
   // wave, a share each); at the end of item j - 2 every wave waits for its own
   // share (vmcnt = one item's DMA count: item j + 1's may stay in flight) and the
   // barrier publishes the slot; item j - 1 stages it (put) into LDS stage j & 1.
-  const int nops = (wave < 7 ? 1 : 0) + 1 + (wave + 8 < DPIECE / 64 ? 1 : 0);
+  const int nops = NW == 8 ? (wave < 7 ? 1 : 0) + 1 + (wave + 8 < DPIECE / 64 ? 1 : 0)
+                            : (wave < 7 ? 1 : 0) + (wave >= 6 ? 1 : 0);
   auto wait_raw = [&]() {   // all but the youngest item's DMAs retired
     if (nops == 3) __builtin_amdgcn_s_waitcnt(0x0F73);        // vmcnt(3)
     else if (nops == 2) __builtin_amdgcn_s_waitcnt(0x0F72);   // vmcnt(2)
@@ -450,25 +488,72 @@ __global__ __launch_bounds__(512) void conv1_wgrad_parts_kernel(const float* __r
     wait_raw();   // item 1 retired (item 2 may be in flight)
   }
   part_barrier();
-  const bool late = wave >= 4 && !(dbg & 8);
+  const bool late = (NW == 8 ? wave >= 4 : ((wave >> 2) & 1) != 0) && !(dbg & 8);
   for (int i = 0; i < nit; ++i) {
     const int st = i & 1;
     const bool more = i + 1 < nit;
     if (!late && more) put(i + 1, st ^ 1);
     if (more) dma(i + 3);   // into RAW[i % 3]: item i was staged before the last barrier
-    compute(st);
+    compute(st, i);
     if (late && more) put(i + 1, st ^ 1);
     wait_raw();   // item i + 2 retired (item i + 3 may be in flight)
     part_barrier();
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);   // drain the clamped tail DMAs before the block exits
-  float* out = slab + (size_t)blockIdx.x * 32 * 256;
+  float* X = reinterpret_cast<float*>(L);   // stage space, free now: k-group partials
+  if constexpr (NW == 16 && TPW == 1) {   // odd-k-step partials added to the even ones
+    if (kh) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int co = (r & 3) + 8 * (r >> 2) + 4 * h, n = 32 * wave + l32;
-    out[co * 256 + n] = acc[r];
+      for (int r = 0; r < 16; ++r) X[(r * 8 + tile) * 64 + lane] = acc[0][r];
+    }
+    __syncthreads();
+    if (!kh) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[0][r] += X[(r * 8 + tile) * 64 + lane];
+    }
   }
-  bred[tid] = d_on ? bacc : 0.f;
+  if constexpr (TPW == 2) {   // fixed order: (k0 + k2) + (k1 + k3); slot = tile pair (+ 4)
+    auto xo = [&](int slot, int t, int r) { return ((slot * 2 + t) * 16 + r) * 64 + lane; };
+    const int tp = wave & 3;
+    if (kh >= 2) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) X[xo((kh - 2) * 4 + tp, t, r)] = acc[t][r];
+    }
+    __syncthreads();
+    if (kh < 2) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] += X[xo(kh * 4 + tp, t, r)];
+    }
+    __syncthreads();
+    if (kh == 1) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) X[xo(tp, t, r)] = acc[t][r];
+    }
+    __syncthreads();
+    if (kh == 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] += X[xo(tp, t, r)];
+    }
+  }
+  float* out = slab + (size_t)blockIdx.x * 32 * 256;
+  if (kh == 0) {
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = (r & 3) + 8 * (r >> 2) + 4 * h, n = 32 * (tile + t) + l32;
+        out[co * 256 + n] = acc[t][r];
+      }
+  }
+  if (d_on) bred[dit] = bacc;
   __syncthreads();
   if (tid < 32) {   // channel tid: its 10 pixel octets, fixed order
     float t = 0.f;
@@ -1788,7 +1873,7 @@ static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad"
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
 static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measured best
-static int g_tune[TK_N] = {0, 8, 8, 8, 3, 0, 12, 1, 8, 8, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   if (strcmp(key, "stagger") == 0) {
@@ -2278,7 +2363,7 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
   const long long R = (long long)B * 400;
   PPO_REQUIRE(R < 0x7fffffffLL, "ppo_conv1_wgrad: B too large");
   const double fl = 2.0 * R * 32 * C * 64;
-  if (obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] == 3) {   // part-pipelined
+  if (obs_is_u8 && C == 4 && (g_tune[TK_CONV1_WGRAD] >= 3 && g_tune[TK_CONV1_WGRAD] <= 5)) {   // part-pipelined
     if (B <= 0 || Z <= 0) return 0;
     PPO_REQUIRE((B + Z - 1) / Z <= 512, "ppo_conv1_wgrad: %d images over %d blocks (at most 512 per block)", B, Z);
     int slot;
@@ -2286,6 +2371,12 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
     if (g_products == 1)   // half-precision mode: bf16 dz
       conv1_wgrad_parts_kernel<1><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
                                                                     slab_bias, 0);
+    else if (g_tune[TK_CONV1_WGRAD] == 4)   // four waves per SIMD
+      conv1_wgrad_parts_kernel<3, 16><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
+                                                                         slab, slab_bias, g_stagger >> 4);
+    else if (g_tune[TK_CONV1_WGRAD] == 5)   // four waves per SIMD, two column tiles per wave
+      conv1_wgrad_parts_kernel<3, 16, 2><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
+                                                                            slab, slab_bias, g_stagger >> 4);
     else
       conv1_wgrad_parts_kernel<3><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
                                                                     slab_bias, g_stagger >> 4);
