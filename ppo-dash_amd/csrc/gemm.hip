@@ -24,6 +24,7 @@
 // physical k order inside a BK=16 step is a fixed permutation common to A and B.
 #include "igemm.h"
 #include "igemm_x9.h"
+#include "small.h"
 
 namespace {
 // ---------------------------------------------------------------------------
@@ -1873,9 +1874,17 @@ static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad"
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
 static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measured best
+// small_b: forwards of at most this many samples (images / linear rows) take the
+// small-batch path of small.hip (an output element per thread or wave, fp32 FMA)
+static int g_small_b = 4;
 static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
+  if (strcmp(key, "small_b") == 0) {
+    PPO_REQUIRE(value >= 0, "ppo_tune_set: small_b must be >= 0, got %d", value);
+    g_small_b = value;
+    return 0;
+  }
   if (strcmp(key, "stagger") == 0) {
     g_stagger = value;
     return 0;
@@ -1895,6 +1904,7 @@ PPO_API int ppo_tune_set(const char* key, int value) {
 }
 
 PPO_API int ppo_tune_get(const char* key) {
+  if (strcmp(key, "small_b") == 0) return g_small_b;
   if (strcmp(key, "stagger") == 0) return g_stagger;
   if (strcmp(key, "products") == 0) return g_products;
   for (int i = 0; i < TK_N; ++i)
@@ -1983,6 +1993,8 @@ PPO_API int ppo_conv1_fwd_mask(const void* obs, int obs_is_u8, const int64_t* id
 static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
                           const float* w1, const float* b1, float* out, uint16_t* mbits, void* stream) {
   PPO_REQUIRE(B >= 0 && C > 0, "ppo_conv1_fwd: B=%d C=%d", B, C);
+  if (!mbits && B > 0 && B <= g_small_b)
+    return small_conv1_fwd(obs, obs_is_u8, idx, row0, C, B, w1, b1, out, as_stream(stream));
   if (mbits && !(obs_is_u8 && C == 4 && g_tune[TK_CONV1_FWD] != 9 && g_tune[TK_CONV1_FWD] != 8)) {
     // paths without the fused mask epilogue: the conv, then the mask from its output
     const int rc = conv1_fwd_impl(obs, obs_is_u8, idx, row0, C, B, w1, b1, out, nullptr, stream);
@@ -2052,6 +2064,7 @@ PPO_API int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const f
 
 static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float* b2, float* out, uint16_t* mbits,
                           void* stream) {
+  if (!mbits && B > 0 && B <= g_small_b) return small_conv2_fwd(a1, B, w2p, b2, out, as_stream(stream));
   if (mbits && g_tune[TK_CONV2_FWD] != 12) {   // no fused mask epilogue
     const int rc = conv2_fwd_impl(a1, B, w2p, b2, out, nullptr, stream);
     if (rc != 0 || B <= 0) return rc;
@@ -2090,6 +2103,7 @@ static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float*
 }
 
 PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream) {
+  if (B > 0 && B <= g_small_b) return small_conv3_fwd(a2, B, w3p, b3, out, as_stream(stream));
   if (g_tune[TK_CONV3_FWD] == 8) {
     if (B <= 0) return 0;
     const int n_cu = device_cus();
@@ -2120,6 +2134,7 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
                        void* stream) {
   PPO_REQUIRE(H > 0 && H % 8 == 0 && ldo >= H, "ppo_fc_fwd: H=%d ldo=%d", H, ldo);
   const int K = 1568;
+  if (M > 0 && M <= g_small_b) return small_linear_fwd(x, nullptr, M, K, K, w4p, b, H, out, ldo, 1, as_stream(stream));
   if (use_x9()) {
     // rollout-sized M (4096 rows) fills a quarter of the chip with 128 x 128
     // tiles: narrower tiles there (fc_fwd tune: 0 auto, 1 128x128, 5 8 waves of 16x64)
@@ -2148,6 +2163,7 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
 PPO_API int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, const float* b, int N, float* out,
                                 void* stream) {
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_relu_fwd: K=%d must be a multiple of 4", K);
+  if (M > 0 && M <= g_small_b) return small_linear_fwd(x, nullptr, M, K, K, w, b, N, out, N, 1, as_stream(stream));
   if (use_x9()) {
     DenseReluFwd<X128> p;
     p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K;
@@ -2170,6 +2186,7 @@ PPO_API int ppo_linear_fwd_ex(const float* x, const int64_t* idx, int M, int K, 
                               int N, float* out, int ldo, int act, void* stream) {
   PPO_REQUIRE(K % 4 == 0 && lda % 4 == 0, "ppo_linear_fwd_ex: K=%d lda=%d must be multiples of 4", K, lda);
   PPO_REQUIRE(act >= 0 && act <= 2, "ppo_linear_fwd_ex: act=%d", act);
+  if (M > 0 && M <= g_small_b) return small_linear_fwd(x, idx, M, K, lda, w, b, N, out, ldo, act, as_stream(stream));
   if (use_x9()) {
     if (N <= 64) {
       DenseReluFwd<X64> p;
