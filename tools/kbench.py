@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--z2", type=int, default=0, help="conv2 wgrad split count (default: ppo_wgrad_splits)")
     ap.add_argument("--z1", type=int, default=0, help="conv1 wgrad split count (default: ppo_wgrad_splits)")
     ap.add_argument("--z3", type=int, default=0, help="conv3 wgrad split count (default: ppo_wgrad_splits)")
+    ap.add_argument("--z4", type=int, default=0, help="fc wgrad split count (default: ppo_wgrad_splits)")
     a = ap.parse_args()
     for kv in [x for x in a.tune.split(",") if x]:
         k, v = kv.split("=")
@@ -74,6 +75,7 @@ def main():
     z2 = a.z2 or z2
     z1 = a.z1 or z1
     z3 = a.z3 or z3
+    z4 = a.z4 or z4
     K = {
         "conv1_fwd": (lambda: call("ppo_conv1_fwd", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, w1.data_ptr(),
                                    b1.data_ptr(), a1.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
