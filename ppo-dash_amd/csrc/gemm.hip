@@ -264,13 +264,19 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
     for (int t = 0; t < NT; ++t)
       if (t < ntile) {
         const int rt = rq + 4 * t;
+        uint64_t bal[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float v = fmaxf(acc[t][r] * (1.0f / 255.0f) + bv, 0.f);
           o[(rt * 16 + 4 * g + r) * 32] = v;
-          if constexpr (MASK) {   // ReLU mask bits: lane (g, i16) -> pixel 16 rt + 4g + r, channel 16 ct + i16
-            const uint64_t bal = __builtin_amdgcn_ballot_w64(v > 0.f);
-            if (i16 == 0) mbits[((size_t)b * 400 + rt * 16 + 4 * g + r) * 2 + ct] = (uint16_t)(bal >> (16 * g));
+          if constexpr (MASK) bal[r] = __builtin_amdgcn_ballot_w64(v > 0.f);
+        }
+        if constexpr (MASK) {   // ReLU mask bits: lane (g, i16) of ballot r -> pixel 16 rt + 4g + r,
+          // channel 16 ct + i16; lane j < 16 stores pixel 16 rt + j's 16 bits (one store per tile)
+          if (lane < 16) {
+            const int r = lane & 3, gg = lane >> 2;
+            const uint64_t bsel = r == 0 ? bal[0] : r == 1 ? bal[1] : r == 2 ? bal[2] : bal[3];
+            mbits[((size_t)b * 400 + rt * 16 + lane) * 2 + ct] = (uint16_t)(bsel >> (16 * gg));
           }
         }
       }
