@@ -47,12 +47,14 @@ def _with_precision(fn):
 class _Workspace:
     def __init__(self):
         self.bufs = {}
+        self.version = 0   # bumped by every (re)allocation: a captured graph's buffers moved
 
     def get(self, name, numel, dtype=torch.float32, device=None):
         t = self.bufs.get(name)
         if t is None or t.numel() < numel or t.dtype != dtype or t.device != device:
             t = torch.empty(max(int(numel), 1), dtype=dtype, device=device)
             self.bufs[name] = t
+            self.version += 1
         return t
 
 

@@ -63,8 +63,9 @@ class GraphedActor(object):
         """every buffer address baked into the graph that could be reallocated"""
         e = self.eng
         gp = getattr(e, "gru_packed", None)
+        ws = e.ws["graph"]
         return (id(e), e.flat.data_ptr(), e.packed.data_ptr(), None if gp is None else gp.data_ptr(),
-                tuple((k, t.data_ptr()) for k, t in sorted(e.ws["graph"].bufs.items())))
+                id(ws), ws.version)   # any workspace reallocation bumps its version
 
     def act(self, visual_inputs, vector_inputs, rnn_hxs, masks, deterministic=True):
         """Policy.act (model.py:54-66) for the captured batch -> (value, action, log_prob, rnn_hxs)"""
