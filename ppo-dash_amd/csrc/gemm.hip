@@ -2391,7 +2391,10 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
     PPO_REQUIRE((B + Z - 1) / Z <= 512, "ppo_conv1_wgrad: %d images over %d blocks (at most 512 per block)", B, Z);
     int slot;
     const bool prof = ppo_prof_begin("conv1_wgrad_u8", as_stream(stream), &slot);
-    if (g_products == 1)   // half-precision mode: bf16 dz
+    if (g_products == 1 && g_tune[TK_CONV1_WGRAD] == 5)   // half-precision mode: bf16 dz
+      conv1_wgrad_parts_kernel<1, 16, 2><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
+                                                                            slab, slab_bias, 0);
+    else if (g_products == 1)
       conv1_wgrad_parts_kernel<1><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
                                                                     slab_bias, 0);
     else if (g_tune[TK_CONV1_WGRAD] == 4)   // four waves per SIMD
