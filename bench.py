@@ -159,6 +159,9 @@ def parse():
     p.add_argument("--gae-lanes", type=int, default=1 << 20)
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="collectives backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
+    p.add_argument("--force-collectives", action="store_true",
+                   help="run every collective (parameter broadcast, advantage statistics, per-minibatch gradient "
+                        "all-reduce, losses) even at N = 1, on a one-rank communicator of --dist-backend")
     return p.parse_args()
 
 
@@ -300,9 +303,13 @@ def eval_latency(device, H=256, V=14, steps=200, cpu_steps=20):
     hx = torch.zeros(1, H, device=device)
     m = torch.ones(1, 1, device=device)
     ga = GraphedActor(pol)
+    gr = GraphedActor(pol, carry_hidden=True)   # the eval loop's form: inputs written in place, h fed back in-graph
+    gr.obs.copy_(obs)
+    gr.vec.copy_(vec)
     res = {}
     for name, fn in (("eager", lambda h: pol.act(obs, vec, h, m, deterministic=True)),
-                     ("graph", lambda h: ga.act(obs, vec, h, m))):
+                     ("graph", lambda h: ga.act(obs, vec, h, m)),
+                     ("replay", lambda h: gr.replay())):
         h = hx
         for _ in range(10):
             h = fn(h)[3]
@@ -322,7 +329,9 @@ def eval_latency(device, H=256, V=14, steps=200, cpu_steps=20):
     cpu_ms = (time.perf_counter() - t0) / cpu_steps * 1e3
     return {"config": f"1 env, CNNBase+GRU H={H} + {V} vector obs, deterministic act, synchronised per step",
             "eager_ms_per_act": round(res["eager"], 4), "graph_ms_per_act": round(res["graph"], 4),
-            "graph_acts_per_s": round(1e3 / res["graph"], 1),
+            "replay_ms_per_act": round(res["replay"], 4), "replay_acts_per_s": round(1e3 / res["replay"], 1),
+            "note": "graph = GraphedActor.act (Policy.act signature: validity checks + input copies per act); "
+                    "replay = GraphedActor.replay (inputs written in place, hidden state carried in-graph)",
             "cpu_baseline": {"value": round(cpu_ms, 3), "unit": "ms/act", "cores": 1, "kind": "port",
                              "sample": f"oracle float64 numpy forward of one sample, {cpu_steps} acts"}}
 
@@ -509,12 +518,20 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
+    if world == 1 and args.force_collectives:   # a one-rank communicator, no launcher
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or args.force_collectives:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=device)   # RCCL over xGMI
         else:
             dist.init_process_group(args.dist_backend)
         assert dist.get_world_size() == args.gpus
+    from a2c_ppo_acktr import _dist
+    _dist.force_collectives(args.force_collectives)
+    collectives = _dist.active()
 
     from a2c_ppo_acktr import _hip
     from a2c_ppo_acktr.algo import PPO
@@ -574,7 +591,8 @@ def main():
     launches_per_iter = 8 * T + 32 * E * M + 64
     names = [k for k in args.profile_kernels.split(",") if k]
     _hip.call("ppo_prof_enable", ",".join(names).encode(), args.steps * launches_per_iter)
-    if world > 1:
+    _dist.time_grads(collectives)
+    if collectives:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -582,10 +600,22 @@ def main():
     for _ in range(args.steps):
         losses = iteration()
     torch.cuda.synchronize()
-    if world > 1:
+    if collectives:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     per_kernel = prof_collect(names)
+    _dist.time_grads(False)
+    allreduce = None
+    ar = _dist.grad_allreduce_times()
+    if ar:
+        ms = sum(t for t, _ in ar)
+        nbytes = ar[0][1]
+        allreduce = {"backend": "rccl" if args.dist_backend == "nccl" else args.dist_backend, "world": world,
+                     "per_minibatch_ms": round(ms / len(ar), 4), "launches": len(ar), "bytes": nbytes,
+                     "ms_per_iteration": round(ms / args.steps, 3),
+                     "algbw_GBps": round(nbytes / (ms / len(ar) * 1e-3) / 1e9, 1),
+                     "note": "HIP events on the engine's stream around each flat-gradient all-reduce "
+                             "(one per minibatch) inside the timed region"}
 
     # per-kernel breakdown: one more iteration with every kernel family event-timed
     # (outside the timed region: the extra events would perturb `value`)
@@ -604,7 +634,7 @@ def main():
                      "coverage": round(covered / pass_ms, 4),
                      "note": "sum of the event-timed kernel families / wall time of one profiled iteration"}
 
-    if world > 1:
+    if collectives:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
@@ -659,13 +689,16 @@ def main():
         "config": {"workload": workload,
                    "envs_per_gpu": N, "num_steps": T, "ppo_epoch": E, "num_mini_batch": M, "hidden": H,
                    "global_batch": N * T * world, "parallelism": f"dp{world}",
-                   "dist_backend": (args.dist_backend if world > 1 else None)},
+                   "dist_backend": (args.dist_backend if collectives else None),
+                   "collectives": ("forced at N=1" if collectives and world == 1 else
+                                   "per minibatch" if collectives else "none (N=1)")},
+        "allreduce": allreduce,
         "roofline": roof, "cpu_baseline": cpu, "gae_roofline": gae, "boundary_roofline": boundary, "eval_latency": evalp,
         "profile_pass": pass_info, "kernel_rooflines": kernels,
         "losses": [round(x, 6) for x in losses],
     }
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if collectives:
         dist.destroy_process_group()
 
 

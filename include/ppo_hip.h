@@ -12,8 +12,14 @@
  * Conventions
  *   - every pointer is a device pointer owned by the caller (the library never
  *     allocates or frees caller memory); `stream` is a hipStream_t;
- *   - calls are asynchronous on `stream`, never synchronise, and are safe from
- *     several host threads on distinct streams;
+ *   - calls are asynchronous on `stream` and never synchronise the device (the
+ *     two readers of device state, ppo_gru_persist_timeouts and the profiler's
+ *     collect, wait for their own stream / events only);
+ *   - kernel launches are safe from several host threads on distinct streams:
+ *     the library's scratch (the persistent GRU's counters) is keyed by
+ *     (device, stream), or passed in by the caller (ppo_gru_seq_fwd_ws).  The
+ *     tuning knobs (ppo_tune_set, ppo_gru_*_set) and the profiler are
+ *     process-global configuration: set them from one thread, between launches;
  *   - return 0 on success, a hipError_t or a PPO_E* code otherwise;
  *     ppo_last_error() returns the message of the calling thread's last error;
  *   - storage planes are [T(+1)][N] fp32 (time-major, env-minor), actions i64,
@@ -217,14 +223,32 @@ int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* idx, con
                     const float* gi, int T, int n, int H, float* hout, float* save_r, float* save_z, float* save_n,
                     float* save_ghn, float* save_hin, void* stream);
 /* ppo_gru_seq_fwd runs as ONE persistent launch when ceil(n/32)·H/16 blocks fit
- * one per CU (H in {64,128,256,512}, variant 0): row groups synchronise through
- * agent-scope release/acquire counters, bounded waits; bit-identical to the
- * step launches.  persist 0 forces the step launches. */
+ * one per CU (H in {64,128,256,512}, variant 0): row groups hand h(t) over with
+ * write-through stores and relaxed agent-scope counters, every wait bounded;
+ * bit-identical to the step launches.  persist 0 forces the step launches.
+ * Co-residency of the grid is assumed from its size, which holds on an unshared
+ * device; when another process holds CUs a wait may run out: the launch then
+ * sets its error word and every block returns without computing further steps
+ * (fail-safe, not a hang).  With the library-held words (ppo_gru_seq_fwd) the
+ * word is read by ppo_gru_persist_timeouts(stream); with ppo_gru_seq_fwd_ws the
+ * caller owns it (sticky until the caller clears it; a launch that starts with
+ * it set returns at once) and passes it to ppo_clip_adam_guarded. */
 int ppo_gru_persist_set(int v);
 int ppo_gru_persist_get(void);
-/* 1 if a persistent launch's bounded wait timed out since the last call (its
- * results are invalid); synchronises the device and clears the flag */
-int ppo_gru_persist_timeouts(void);
+/* polls before a bounded wait gives up (default 2^21; tests force timeouts with 1) */
+int ppo_gru_persist_spin_set(int polls);
+/* 1 if a ppo_gru_seq_fwd launch on `stream` timed out since the last call (its
+ * results are invalid), 0 if not, -1 on error; waits for `stream` only (a
+ * stream-ordered read of the word) and clears it */
+int ppo_gru_persist_timeouts(void* stream);
+/* counters a persistent launch over n rows needs (ints) */
+int ppo_gru_seq_counters(int n);
+/* ppo_gru_seq_fwd with caller-owned synchronisation words: counters
+ * (ppo_gru_seq_counters(n) ints, reset by the call on `stream`) and err (one int,
+ * see above); both may be NULL when the step launches run (persist 0) */
+int ppo_gru_seq_fwd_ws(const float* h0, const float* masks, const int64_t* idx, const float* whh, const float* bhh,
+                       const float* gi, int T, int n, int H, float* hout, float* save_r, float* save_z,
+                       float* save_n, float* save_ghn, float* save_hin, int* counters, int* err, void* stream);
 int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float* save_z, const float* save_n,
                     const float* save_ghn, const float* save_hin, const float* masks, const int64_t* idx,
                     const float* whhT, int T, int n, int H, float* dgi, float* dgh, float* dhz, float* carry,
@@ -279,6 +303,15 @@ int ppo_grad_sumsq(const float* g, long long n, float scale, double* partials, v
 int ppo_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, long long n,
                   const double* partials, float scale, double max_norm, double lr, double beta1, double beta2,
                   double eps, long long step, double* norm_out, void* stream);
+/* the same step, skipped when a guard is set: *guard_i != 0 (the persistent GRU's
+ * error word) or *guard_d > 0 (loss_acc[3], stored actions outside [0, A) — where
+ * the reference raises before its optimizer step, distributions.py:22); a skipped
+ * step leaves params, grads and moments bit-unchanged and adds 1 to *skipped.
+ * Any guard pointer may be NULL. */
+int ppo_clip_adam_guarded(float* params, float* grads, float* exp_avg, float* exp_avg_sq, long long n,
+                          const double* partials, float scale, double max_norm, double lr, double beta1,
+                          double beta2, double eps, long long step, double* norm_out, const int* guard_i,
+                          const double* guard_d, int* skipped, void* stream);
 
 #ifdef __cplusplus
 }

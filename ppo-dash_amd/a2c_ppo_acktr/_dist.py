@@ -12,10 +12,26 @@ RCCL over xGMI on ROCm.  Exchanges, all on the current stream:
 
 These helpers are plain torch.distributed calls so they run unchanged under
 gloo on CPU tensors (tests/test_dist_gloo.py) and under RCCL on the MI355X.
+
+force_collectives(True) runs every exchange even at world size 1 (a one-rank
+RCCL communicator: bench.py --force-collectives), so the RCCL path — stream
+ordering against the engine's raw-stream launches included — executes on a
+one-GPU box; a one-rank sum is exact, so results are bit-identical to the
+collective-free path.  time_grads(True) records HIP events around every
+gradient all-reduce on the current stream (the one the engine launches on).
 """
 import math
 
+import torch
 import torch.distributed as dist
+
+_FORCE = False
+_TIMING = {"on": False, "events": []}
+
+
+def force_collectives(on=True):
+    global _FORCE
+    _FORCE = bool(on)
 
 
 def world_size():
@@ -24,29 +40,57 @@ def world_size():
     return 1
 
 
+def active():
+    """collectives run: torch.distributed initialised and more than one rank, or forced"""
+    return dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or _FORCE)
+
+
 def broadcast_params(flat):
-    if world_size() > 1:
+    if active():
         dist.broadcast(flat, src=0)
 
 
 def allreduce_stats(stats):
-    if world_size() > 1:
+    if active():
         dist.all_reduce(stats)
     return stats
+
+
+def time_grads(on=True):
+    """start (clearing) / stop event timing of allreduce_grads"""
+    _TIMING["on"] = bool(on)
+    if on:
+        _TIMING["events"] = []
+
+
+def grad_allreduce_times():
+    """[(ms, bytes)] of the timed gradient all-reduces (synchronises the events)"""
+    out = []
+    for e0, e1, nbytes in _TIMING["events"]:
+        e1.synchronize()
+        out.append((e0.elapsed_time(e1), nbytes))
+    return out
 
 
 def allreduce_grads(grad):
     """Sum the flat gradient over ranks; returns the scale (1/G) that turns it
     into the mean, applied inside the clip + Adam kernels."""
     G = world_size()
-    if G > 1:
-        dist.all_reduce(grad)
+    if active():
+        if _TIMING["on"]:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            dist.all_reduce(grad)
+            e1.record()
+            _TIMING["events"].append((e0, e1, grad.numel() * grad.element_size()))
+        else:
+            dist.all_reduce(grad)
     return 1.0 / G
 
 
 def allreduce_losses(acc):
     G = world_size()
-    if G > 1:
+    if active():
         dist.all_reduce(acc)
         acc /= G
     return acc

@@ -87,6 +87,16 @@ class CNNEngine:
         self.rng_seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFFFFFF
         self.rng_counter = 0
         self._n_cu = None   # CU count of the device, read at the first weight gradient
+        self._init_status()
+
+    def _init_status(self):
+        # device status words: [0] persistent-GRU timeout of the running update
+        # (sticky; gates clip + Adam), [1] optimizer steps skipped by a guard,
+        # [2] persistent-GRU timeout of evaluate_sequence
+        self.status = torch.zeros(4, dtype=torch.int32, device=self.device)
+
+    def status_ptr(self, i):
+        return self.status.data_ptr() + 4 * i
 
     # ------------------------------------------------------------ parameters
     def _flatten(self):
@@ -438,8 +448,14 @@ class RecurrentEngine(CNNEngine):
         m = masks.to(self.device, torch.float32).reshape(R).contiguous()
         hout = torch.empty(R, self.H, device=self.device)
         H, s = self.H, stream()
-        call("ppo_gru_seq_fwd", hxs.data_ptr(), m.data_ptr(), None, self.pv(self.GHH), self.pv(self.GBH),
-             gi.data_ptr(), T, N, H, hout.data_ptr(), None, None, None, None, None, s)
+        cnt = ws.get("gru_cnt", call("ppo_gru_seq_counters", N), torch.int32, self.device)
+        call("ppo_gru_seq_fwd_ws", hxs.data_ptr(), m.data_ptr(), None, self.pv(self.GHH), self.pv(self.GBH),
+             gi.data_ptr(), T, N, H, hout.data_ptr(), None, None, None, None, None, cnt.data_ptr(), self.status_ptr(2),
+             s)
+        if int(self.status[2].item()):   # stream-ordered read of the launch's error word
+            self.status[2].zero_()
+            raise RuntimeError("evaluate_actions: the persistent GRU kernel timed out (its outputs are invalid; "
+                               "ppo_gru_persist_set(0) selects the per-step launches)")
         value, _, logp, ent = self._heads(hout, R, given=action.to(self.device, torch.int64), want_entropy=True)
         return value, logp, ent, hout[(T - 1) * N:]
 
@@ -463,9 +479,11 @@ class RecurrentEngine(CNNEngine):
         hout = ws.get("hout", R * H, device=dev)
         sv = {k: ws.get("s_" + k, R * H, device=dev) for k in ("r", "z", "n", "ghn", "hin")}
         masks = storage.masks
-        call("ppo_gru_seq_fwd", h0.data_ptr(), masks.data_ptr(), idx.data_ptr(), self.pv(self.GHH), self.pv(self.GBH),
-             gi.data_ptr(), T, n, H, hout.data_ptr(), sv["r"].data_ptr(), sv["z"].data_ptr(), sv["n"].data_ptr(),
-             sv["ghn"].data_ptr(), sv["hin"].data_ptr(), s)
+        cnt = ws.get("gru_cnt", call("ppo_gru_seq_counters", n), torch.int32, dev)
+        # error word status[0]: sticky for the update, gates every clip + Adam after a timeout
+        call("ppo_gru_seq_fwd_ws", h0.data_ptr(), masks.data_ptr(), idx.data_ptr(), self.pv(self.GHH),
+             self.pv(self.GBH), gi.data_ptr(), T, n, H, hout.data_ptr(), sv["r"].data_ptr(), sv["z"].data_ptr(),
+             sv["n"].data_ptr(), sv["ghn"].data_ptr(), sv["hin"].data_ptr(), cnt.data_ptr(), self.status_ptr(0), s)
         dout = ws.get("dout", R * H, device=dev)
         self._heads_train(storage, adv, idx, hout, R, hp, loss_acc, dout, feat_act=0)
         # backward through time
@@ -514,6 +532,7 @@ class MLPEngine(CNNEngine):
         self._flatten()
         self.rng_seed = int(torch.initial_seed()) & 0xFFFFFFFFFFFFFFFF
         self.rng_counter = 0
+        self._init_status()
 
     def pack(self, force=False):
         key = (sum(p._version for p in self.params), self.epoch)

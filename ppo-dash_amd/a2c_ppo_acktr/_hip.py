@@ -83,8 +83,12 @@ SIGNATURES = {
     "ppo_gru_variant_get": [],
     "ppo_gru_persist_set": [c_int],
     "ppo_gru_persist_get": [],
-    "ppo_gru_persist_timeouts": [],
+    "ppo_gru_persist_timeouts": [c_p],
+    "ppo_gru_persist_spin_set": [c_int],
+    "ppo_gru_seq_counters": [c_int],
     "ppo_gru_seq_fwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    "ppo_gru_seq_fwd_ws": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                           c_p],
     "ppo_gru_seq_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
     "ppo_gru_step_bwd_cell": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "ppo_gru_pack": [c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p],
@@ -99,13 +103,15 @@ SIGNATURES = {
     "ppo_grad_partials_count": [c_ll],
     "ppo_grad_sumsq": [c_p, c_ll, c_f, c_p, c_p],
     "ppo_clip_adam": [c_p, c_p, c_p, c_p, c_ll, c_p, c_f, c_d, c_d, c_d, c_d, c_d, c_ll, c_p, c_p],
+    "ppo_clip_adam_guarded": [c_p, c_p, c_p, c_p, c_ll, c_p, c_f, c_d, c_d, c_d, c_d, c_d, c_ll, c_p, c_p, c_p, c_p,
+                              c_p],
 }
 _RESTYPES = {"ppo_last_error": ctypes.c_char_p, "ppo_packed_weights_size": c_ll}
 # functions whose int return value is a result, not a status
 _VALUE_FUNCS = {"ppo_abi_version", "ppo_gae_partials_count", "ppo_gae_scan_partials_count", "ppo_adv_diff_partials_count",
                 "ppo_packed_weights_size", "ppo_wgrad_splits", "ppo_heads_train_blocks", "ppo_grad_partials_count",
                 "ppo_conv2_dgrad_bits_ok", "ppo_conv3_dgrad_bits_ok", "ppo_tune_get",
-                "ppo_gru_persist_get", "ppo_gru_persist_timeouts"}
+                "ppo_gru_persist_get", "ppo_gru_persist_timeouts", "ppo_gru_seq_counters"}
 
 _LIB = None
 

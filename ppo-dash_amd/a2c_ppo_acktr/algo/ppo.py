@@ -37,6 +37,9 @@ class FlatAdam(object):
         self._partials = None
         self.last_grad_norm = None
         self._norm = None
+        # (int* error word, double* bad-action count, int* skipped-step count) device
+        # pointers set by PPO.update: a guarded step is skipped on the device
+        self.guard = None
 
     def zero_grad(self, set_to_none=False):
         for p in self.param_groups[0]["params"]:
@@ -67,9 +70,10 @@ class FlatAdam(object):
         s = stream()
         call("ppo_grad_sumsq", eng.grad.data_ptr(), n, scale, self._partials.data_ptr(), s)
         mn = self.max_grad_norm if self.max_grad_norm is not None else -1.0
-        call("ppo_clip_adam", eng.flat.data_ptr(), eng.grad.data_ptr(), self.exp_avg.data_ptr(),
+        gi, gd, sk = self.guard if self.guard is not None else (None, None, None)
+        call("ppo_clip_adam_guarded", eng.flat.data_ptr(), eng.grad.data_ptr(), self.exp_avg.data_ptr(),
              self.exp_avg_sq.data_ptr(), n, self._partials.data_ptr(), scale, float(mn), float(g["lr"]),
-             float(b1), float(b2), float(g["eps"]), self.step_count, self._norm.data_ptr(), s)
+             float(b1), float(b2), float(g["eps"]), self.step_count, self._norm.data_ptr(), gi, gd, sk, s)
 
     def state_dict(self):
         return {"step": self.step_count, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
@@ -104,7 +108,7 @@ class PPO():
         self.use_clipped_value_loss = use_clipped_value_loss
         self.optimizer = FlatAdam(actor_critic.parameters(), lr=lr, eps=eps, max_grad_norm=max_grad_norm)
         self._loss_acc = None
-        if _dist.world_size() > 1:
+        if _dist.active():
             # one-time parameter broadcast so every rank starts from rank 0's weights
             eng = actor_critic.hip_engine()
             _dist.broadcast_params(eng.flat)
@@ -114,10 +118,16 @@ class PPO():
         eng = self.actor_critic.hip_engine()
         advantages = rollouts.normalized_advantages()            # ppo.py:35-37
         if self._loss_acc is None or self._loss_acc.device != eng.device:
-            # {value loss, action loss, entropy} sums + the count of stored actions outside [0, A)
-            self._loss_acc = torch.zeros(4, dtype=torch.float64, device=eng.device)
+            # {value loss, action loss, entropy} sums, the count of stored actions outside
+            # [0, A), and (filled at the end) the persistent-GRU timeout flag
+            self._loss_acc = torch.zeros(5, dtype=torch.float64, device=eng.device)
         else:
             self._loss_acc.zero_()
+        # device guards of every clip + Adam of this update: a persistent-GRU timeout
+        # (status[0]) or an out-of-range stored action (loss_acc[3]) turns the step
+        # into a no-op on the device, counted in status[1]; _losses() raises
+        eng.status[:2].zero_()
+        self.optimizer.guard = (eng.status_ptr(0), self._loss_acc.data_ptr() + 8 * 3, eng.status_ptr(1))
         hp = {"clip": float(self.clip_param), "value_coef": float(self.value_loss_coef),
               "entropy_coef": float(self.entropy_coef), "use_clipped_value_loss": bool(self.use_clipped_value_loss)}
         num_steps, num_processes = rollouts.rewards.size()[0:2]
@@ -158,15 +168,25 @@ class PPO():
                 eng.train_minibatch_rec(rollouts, advantages, envs, hp, self._loss_acc, self.optimizer)
 
     def _losses(self):
-        _dist.allreduce_losses(self._loss_acc)
+        eng = self.actor_critic.hip_engine()
+        self._loss_acc[4].copy_(eng.status[0])    # the timeout flag travels with the losses (one all-reduce):
+        _dist.allreduce_losses(self._loss_acc)     # every rank sees any rank's failure and raises with it
         num_updates = self.ppo_epoch * self.num_mini_batch        # ppo.py:90 (not the drop_last count)
         acc = self._loss_acc.tolist()                              # one D2H per update
-        if self.actor_critic.is_recurrent and call("ppo_gru_persist_timeouts"):
-            # a persistent GRU sequence kernel gave up a bounded wait: its outputs are invalid
-            raise RuntimeError("PPO.update: persistent GRU kernel timed out (ppo_gru_persist_set(0) disables it)")
+        self.optimizer.guard = None
+        if acc[3] > 0 or acc[4] > 0:
+            # the guarded steps were no-ops on the device: undo their step count so the
+            # parameters, moments and step counter are those of the last good step
+            self.optimizer.step_count -= int(eng.status[1].item())
+            eng.status[:2].zero_()
+        if acc[4] > 0:
+            # a persistent GRU sequence kernel gave up a bounded wait: no step used its outputs
+            raise RuntimeError("PPO.update: persistent GRU kernel timed out; the optimizer steps from that "
+                               "minibatch on were skipped (ppo_gru_persist_set(0) selects the step launches)")
         if acc[3] > 0:
-            # the reference's log_probs gather (distributions.py:22) raises on such an index
+            # the reference's log_probs gather (distributions.py:22) raises on such an index, before
+            # its optimizer step; each epoch visits every stored row once, hence / ppo_epoch
             raise IndexError("PPO.update: {:.0f} stored action(s) outside [0, {}) in the rollout".format(
-                acc[3] * _dist.world_size(), self.actor_critic.hip_engine().A))
+                acc[3] * _dist.world_size() / self.ppo_epoch, eng.A))
         value_loss_epoch, action_loss_epoch, dist_entropy_epoch = (x / num_updates for x in acc[:3])
         return value_loss_epoch, action_loss_epoch, dist_entropy_epoch

@@ -19,6 +19,8 @@
 //   after the loop: dW_hh, dW_ih as split-K wgrads over all T·n_env rows,
 //     dx = dgi · W_ih[:, :H] masked by the fc ReLU.
 // Saved per step for the backward: r, z, n, W_hn h + b_hn, h_in ([T][n][H] each).
+#include <mutex>
+
 #include "igemm.h"
 
 namespace {
@@ -345,8 +347,16 @@ __global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict
 // h(t) tile (write-through sc1 stores drained by every wave, then one relaxed
 // agent-scope counter increment of its group) and waits for the group's count
 // before step t + 1 (relaxed polls), reading h only with sc1 loads — the R1
-// hand-off of cdna_hip_programming.md §6 G16, correct wherever the blocks run.  The grid (<= one block per CU) is
-// resident by its size; every wait is bounded and a timeout sets *err.
+// hand-off of cdna_hip_programming.md §6 G16, correct wherever the blocks run.
+// Co-residency: the grid (<= one block per CU) is resident by its size when the
+// device is not shared; it is NOT guaranteed when another process's kernels hold
+// CUs.  So every wait is bounded (spin_max polls) and fail-safe: a block whose
+// wait runs out sets *err and returns at once, and every waiting block also polls
+// *err and leaves as soon as it is set — no block computes with a stale h(t-1),
+// and the error reaches the host after at most one bounded wait.  *err is sticky
+// (the caller clears it): a launch that starts with it set returns immediately,
+// and ppo_clip_adam_guarded skips the optimizer step while it is set, so a timed
+// out minibatch never changes the parameters.
 template <int H>
 __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict__ h0, const float* __restrict__ masks,
                                                         const int64_t* __restrict__ idx, const float* __restrict__ whh,
@@ -354,9 +364,13 @@ __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict_
                                                         int T, int n, float* __restrict__ hout, float* __restrict__ sr,
                                                         float* __restrict__ sz, float* __restrict__ sn,
                                                         float* __restrict__ sghn, float* __restrict__ shin,
-                                                        int* __restrict__ cnt, int* __restrict__ err) {
+                                                        int* __restrict__ cnt, int* __restrict__ err, int spin_max) {
   __shared__ f32x4 P[4][6][64];
+  __shared__ int s_abort;
   const int j0 = blockIdx.y * 16, m0 = blockIdx.x * 32, grp = blockIdx.x, need = H / 16;
+  if (threadIdx.x == 0) s_abort = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_abort) return;   // an earlier launch on these words timed out: its outputs (and ours) are invalid
   float b[3][H / 16];
   gru_load_whh<H>(whh, j0, b);
   const bool sv = sr != nullptr;
@@ -365,17 +379,24 @@ __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict_
     if (t > 0) {   // h(t-1) of the group's rows complete (all its unit blocks published)
       if (threadIdx.x == 0) {
         const int target = need * t;
-        int it = 0;
+        int it = 0, ab = 0;
         while (__hip_atomic_load(cnt + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-          if (++it > (1 << 21)) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {   // another block gave up
+            ab = 1;
+            break;
+          }
+          if (++it > spin_max) {
             __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ab = 1;
             break;
           }
           __builtin_amdgcn_s_sleep(2);
         }
+        s_abort = ab;
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: h loads stay below the poll
       __syncthreads();
+      if (s_abort) return;   // never compute step t from an incomplete h(t-1)
     }
     const float* mk = masks && !idx ? masks + (size_t)t * n : masks;
     gru_fwd_tile<H, true>(m0, j0, t == 0 ? h0 : hout + o - (size_t)n * H, mk, idx ? idx + (size_t)t * n : nullptr, b, bhh,
@@ -477,21 +498,48 @@ static int g_gru_variant = 0;
 // grid fits one block per CU; 0: one step kernel per step
 static int g_gru_persist = 1;
 
-// group counters + timeout word of the persistent kernels (one stream at a time)
-static int* persist_words(int groups) {
-  static int* buf = nullptr;
-  static int cap = 0;
-  if (groups + 1 > cap) {
-    if (buf) (void)hipFree(buf);
-    cap = groups + 1 > 4096 ? groups + 1 : 4096;
-    if (hipMalloc(&buf, (size_t)cap * sizeof(int)) != hipSuccess) {
-      buf = nullptr;
-      cap = 0;
-      return nullptr;
-    }
-    if (hipMemset(buf, 0, (size_t)cap * sizeof(int)) != hipSuccess) return nullptr;
+// bounded-wait length of the persistent kernels (polls of ~64 clocks each)
+static int g_gru_spin = 1 << 21;
+
+// Library-held synchronisation words for ppo_gru_seq_fwd (callers that pass their
+// own use ppo_gru_seq_fwd_ws): one buffer {err, counters...} per (device, stream),
+// so launches in flight on different streams or devices never share counters.
+// Grow-only; a buffer is reallocated only after its stream has drained.
+struct PersistWords {
+  int dev;
+  hipStream_t stream;
+  int* buf;
+  int cap;
+};
+static std::mutex g_words_mu;
+static PersistWords g_words[64];
+static int g_nwords = 0;
+
+static int* persist_words(hipStream_t st, int groups) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_words_mu);
+  PersistWords* w = nullptr;
+  for (int i = 0; i < g_nwords; ++i)
+    if (g_words[i].dev == dev && g_words[i].stream == st) w = &g_words[i];
+  if (!w) {
+    if (g_nwords == 64) return nullptr;
+    w = &g_words[g_nwords++];
+    *w = PersistWords{dev, st, nullptr, 0};
   }
-  return buf;
+  if (groups + 1 > w->cap) {
+    if (w->buf) {
+      if (hipStreamSynchronize(st) != hipSuccess) return nullptr;   // the old buffer's launches are done
+      (void)hipFree(w->buf);
+    }
+    const int cap = groups + 1 > 4096 ? groups + 1 : 4096;
+    w->buf = nullptr;
+    w->cap = 0;
+    if (hipMalloc(&w->buf, (size_t)cap * sizeof(int)) != hipSuccess) return (w->buf = nullptr);
+    if (hipMemset(w->buf, 0, (size_t)cap * sizeof(int)) != hipSuccess) return nullptr;
+    w->cap = cap;
+  }
+  return w->buf;
 }
 
 static int gru_cus() {
@@ -509,13 +557,12 @@ static int gru_cus() {
 template <int H>
 int launch_seq16(const float* h0, const float* masks, const int64_t* idx, const float* whh, const float* bhh,
                  const float* gi, int T, int n, float* hout, float* sr, float* sz, float* sn, float* sghn,
-                 float* shin, hipStream_t st) {
+                 float* shin, int* cnt, int* err, hipStream_t st) {
   const int groups = ceil_div(n, 32);
-  int* w = persist_words(groups);
-  PPO_REQUIRE(w != nullptr, "ppo_gru_seq_fwd: counter allocation failed");
-  PPO_HIP_CHECK(hipMemsetAsync(w + 1, 0, (size_t)groups * sizeof(int), st), "ppo_gru_seq_fwd: counter reset");
+  PPO_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)groups * sizeof(int), st), "ppo_gru_seq_fwd: counter reset");
   dim3 grid((unsigned)groups, H / 16);
-  gru_seq16_kernel<H><<<grid, 256, 0, st>>>(h0, masks, idx, whh, bhh, gi, T, n, hout, sr, sz, sn, sghn, shin, w + 1, w);
+  gru_seq16_kernel<H><<<grid, 256, 0, st>>>(h0, masks, idx, whh, bhh, gi, T, n, hout, sr, sz, sn, sghn, shin, cnt, err,
+                                            g_gru_spin);
   PPO_LAUNCH_CHECK("gru_seq16_kernel");
   return 0;
 }
@@ -626,18 +673,24 @@ PPO_API int ppo_gru_variant_get(void) { return g_gru_variant; }
 // which at ~10 us per step kernel were the critical path of the recurrent update.
 // Rows of step t are t*n .. t*n + n - 1; mask of row j at step t: masks[idx[t*n + j]]
 // (idx NULL: masks[t*n + j]).
-PPO_API int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* idx, const float* whh,
-                            const float* bhh, const float* gi, int T, int n, int H, float* hout, float* save_r,
-                            float* save_z, float* save_n, float* save_ghn, float* save_hin, void* stream) {
+PPO_API int ppo_gru_seq_counters(int n) { return n > 0 ? ceil_div(n, 32) : 1; }
+
+PPO_API int ppo_gru_seq_fwd_ws(const float* h0, const float* masks, const int64_t* idx, const float* whh,
+                               const float* bhh, const float* gi, int T, int n, int H, float* hout, float* save_r,
+                               float* save_z, float* save_n, float* save_ghn, float* save_hin, int* counters, int* err,
+                               void* stream) {
   PPO_REQUIRE(T >= 0 && n >= 0 && H > 0 && H % 32 == 0, "ppo_gru_seq_fwd: T=%d n=%d H=%d", T, n, H);
   ProfScope prof("gru_seq_fwd", as_stream(stream), 2.0 * T * n * 3.0 * H * H);
-  if (T > 0 && n > 0 && g_gru_variant == 0 && g_gru_persist && (long long)ceil_div(n, 32) * (H / 16) <= gru_cus()) {
+  if (T > 0 && n > 0 && g_gru_variant == 0 && g_gru_persist && (long long)ceil_div(n, 32) * (H / 16) <= gru_cus() &&
+      (H == 64 || H == 128 || H == 256 || H == 512)) {
+    PPO_REQUIRE(counters != nullptr && err != nullptr, "ppo_gru_seq_fwd_ws: the persistent launch needs counters "
+                                                       "(ppo_gru_seq_counters(n) ints) and an error word");
     hipStream_t st = as_stream(stream);
     switch (H) {
-      case 64: return launch_seq16<64>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, st);
-      case 128: return launch_seq16<128>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, st);
-      case 256: return launch_seq16<256>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, st);
-      case 512: return launch_seq16<512>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, st);
+      case 64: return launch_seq16<64>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, counters, err, st);
+      case 128: return launch_seq16<128>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, counters, err, st);
+      case 256: return launch_seq16<256>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, counters, err, st);
+      default: return launch_seq16<512>(h0, masks, idx, whh, bhh, gi, T, n, hout, save_r, save_z, save_n, save_ghn, save_hin, counters, err, st);
     }
   }
   const bool sv = save_r != nullptr;
@@ -652,6 +705,19 @@ PPO_API int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* 
     if (rc) return rc;
   }
   return 0;
+}
+
+// the same with the library's per-(device, stream) words (ppo_gru_persist_timeouts reads them)
+PPO_API int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* idx, const float* whh,
+                            const float* bhh, const float* gi, int T, int n, int H, float* hout, float* save_r,
+                            float* save_z, float* save_n, float* save_ghn, float* save_hin, void* stream) {
+  int* w = nullptr;
+  if (T > 0 && n > 0 && g_gru_persist) {
+    w = persist_words(as_stream(stream), ppo_gru_seq_counters(n));
+    PPO_REQUIRE(w != nullptr, "ppo_gru_seq_fwd: counter allocation failed");
+  }
+  return ppo_gru_seq_fwd_ws(h0, masks, idx, whh, bhh, gi, T, n, H, hout, save_r, save_z, save_n, save_ghn, save_hin,
+                            w ? w + 1 : nullptr, w, stream);
 }
 
 PPO_API int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float* save_z, const float* save_n,
@@ -688,15 +754,30 @@ PPO_API int ppo_gru_persist_set(int v) {
 }
 PPO_API int ppo_gru_persist_get(void) { return g_gru_persist; }
 
-// 1 if a persistent kernel's bounded wait has timed out since the last call
-// (results of that launch are invalid); synchronises the device; clears the word
-PPO_API int ppo_gru_persist_timeouts(void) {
-  int* w = persist_words(0);
-  PPO_REQUIRE(w != nullptr, "ppo_gru_persist_timeouts: no counter buffer");
+// bounded-wait length (polls) of the persistent kernels; tests force a timeout with 1
+PPO_API int ppo_gru_persist_spin_set(int polls) {
+  PPO_REQUIRE(polls >= 0, "ppo_gru_persist_spin_set: %d", polls);
+  g_gru_spin = polls;
+  return 0;
+}
+
+// 1 if a ppo_gru_seq_fwd launch on `stream` timed out since the last call (its
+// results are invalid), else 0; reads the library's word for (this device,
+// stream) in stream order — waits for that stream only — and clears it
+PPO_API int ppo_gru_persist_timeouts(void* stream) {
+  hipStream_t st = as_stream(stream);
+  int* w = persist_words(st, 0);
+  if (w == nullptr) {
+    ppo_set_error("ppo_gru_persist_timeouts: no counter buffer");
+    return -1;
+  }
   int v = 0;
-  PPO_HIP_CHECK(hipDeviceSynchronize(), "ppo_gru_persist_timeouts");
-  PPO_HIP_CHECK(hipMemcpy(&v, w, sizeof(int), hipMemcpyDeviceToHost), "ppo_gru_persist_timeouts");
-  if (v) PPO_HIP_CHECK(hipMemset(w, 0, sizeof(int)), "ppo_gru_persist_timeouts");
+  if (hipMemcpyAsync(&v, w, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    ppo_set_error("ppo_gru_persist_timeouts: read failed");
+    return -1;
+  }
+  if (v && hipMemsetAsync(w, 0, sizeof(int), st) != hipSuccess) return -1;
   return v;
 }
 

@@ -44,7 +44,19 @@ __global__ __launch_bounds__(OPT_THREADS) void clip_adam_kernel(float* __restric
                                                                const double* __restrict__ partials, int nparts,
                                                                float scale, float max_norm, float step_size,
                                                                float bc2_sqrt, float beta1, float beta2, float eps,
-                                                               double* __restrict__ norm_out) {
+                                                               double* __restrict__ norm_out,
+                                                               const int* __restrict__ guard_i,
+                                                               const double* __restrict__ guard_d,
+                                                               int* __restrict__ skipped) {
+  // guards (stream-ordered: written by earlier kernels of this minibatch): a timed
+  // out persistent GRU launch (*guard_i != 0) or stored actions outside [0, A)
+  // (*guard_d > 0) make this step a no-op — parameters, moments and gradient stay
+  // bit-unchanged — and count it, so the host can undo its step counter and raise
+  const bool skip = (guard_i && *guard_i != 0) || (guard_d && *guard_d > 0.0);
+  if (skip) {
+    if (skipped && blockIdx.x == 0 && threadIdx.x == 0) *skipped += 1;
+    return;
+  }
   __shared__ double r[OPT_THREADS];
   double s = 0.0;
   for (int i = threadIdx.x; i < nparts; i += OPT_THREADS) s += partials[i];
@@ -93,6 +105,14 @@ PPO_API int ppo_grad_sumsq(const float* g, long long n, float scale, double* par
 PPO_API int ppo_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, long long n,
                           const double* partials, float scale, double max_norm, double lr, double beta1, double beta2,
                           double eps, long long step, double* norm_out, void* stream) {
+  return ppo_clip_adam_guarded(params, grads, exp_avg, exp_avg_sq, n, partials, scale, max_norm, lr, beta1, beta2, eps,
+                               step, norm_out, nullptr, nullptr, nullptr, stream);
+}
+
+PPO_API int ppo_clip_adam_guarded(float* params, float* grads, float* exp_avg, float* exp_avg_sq, long long n,
+                                  const double* partials, float scale, double max_norm, double lr, double beta1,
+                                  double beta2, double eps, long long step, double* norm_out, const int* guard_i,
+                                  const double* guard_d, int* skipped, void* stream) {
   PPO_REQUIRE(n > 0 && step >= 1, "ppo_clip_adam: n=%lld step=%lld", n, step);
   ProfScope prof("clip_adam", as_stream(stream), 28.0 * n);
   const double bc1 = 1.0 - pow(beta1, (double)step);
@@ -103,7 +123,7 @@ PPO_API int ppo_clip_adam(float* params, float* grads, float* exp_avg, float* ex
   long long b = (n + OPT_THREADS - 1) / OPT_THREADS;
   clip_adam_kernel<<<(unsigned)(b < 1024 ? b : 1024), OPT_THREADS, 0, as_stream(stream)>>>(
       params, grads, exp_avg, exp_avg_sq, n, partials, ppo_grad_partials_count(n), scale, mn, step_size, bc2_sqrt,
-      (float)beta1, (float)beta2, (float)eps, norm_out);
+      (float)beta1, (float)beta2, (float)eps, norm_out, guard_i, guard_d, skipped);
   PPO_LAUNCH_CHECK("clip_adam_kernel");
   return 0;
 }

@@ -62,3 +62,45 @@ def test_graphed_actor_vs_oracle(gpu):
     np.testing.assert_allclose(v.cpu().numpy().ravel(), np.ravel(value), rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(h1.cpu().numpy(), np.reshape(hT, (1, H)), rtol=1e-4, atol=1e-5)
     assert int(a.item()) == int(np.argmax(logits.ravel()))
+
+
+def test_graphed_replay_carries_hidden_state(gpu):
+    """GraphedActor.replay (the evaluation loop's fast path: inputs written in place
+    into ga.obs / ga.vec / ga.masks, the new hidden state fed back inside the
+    graph) equals eager Policy.act step by step over a masked sequence, bit for bit."""
+    from a2c_ppo_acktr.evaluation import GraphedActor
+    H, V = 256, 14
+    pol = _policy(True, H, V).to(gpu)
+    ga = GraphedActor(pol, carry_hidden=True)
+    g = torch.Generator().manual_seed(5)
+    hx = torch.zeros(1, H, device=gpu)
+    for step in range(8):
+        obs = torch.rand(1, 4, 84, 84, generator=g).to(gpu)
+        vec = torch.rand(1, V, generator=g).to(gpu)
+        m = torch.full((1, 1), 0.0 if step == 4 else 1.0, device=gpu)
+        with torch.no_grad():
+            ve, ae, le, hx = pol.act(obs, vec, hx, m, deterministic=True)
+        ga.obs.copy_(obs)
+        ga.vec.copy_(vec)
+        ga.masks.copy_(m)
+        vg, ag, lg, hg = ga.replay()
+        for a, b in ((ve, vg), (ae, ag), (le, lg), (hx, hg), (hx, ga.hxs)):
+            assert torch.equal(a, b), step
+
+
+def test_graphed_actor_recaptures_on_precision_change(gpu):
+    """Policy.half() / float() after a GraphedActor was built: the next act follows
+    the new arithmetic mode (re-captured), i.e. equals eager acting in that mode."""
+    from a2c_ppo_acktr.evaluation import GraphedActor
+    pol = _policy(False, 512, 0).to(gpu)
+    ga = GraphedActor(pol)
+    obs = torch.rand(1, 4, 84, 84, generator=torch.Generator().manual_seed(2)).to(gpu)
+    hx, m = torch.zeros(1, 1, device=gpu), torch.ones(1, 1, device=gpu)
+    n0 = ga.captures
+    for mode in ("half", "float"):
+        getattr(pol, mode)()
+        with torch.no_grad():
+            ve = pol.act(obs, None, hx, m, deterministic=True)[0].clone()
+        vg = ga.act(obs, None, hx, m)[0]
+        assert torch.equal(ve, vg), mode
+    assert ga.captures == n0 + 2

@@ -1284,7 +1284,7 @@ def test_gru_persistent_sequence_equals_steps(gpu, T, n, H, use_idx):
         finally:
             Hh.call("ppo_gru_persist_set", 1)
         outs[persist] = o
-    assert Hh.call("ppo_gru_persist_timeouts") == 0
+    assert Hh.call("ppo_gru_persist_timeouts", _s()) == 0
     for k in outs[0]:
         assert torch.isfinite(outs[1][k]).all(), k
         assert torch.equal(outs[0][k], outs[1][k]), (k, (outs[0][k] - outs[1][k]).abs().max().item(),

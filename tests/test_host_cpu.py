@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = _hip.lib()   # loads without a GPU; no compute calls are made
     missing = [s for s in header_symbols() if not hasattr(lib, s)]
     assert not missing, missing
-    assert lib.ppo_abi_version() == 1
+    assert lib.ppo_abi_version() == 2
 
 
 def test_ctypes_table_matches_header():

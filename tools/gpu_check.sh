@@ -19,6 +19,8 @@ for s in $STEPS; do
   case $s in
     pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     pytestall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
+    new) run pytest_new 900 python -u -m pytest ${TESTS:-tests/test_failsafe.py tests/test_rccl.py tests/test_evaluation.py} -m gpu -x -v -s --timeout 300 --timeout-method thread ;;
+    rcclbench) run bench_rccl 900 python bench.py --force-collectives --no-cpu-baseline --no-gae-roofline --no-boundary --steps 3 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench 900 python bench.py --no-cpu-baseline --steps 2 --warmup 1 ;;
