@@ -82,6 +82,12 @@ def profiled(products):
         # conv1 forward: 79,424 B of compulsory HBM traffic per sample (28,224 B u8 in, 51,200 B f32 out)
         # against 6.55 MFLOP at bf16/3 -> HBM-bound
         "conv1_fwd_u8": ("hbm", PEAK_HBM_GBPS, "conv1_flop", "v_mfma_f32_16x16x32_bf16 x3 (u8 exact), image-resident"),
+        # --obs f32 / rgb: conv1 over fp32 operands (both split): the split MFMA ceiling
+        "conv1_fwd_f32": mf(", conv1 on fp32 observation rows, image-resident parts"),
+        "conv1_fwd_rgb": mf(", conv1 on raw RGB frames, NormalizeWrapper + FrameStackMono(2) decode fused"),
+        "conv1_wgrad_f32": mf(", conv1 weight gradient on fp32 observation rows"),
+        "conv1_wgrad_rgb": mf(", conv1 weight gradient on raw RGB frames, decode fused"),
+        "obs_preprocess": hbm("f2 chain into the fp32 storage slot (--obs f32 env step)"),
         "fc_fwd": mf(", fc 1568->H + ReLU (tile GEMM)"),
         "linear_dgrad_mask": mf(", fc dgrad with conv3's ReLU mask"),
         "linear_wgrad": mf(", fc / GRU weight gradients, split-K slabs"),
@@ -108,7 +114,7 @@ def profiled(products):
 # event-timed inside the timed region (the MFMA trunk kernels; the dominant one
 # is the `roofline` line); the rest are timed in one profiled iteration after it
 TIMED = ("conv2_fwd", "conv2_dgrad", "conv2_wgrad", "conv3_fwd", "conv3_dgrad", "conv3_wgrad", "conv1_wgrad_u8",
-         "conv1_fwd_u8")
+         "conv1_fwd_u8", "conv1_fwd_f32", "conv1_wgrad_f32", "conv1_fwd_rgb", "conv1_wgrad_rgb")
 PROFILED = profiled(6)
 # compulsory HBM bytes per image of the image-resident conv kernels (fp32 NHWC
 # activations, u8 observations, ReLU mask bits) and the layer's MACs per image:
@@ -116,6 +122,10 @@ PROFILED = profiled(6)
 # image for 3.3 M MACs), so both rooflines are reported
 CONV_HBM = {
     "conv1_fwd_u8": (3276800, 28224 + 51200),
+    "conv1_fwd_f32": (3276800, 112896 + 51200),         # fp32 rows in, a1 out
+    "conv1_fwd_rgb": (3276800, 21168 + 51200),          # raw RGB frame in, a1 out
+    "conv1_wgrad_f32": (3276800, 51200 + 112896),
+    "conv1_wgrad_rgb": (3276800, 51200 + 21168),
     "conv1_wgrad_u8": (3276800, 51200 + 28224),          # dz1 + u8 image
     "conv2_fwd": (2654208, 51200 + 20736),               # a1 + a2 (+ 648 B mask bits, training)
     "conv2_dgrad": (2654208, 20736 + 1600 + 51200),      # dz2 + conv1 mask bits + dz1
@@ -159,6 +169,11 @@ def parse():
     p.add_argument("--gae-lanes", type=int, default=1 << 20)
     p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                    help="collectives backend for N > 1 (nccl = RCCL; gloo only to rehearse on one GPU)")
+    p.add_argument("--obs", default="u8", choices=("u8", "f32", "rgb"),
+                   help="observation form: u8 4x84x84 synthetic frames (default, the headline); f32 = the reference's "
+                        "fp32 storage plane fed by the f1/f2 chain (raw RGB frame -> NormalizeWrapper + "
+                        "FrameStackMono(2) on the GPU, ppo_obs_preprocess); rgb = raw u8 RGB frames stored, the same "
+                        "decode fused into conv1")
     p.add_argument("--force-collectives", action="store_true",
                    help="run every collective (parameter broadcast, advantage statistics, per-minibatch gradient "
                         "all-reduce, losses) even at N = 1, on a one-rank communicator of --dist-backend")
@@ -545,16 +560,39 @@ def main():
     H = args.hidden or (256 if args.recurrent else 512)
     V = args.vec_len if args.recurrent else 0
     torch.manual_seed(1)
-    env = SyntheticVecEnv(N, seed=123 + 7919 * rank, p_done=0.01, device=device)
+    frame_shape = (4, 84, 84) if args.obs == "u8" else (84, 84, 3)   # f32 / rgb: raw RGB frames from the env
+    env = SyntheticVecEnv(N, obs_shape=frame_shape, seed=123 + 7919 * rank, p_done=0.01, device=device)
     policy = Policy((4, 84, 84), env.action_space, base=CNNBase,
                     base_kwargs={"recurrent": args.recurrent, "hidden_size": H}, vector_obs_len=V)
     policy.to(device)
     if args.half_precision:
         policy.half()
+    pre = None
+    if args.obs != "u8":
+        from a2c_ppo_acktr.vec_env import ObsPreprocess
+        # NormalizeWrapper("ObtRetro-v6")'s shapes: a fp32-valued mean [84][84][3] (synthetic: the reference's
+        # file stays on the host) and its std value
+        mean = np.random.default_rng(0).uniform(20, 80, (84, 84, 3)).astype(np.float32).astype(np.float64)
+        pre = ObsPreprocess(84, "norm", mean, 36.31282043457031, mono=True, device=device)
+        if args.obs == "rgb":
+            policy.set_obs_decode(pre)
     agent = PPO(policy, 0.1, E, M, 0.5, 0.001, lr=1e-4, eps=1e-5, max_grad_norm=0.5)
-    rollouts = RolloutStorage(T, N, (4, 84, 84), [V], env.action_space, policy.recurrent_hidden_state_size,
-                              obs_dtype=torch.uint8, device=device)
-    env.reset_into(rollouts.obs[0])
+    store_shape, store_dtype = {"u8": ((4, 84, 84), torch.uint8), "f32": ((4, 84, 84), torch.float32),
+                                "rgb": ((84, 84, 3), torch.uint8)}[args.obs]
+    rollouts = RolloutStorage(T, N, store_shape, [V], env.action_space, policy.recurrent_hidden_state_size,
+                              obs_dtype=store_dtype, device=device)
+    raw = torch.empty(N, 84, 84, 3, dtype=torch.uint8, device=device) if args.obs == "f32" else None
+
+    def env_write(slot, action=None):
+        """the env step into storage slot `slot`: f32 runs the f2 chain (raw frame ->
+        fp32 4-channel policy input) as the reference's VecPyTorch feed does"""
+        if raw is None:
+            return env.step_into(slot, action) if action is not None else env.reset_into(slot)
+        out = env.step_into(raw, action) if action is not None else env.reset_into(raw)
+        pre(raw, out=slot)
+        return out
+
+    env_write(rollouts.obs[0])
     vec_src = torch.rand(N, V, device=device) if V else None   # synthetic vector obs (fixed)
 
     def iteration():
@@ -563,7 +601,7 @@ def main():
                 value, action, logp, hxs = policy.act(rollouts.obs[step], rollouts.vector_obs[step],
                                                       rollouts.recurrent_hidden_states[step], rollouts.masks[step])
             slot = rollouts.obs[step + 1]
-            reward, masks, bad_masks = env.step_into(slot, action)
+            reward, masks, bad_masks = env_write(slot, action)
             rollouts.insert(slot, vec_src if V else rollouts.vector_obs[step + 1], hxs, action, logp, value, reward,
                             masks, bad_masks)
         with torch.no_grad():
@@ -642,8 +680,10 @@ def main():
         dist.destroy_process_group()
         return
 
+    obs_desc = {"u8": "", "f32": ", fp32 obs storage fed by the f2 chain (--obs f32)",
+                "rgb": ", raw RGB obs storage, decode fused into conv1 (--obs rgb)"}[args.obs]
     workload = ((f"c5: CNNBase+GRU H={H} + {V} vector obs" if args.recurrent else f"c3: CNNBase H={H}")
-                + f", {N} env lanes x {T} steps per GPU, PPO {E} epochs x {M} minibatches "
+                + obs_desc + f", {N} env lanes x {T} steps per GPU, PPO {E} epochs x {M} minibatches "
                   f"(rollout + GAE + update, " + ("--half-precision: bf16 GEMM operands, fp32 accumulation"
                                                   if args.half_precision else "fp32") + ")")
     kernels = {}
@@ -685,9 +725,12 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.half_precision else "f32",
         "split_products": 1 if args.half_precision else args.products,
-        "data": "synthetic: counter-hash u8 4x84x84 obs, U[0,1) rewards, Bernoulli(0.01) dones; random-init weights",
+        "data": ("synthetic: counter-hash u8 4x84x84 obs" if args.obs == "u8" else
+                 "synthetic: counter-hash u8 84x84x3 RGB frames, NormalizeWrapper(synthetic fp32 mean, std 36.31) + "
+                 "FrameStackMono(2)") + ", U[0,1) rewards, Bernoulli(0.01) dones; random-init weights",
         "config": {"workload": workload,
                    "envs_per_gpu": N, "num_steps": T, "ppo_epoch": E, "num_mini_batch": M, "hidden": H,
+                   "obs": args.obs,
                    "global_batch": N * T * world, "parallelism": f"dp{world}",
                    "dist_backend": (args.dist_backend if collectives else None),
                    "collectives": ("forced at N=1" if collectives and world == 1 else

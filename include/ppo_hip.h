@@ -117,6 +117,30 @@ int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, long long 
  * (mbits [B][400] u32: bit c of pixel p = out[p][c] > 0, 1.6 KB per image) */
 int ppo_conv1_fwd_mask(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
                        const float* w1, const float* b1, float* out, uint32_t* mbits, void* stream);
+/* conv1 on the observation forms of the reference's own env chain (conv1f.hip):
+ * image-resident split-bf16 MFMA kernels (both operands split three ways, six part
+ * products: fp32 accuracy).  ppo_conv1_fwd / ppo_conv1_wgrad route fp32
+ * observations with C = 4 here.  mbits (nullable): ReLU mask bits as
+ * ppo_conv1_fwd_mask writes them.
+ *   _f32: fp32 rows [4][84][84] (the fp32 storage plane T/run.py fills,
+ *         storage.py:12), 16-B aligned;
+ *   _rgb: raw u8 RGB frames [84][84][3] (21,168 B rows, 16-B aligned) decoded in
+ *         the operand loader exactly as NormalizeWrapper + FrameStackMono(2) +
+ *         TransposeImage + .float() (T/sohojoe_wrappers.py:958-991, 563-638;
+ *         T/make_env.py:411-413; = ppo_obs_preprocess mode 2 / 1 / 0 with mono):
+ *         channel c < 3 = fl32(((double)u - mean[y][x][c]) / std), channel 3 the
+ *         transposed grey plane; mean fp32 [84][84][3] (NULL: 0; then std 255
+ *         gives u/255, std 1 the raw values — raw mode, where the frame is still
+ *         u8 inside FrameStackMono and its grey plane is stored truncated to u8).  Weight gradients: split-K slab
+ *         [Z][32][256] + bias partials [Z][32] (reduce with scale 1). */
+int ppo_conv1_fwd_f32(const float* obs, const int64_t* idx, long long row0, int B, const float* w1, const float* b1,
+                      float* out, uint32_t* mbits, void* stream);
+int ppo_conv1_fwd_rgb(const uint8_t* frames, const int64_t* idx, long long row0, int B, const float* mean, double stdv,
+                      const float* w1, const float* b1, float* out, uint32_t* mbits, void* stream);
+int ppo_conv1_wgrad_f32(const float* dz1, const float* obs, const int64_t* idx, long long row0, int B, int Z,
+                        float* slab, float* slab_bias, void* stream);
+int ppo_conv1_wgrad_rgb(const float* dz1, const uint8_t* frames, const int64_t* idx, long long row0, int B,
+                        const float* mean, double stdv, int Z, float* slab, float* slab_bias, void* stream);
 /* model.py:178 Conv2d(32,64,4,s2)+ReLU */
 int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream);
 /* the same, also writing its ReLU mask as bits (mbits [B][81] u64: bit c of pixel p = out[p][c] > 0) */

@@ -80,6 +80,7 @@ class CNNEngine:
         self.params = list(policy.parameters())
         self.ws = {"act": _Workspace(), "train": _Workspace()}
         self.act_ws = "act"   # workspace of the forward (act / get_value / evaluate) paths
+        self.obs_decode = None   # (mean fp32 [84][84][3] device tensor | None, std) for raw u8 RGB frames
         self.packed = None
         self._pack_key = None
         self.epoch = 0  # bumped by every in-place parameter write done by HIP kernels
@@ -175,6 +176,42 @@ class CNNEngine:
             return 0
         raise TypeError(f"observations must be uint8, float32 or float16, got {obs.dtype}")
 
+    @staticmethod
+    def _is_rgb(obs):
+        """raw u8 RGB frames [..., 84, 84, 3] (decoded inside conv1 by obs_decode)"""
+        return obs.dtype == torch.uint8 and tuple(obs.shape[-3:]) == (84, 84, 3)
+
+    def set_obs_decode(self, mean, std):
+        """NormalizeWrapper + FrameStackMono(2) of raw RGB frames, fused into conv1:
+        mean (fp32-representable [84][84][3], or None) and std (u/255: None, 255)."""
+        if self.C != 4:
+            raise NotImplementedError("the fused RGB decode produces FrameStackMono(2)'s 4 channels (C = 4)")
+        if mean is not None:
+            m64 = torch.as_tensor(mean, dtype=torch.float64).reshape(84, 84, 3)
+            m32 = m64.to(torch.float32)
+            if not torch.equal(m32.to(torch.float64), m64):
+                raise ValueError("the fused decode needs fp32-representable means (NormalizeWrapper's files hold "
+                                 "fp32 values); use ObsPreprocess into fp32 storage otherwise")
+            mean = m32.contiguous().to(self.device)
+        if not float(std):
+            raise ValueError("std must be non-zero")
+        self.obs_decode = (mean, float(std))
+
+    def _conv1(self, obs, idx, B, a1, m1, s):
+        """conv1 (+ ReLU, + mask bits when m1 is given) of B rows of obs"""
+        if self._is_rgb(obs):
+            if self.obs_decode is None:
+                raise TypeError("raw u8 RGB frames need the fused decode: Policy.set_obs_decode(ObsPreprocess)")
+            mean, std = self.obs_decode
+            call("ppo_conv1_fwd_rgb", obs.data_ptr(), ptr(idx, torch.int64, "idx"), 0, B, ptr(mean), std,
+                 self.pv(self.W1), self.pv(self.B1), a1.data_ptr(), ptr(m1), s)
+        elif m1 is not None:
+            call("ppo_conv1_fwd_mask", obs.data_ptr(), self._obs_args(obs), ptr(idx, torch.int64, "idx"), 0, self.C,
+                 B, self.pv(self.W1), self.pv(self.B1), a1.data_ptr(), m1.data_ptr(), s)
+        else:
+            call("ppo_conv1_fwd", obs.data_ptr(), self._obs_args(obs), ptr(idx, torch.int64, "idx"), 0, self.C, B,
+                 self.pv(self.W1), self.pv(self.B1), a1.data_ptr(), s)
+
     def _obs_f32(self, obs, idx, B, ws):
         """fp16 observations (RolloutStorage.half(), storage.py:48-58): the rows the
         trunk reads (idx into the plane, or the batch) converted to an fp32
@@ -192,7 +229,6 @@ class CNNEngine:
         output (post-ReLU) to `out` (row stride ldo) or a workspace [B,H]."""
         dev = self.device
         obs, idx = self._obs_f32(obs, idx, B, ws)
-        is_u8 = self._obs_args(obs)
         a1 = ws.get("a1", B * 400 * 32, device=dev)
         a2 = ws.get("a2", B * 81 * 64, device=dev)
         a3 = ws.get("a3", B * FEAT, device=dev)
@@ -204,14 +240,12 @@ class CNNEngine:
             # read by the conv2 / conv3 dgrads instead of the fp32 activations
             m1 = ws.get("m1bits", B * 400, dtype=torch.int32, device=dev)
             m2 = ws.get("m2bits", B * 81, dtype=torch.int64, device=dev)
-            call("ppo_conv1_fwd_mask", obs.data_ptr(), is_u8, ptr(idx, torch.int64, "idx"), 0, self.C, B,
-                 self.pv(self.W1), self.pv(self.B1), a1.data_ptr(), m1.data_ptr(), s)
+            self._conv1(obs, idx, B, a1, m1[:B * 400], s)
             call("ppo_conv2_fwd_mask", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), m2.data_ptr(),
                  s)
             self._mask_rows = B
         else:
-            call("ppo_conv1_fwd", obs.data_ptr(), is_u8, ptr(idx, torch.int64, "idx"), 0, self.C, B,
-                 self.pv(self.W1), self.pv(self.B1), a1.data_ptr(), s)
+            self._conv1(obs, idx, B, a1, None, s)
             call("ppo_conv2_fwd", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), s)
         call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
         call("ppo_fc_fwd", a3.data_ptr(), B, self.pk(2), self.pv(self.B4), self.H, out.data_ptr(), ldo, s)
@@ -219,8 +253,12 @@ class CNNEngine:
 
     def _check_obs(self, obs):
         obs = obs if obs.is_cuda else obs.to(self.device)
+        if self.obs_decode is not None and self._is_rgb(obs) and obs.dim() == 4:
+            return obs.contiguous()
         if tuple(obs.shape[1:]) != (self.C, 84, 84):
-            raise RuntimeError(f"CNNBase expects [N,{self.C},84,84] observations, got {tuple(obs.shape)}")
+            raise RuntimeError(f"CNNBase expects [N,{self.C},84,84] observations"
+                               + (" or raw [N,84,84,3] u8 frames" if self.obs_decode is not None else "")
+                               + f", got {tuple(obs.shape)}")
         return obs.contiguous()
 
     def _heads(self, h, B, deterministic=False, noise=None, given=None, want_entropy=False, value_only=False,
@@ -342,7 +380,11 @@ class CNNEngine:
         Z = call("ppo_wgrad_splits", R, tiles, target, 16)
         slab = ws.get("slab", Z * M * NW, device=dev)
         slab_b = ws.get("slab_b", Z * M, device=dev)
-        if layer == "conv1":
+        if layer == "conv1" and self._is_rgb(x):
+            mean, std = self.obs_decode
+            call("ppo_conv1_wgrad_rgb", dz.data_ptr(), x.data_ptr(), ptr(idx), 0, B, ptr(mean), std, Z,
+                 slab.data_ptr(), slab_b.data_ptr(), s)
+        elif layer == "conv1":
             call("ppo_conv1_wgrad", dz.data_ptr(), x.data_ptr(), self._obs_args(x), ptr(idx), 0, self.C, B, Z,
                  slab.data_ptr(), slab_b.data_ptr(), s)
         elif layer == "conv2":
@@ -352,7 +394,8 @@ class CNNEngine:
         else:
             call("ppo_linear_wgrad", dz.data_ptr(), x.data_ptr(), B, self.H, FEAT, Z, slab.data_ptr(),
                  slab_b.data_ptr(), s)
-        scale = 1.0 / 255.0 if layer == "conv1" and x.dtype == torch.uint8 else 1.0   # u8 staged as integers
+        # u8 4-channel observations are staged as integers (1/255 in the reduce); RGB frames are decoded to fp32
+        scale = 1.0 / 255.0 if layer == "conv1" and x.dtype == torch.uint8 and not self._is_rgb(x) else 1.0
         call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, M, NW, kind, ka, kb, self.gv(wi), self.gv(bi),
              scale, 0, s)
 

@@ -46,6 +46,10 @@ SIGNATURES = {
     "ppo_pack_weights": [c_p, c_p, c_p, c_int, c_p, c_p],
     "ppo_conv1_fwd": [c_p, c_int, c_p, c_ll, c_int, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv1_fwd_mask": [c_p, c_int, c_p, c_ll, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
+    "ppo_conv1_fwd_f32": [c_p, c_p, c_ll, c_int, c_p, c_p, c_p, c_p, c_p],
+    "ppo_conv1_fwd_rgb": [c_p, c_p, c_ll, c_int, c_p, c_d, c_p, c_p, c_p, c_p, c_p],
+    "ppo_conv1_wgrad_f32": [c_p, c_p, c_p, c_ll, c_int, c_int, c_p, c_p, c_p],
+    "ppo_conv1_wgrad_rgb": [c_p, c_p, c_p, c_ll, c_int, c_p, c_d, c_int, c_p, c_p, c_p],
     "ppo_conv2_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv2_fwd_mask": [c_p, c_int, c_p, c_p, c_p, c_p, c_p],
     "ppo_conv3_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],

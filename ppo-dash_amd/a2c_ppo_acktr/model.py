@@ -104,6 +104,25 @@ class Policy(nn.Module):
     def half_precision(self):
         return getattr(self, "_half_mode", False)
 
+    def set_obs_decode(self, preprocess):
+        """Feed raw u8 RGB frames [N][84][84][3] (VecPyTorch(..., fused=True),
+        RolloutStorage(..., (84, 84, 3), obs_dtype=torch.uint8)) instead of the fp32
+        4-channel policy input: the env-side NormalizeWrapper + FrameStackMono(2) +
+        TransposeImage + .float() chain (T/make_env.py:411-413) that `preprocess`
+        (a vec_env.ObsPreprocess, mono=True) describes then runs inside conv1's
+        operand loader, bit-identical to it (csrc/conv1f.hip).  None switches back."""
+        eng = self.hip_engine()
+        if preprocess is None:
+            eng.obs_decode = None
+            return self
+        if not preprocess.mono or preprocess.size != 84:
+            raise NotImplementedError("the fused decode is FrameStackMono(2) on 84x84 frames (mono=True)")
+        if preprocess.mode == "norm":
+            eng.set_obs_decode(preprocess.mean, preprocess.std)
+        else:
+            eng.set_obs_decode(None, 255.0 if preprocess.mode == "div255" else 1.0)
+        return self
+
     # ------------------------------------------------------------- engine
     def __getstate__(self):
         st = self.__dict__.copy()

@@ -112,7 +112,14 @@ class VecPyTorch(object):
     transpose wrappers moved onto the GPU); without it visual obs are copied as
     they come and cast to fp32 (fp16 with half_precision) on the device."""
 
-    def __init__(self, venv, device, half_precision=False, preprocess=None):
+    def __init__(self, venv, device, half_precision=False, preprocess=None, fused=False):
+        """fused=True: hand the raw u8 RGB frames on unchanged ([N][S][S][3], 21 KB
+        per frame in HBM) for a policy that decodes them inside conv1
+        (Policy.set_obs_decode(preprocess)); store them in a
+        RolloutStorage(..., (S, S, 3), ..., obs_dtype=torch.uint8)."""
+        if fused and preprocess is None:
+            raise ValueError("fused=True needs the preprocess the policy decodes with")
+        self.fused = bool(fused)
         self.venv = venv
         self.num_envs = venv.num_envs
         self.device = device
@@ -138,7 +145,9 @@ class VecPyTorch(object):
             obs = obs["visual"]
         dt = torch.float16 if self._half_precision else torch.float32
         vis = self._stage["visual"].upload(obs, self.device)   # u8 frames cross PCIe as u8
-        if self.preprocess is not None:
+        if self.fused:
+            pass   # raw frames: the policy's conv1 applies the decode
+        elif self.preprocess is not None:
             vis = self.preprocess(vis)
             if self._half_precision:
                 vis = vis.half()

@@ -2001,6 +2001,10 @@ static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, lo
   PPO_REQUIRE(B >= 0 && C > 0, "ppo_conv1_fwd: B=%d C=%d", B, C);
   if (!mbits && B > 0 && B <= g_small_b)
     return small_conv1_fwd(obs, obs_is_u8, idx, row0, C, B, w1, b1, out, as_stream(stream));
+  // float observations (the reference's fp32 storage plane): the image-resident
+  // split-bf16 kernel of conv1f.hip (tune 7: the fp32-MFMA tile GEMM, for A/B)
+  if (!obs_is_u8 && C == 4 && g_tune[TK_CONV1_FWD] != 7 && ((uintptr_t)obs & 15) == 0)
+    return ppo_conv1_fwd_f32((const float*)obs, idx, row0, B, w1, b1, out, reinterpret_cast<uint32_t*>(mbits), stream);
   if (mbits && !(obs_is_u8 && C == 4 && g_tune[TK_CONV1_FWD] != 9 && g_tune[TK_CONV1_FWD] != 8)) {
     // paths without the fused mask epilogue: the conv, then the mask from its output
     const int rc = conv1_fwd_impl(obs, obs_is_u8, idx, row0, C, B, w1, b1, out, nullptr, stream);
@@ -2410,6 +2414,8 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
     PPO_LAUNCH_CHECK("conv1_wgrad_parts_kernel");
     return 0;
   }
+  if (!obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] != 9 && ((uintptr_t)obs & 15) == 0)   // conv1f.hip
+    return ppo_conv1_wgrad_f32(dz1, (const float*)obs, idx, row0, B, Z, slab, slab_bias, stream);
   if (obs_is_u8) {
     if (g_tune[TK_CONV1_WGRAD] == 9) {
       Conv1Wgrad<uint8_t, CfgW32n> p;

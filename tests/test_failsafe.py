@@ -114,23 +114,57 @@ def test_gru_timeout_in_evaluate_actions_raises(gpu):
 
 @pytest.mark.parametrize("recurrent", [False, True])
 def test_out_of_range_action_raises_before_any_step(gpu, recurrent):
-    """A stored action outside [0, A) (the reference's gather raises on it before
-    its optimizer step): IndexError with the true count (not multiplied by the
-    epoch count), parameters / moments / step counter bit-unchanged; after the
-    caller repairs the rollout, the update succeeds."""
+    """Stored actions outside [0, A) in every lane of one step (so the update's
+    first minibatch already holds one): IndexError with the true count (not
+    multiplied by the epoch count), parameters / moments / step counter
+    bit-unchanged; after the caller repairs the rollout, the update succeeds."""
     pol, agent, st, fill = _rollout(gpu, recurrent=recurrent)
     fill()
     agent.update(st)
     st.after_update()
     fill()
     before = _state(pol, agent)
-    good = st.actions[3, 5].clone()
-    st.actions[3, 5] = 99
-    with pytest.raises(IndexError, match=r"\b1 stored action"):
+    good = st.actions[3].clone()
+    st.actions[3] = 99
+    with pytest.raises(IndexError, match=r"\b64 stored action"):
         agent.update(st)
     torch.cuda.synchronize()
     _assert_same(_state(pol, agent), before)
-    st.actions[3, 5] = good
+    st.actions[3] = good
     losses = agent.update(st)
     assert all(np.isfinite(losses))
     assert _state(pol, agent)[3] == before[3] + 4
+
+
+@pytest.mark.parametrize("recurrent", [False, True])
+def test_out_of_range_action_mid_update(gpu, recurrent):
+    """One bad stored action: as in the reference, the minibatches before the one
+    holding it take their optimizer steps and the update raises there — the step
+    counter advances by exactly that many steps (found by replaying the update's
+    randperm draws on the default generator) and no later step lands."""
+    pol, agent, st, fill = _rollout(gpu, recurrent=recurrent)
+    fill()
+    agent.update(st)
+    st.after_update()
+    fill()
+    before = _state(pol, agent)
+    N, T, E, M = 64, 16, 2, 2
+    st.actions[3, 5] = 99
+    rng = torch.get_rng_state()
+    first = None
+    for e in range(E):   # the update's sampler draws (storage.py:138-141 / :170)
+        perm = torch.randperm(N if recurrent else N * T)
+        per = (N if recurrent else N * T) // M
+        for j in range(M):
+            chunk = perm[j * per:(j + 1) * per]
+            hit = (chunk == 5).any() if recurrent else (chunk == 3 * N + 5).any()
+            if first is None and bool(hit):
+                first = e * M + j
+    torch.set_rng_state(rng)
+    with pytest.raises(IndexError, match=r"\b1 stored action"):
+        agent.update(st)
+    torch.cuda.synchronize()
+    after = _state(pol, agent)
+    assert after[3] == before[3] + first
+    if first == 0:
+        _assert_same(after, before)

@@ -67,28 +67,66 @@ def _check_returns(st, nv):
     return adv
 
 
-@pytest.mark.parametrize("N", [4096, 1024])   # c3, c2 (T=128, 8 minibatches)
-def test_cnn_iteration_full_size(gpu, N):
-    from a2c_ppo_acktr import model as M
+def _obs_setup(kind, N, T, gpu, pol, env):
+    """storage + env-step writer for an observation form (bench.py --obs):
+    u8 — synthetic u8 4x84x84 frames (the headline); f32 — the reference's fp32
+    storage plane, filled by the f2 chain from raw RGB frames (ppo_obs_preprocess);
+    rgb — the raw RGB frames stored, the same decode fused into conv1.  Returns
+    (storage, write(slot, action|None), decode(rows of the obs plane) -> fp32 x)."""
     from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.vec_env import ObsPreprocess
+    if kind == "u8":
+        st = RolloutStorage(T, N, (4, 84, 84), [0], env.action_space, 1, obs_dtype=torch.uint8, device=gpu)
+        write = lambda slot, a=None: env.step_into(slot, a) if a is not None else env.reset_into(slot)  # noqa: E731
+        return st, write, lambda rows: rows.double() / 255.0
+    mean = np.random.default_rng(0).uniform(20, 80, (84, 84, 3)).astype(np.float32).astype(np.float64)
+    pre = ObsPreprocess(84, "norm", mean, 36.31282043457031, device=gpu)
+    if kind == "rgb":
+        pol.set_obs_decode(pre)
+        st = RolloutStorage(T, N, (84, 84, 3), [0], env.action_space, 1, obs_dtype=torch.uint8, device=gpu)
+        write = lambda slot, a=None: env.step_into(slot, a) if a is not None else env.reset_into(slot)  # noqa: E731
+        return st, write, lambda rows: pre(rows.contiguous())
+    st = RolloutStorage(T, N, (4, 84, 84), [0], env.action_space, 1, obs_dtype=torch.float32, device=gpu)
+    raw = torch.empty(N, 84, 84, 3, dtype=torch.uint8, device=gpu)
+
+    def write(slot, a=None):
+        out = env.step_into(raw, a) if a is not None else env.reset_into(raw)
+        pre(raw, out=slot)
+        return out
+    return st, write, lambda rows: rows
+
+
+@pytest.mark.parametrize("N,kind", [(4096, "u8"), (1024, "u8"), (4096, "f32"), (4096, "rgb")])   # c3, c2 (T=128, 8 minibatches)
+def test_cnn_iteration_full_size(gpu, N, kind):
+    """kind f32 / rgb: the observation forms the reference's own env chain hands
+    over (fp32 storage plane; raw RGB frames with the decode fused into conv1),
+    held to the same bar as the u8 headline path."""
+    from a2c_ppo_acktr import model as M
     from a2c_ppo_acktr.synthetic import SyntheticVecEnv
     T, H, Mb = 128, 512, 8
     torch.manual_seed(1)
-    env = SyntheticVecEnv(N, seed=123, p_done=0.01, device=gpu)
+    env = SyntheticVecEnv(N, obs_shape=(4, 84, 84) if kind == "u8" else (84, 84, 3), seed=123, p_done=0.01,
+                          device=gpu)
     pol = M.Policy((4, 84, 84), env.action_space, base=M.CNNBase, base_kwargs={"recurrent": False, "hidden_size": H})
     flat0 = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).clone()
     pol.to(gpu)
-    st = RolloutStorage(T, N, (4, 84, 84), [0], env.action_space, 1, obs_dtype=torch.uint8, device=gpu)
-    env.reset_into(st.obs[0])
-    nv = _rollout(pol, st, env, T)
+    st, write, decode = _obs_setup(kind, N, T, gpu, pol, env)
+    write(st.obs[0])
+    for step in range(T):
+        with torch.no_grad():
+            v, a, lp, h = pol.act(st.obs[step], st.vector_obs[step], st.recurrent_hidden_states[step], st.masks[step])
+        r, m, bm = write(st.obs[step + 1], a)
+        st.insert(st.obs[step + 1], st.vector_obs[step + 1], h, a, lp, v, r, m, bm)
+    with torch.no_grad():
+        nv = pol.get_value(st.obs[-1], st.vector_obs[-1], st.recurrent_hidden_states[-1], st.masks[-1])
     torch.cuda.synchronize()
 
     # stored values / log-probs of the rollout vs the float64 forward (strided subset)
     shapes = O.cnn_param_shapes(H)
     p64 = O.unflatten(flat0.numpy(), shapes)
     ts, ns = np.array([0, T // 2, T - 1]), np.arange(0, N, 64)
-    obs = st.obs[ts][:, ns].cpu().numpy().reshape(-1, 4, 84, 84)
-    value, logits, _ = O.cnn_forward(p64, O.decode_obs(obs))
+    rows = st.obs[ts][:, ns].reshape(len(ts) * len(ns), *st.obs.shape[2:])
+    value, logits, _ = O.cnn_forward(p64, decode(rows).double().cpu().numpy())
     c = O.categorical(logits)
     acts = st.actions[ts][:, ns].cpu().numpy().reshape(-1)
     lp_ref = np.take_along_axis(c["norm_logits"], acts[:, None], 1)[:, 0]
@@ -105,18 +143,24 @@ def test_cnn_iteration_full_size(gpu, N):
     cap = _GradCapture()
     eng.train_minibatch(st, adv, idx, HP, loss, cap)
     torch.cuda.synchronize()
-    p = TR.unflatten(flat0, H, dtype=torch.float64, device=gpu, requires_grad=True)
     flat = lambda t: t[:T].reshape(T * N, *t.shape[2:])  # noqa: E731
-    grads, losses = TR.minibatch_grads(p, flat(st.obs), flat(st.actions), flat(st.action_log_probs),
-                                       adv.reshape(-1), flat(st.value_preds), flat(st.returns), idx=idx,
-                                       clip=HP["clip"], value_coef=HP["value_coef"], entropy_coef=HP["entropy_coef"])
+    if kind == "u8":
+        obs_in, planes, ridx = flat(st.obs), [flat(st.actions), flat(st.action_log_probs), adv.reshape(-1),
+                                              flat(st.value_preds), flat(st.returns)], idx
+    else:   # the minibatch's fp32 policy input (the reference chain's values), rows in minibatch order
+        obs_in = decode(flat(st.obs)[idx])
+        planes = [flat(st.actions)[idx], flat(st.action_log_probs)[idx], adv.reshape(-1)[idx],
+                  flat(st.value_preds)[idx], flat(st.returns)[idx]]
+        ridx = None
+    p = TR.unflatten(flat0, H, dtype=torch.float64, device=gpu, requires_grad=True)
+    grads, losses = TR.minibatch_grads(p, obs_in, *planes, idx=ridx, clip=HP["clip"], value_coef=HP["value_coef"],
+                                       entropy_coef=HP["entropy_coef"])
     print("float64 reference done", flush=True)
     # the same gradient at the reference's precision: torch fp32 autograd on the
     # device (im2col GEMMs on the vendor BLAS, chunk gradients summed in fp32)
     p32 = TR.unflatten(flat0, H, dtype=torch.float32, device=gpu, requires_grad=True)
-    g32, _ = TR.minibatch_grads(p32, flat(st.obs), flat(st.actions), flat(st.action_log_probs),
-                                adv.reshape(-1), flat(st.value_preds), flat(st.returns), idx=idx, chunk=8192,
-                                clip=HP["clip"], value_coef=HP["value_coef"], entropy_coef=HP["entropy_coef"])
+    g32, _ = TR.minibatch_grads(p32, obs_in, *planes, idx=ridx, chunk=8192, clip=HP["clip"],
+                                value_coef=HP["value_coef"], entropy_coef=HP["entropy_coef"])
     print("fp32 comparator done", flush=True)
     g32 = torch.cat([t.reshape(-1) for t in g32]).cpu().numpy()
     _check_grads(cap.grad.cpu().numpy(), grads, shapes, fp32_flat=g32)

@@ -19,7 +19,8 @@ for s in $STEPS; do
   case $s in
     pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     pytestall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
-    new) run pytest_new 900 python -u -m pytest ${TESTS:-tests/test_failsafe.py tests/test_rccl.py tests/test_evaluation.py} -m gpu -x -v -s --timeout 300 --timeout-method thread ;;
+    new) run pytest_new 1100 python -u -m pytest ${TESTS:-tests/test_failsafe.py tests/test_rccl.py tests/test_evaluation.py} ${KSEL:+-k "$KSEL"} -m gpu -x -v -s --timeout 600 --timeout-method thread ;;
+    obsbench) for o in f32 rgb; do run bench_obs_$o 900 python bench.py --obs $o --no-cpu-baseline --no-gae-roofline --no-boundary --steps 3; done ;;
     rcclbench) run bench_rccl 900 python bench.py --force-collectives --no-cpu-baseline --no-gae-roofline --no-boundary --steps 3 ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;

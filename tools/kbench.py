@@ -72,10 +72,17 @@ def main():
         return call("ppo_wgrad_splits", R, tiles, 2048, 16)
 
     z1, z2, z3, z4 = zs(B * 400, 1), zs(B * 81, 4), zs(B * 49, 5), zs(B, ((H + 127) // 128) * 13)
+    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+    z1c = a.z1 or max(n_cu, -(-B // 512))   # the engine's split for the image-resident conv1 wgrads
     z2 = a.z2 or z2
     z1 = a.z1 or z1
     z3 = a.z3 or z3
     z4 = a.z4 or z4
+    obs32 = frames = mean = None
+    if any(k.endswith(("_f32", "_rgb")) for k in a.only.split(",")):
+        obs32 = (torch.randn(rows, 4, 84, 84, device=dev, generator=g) * 0.8).contiguous()
+        frames = torch.randint(0, 256, (rows, 84, 84, 3), dtype=torch.uint8, device=dev, generator=g)
+        mean = torch.rand(84, 84, 3, device=dev, generator=g) * 60 + 20
     K = {
         "conv1_fwd": (lambda: call("ppo_conv1_fwd", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, w1.data_ptr(),
                                    b1.data_ptr(), a1.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
@@ -114,6 +121,16 @@ def main():
                                      slab_b.data_ptr(), s), 2.0 * B * 81 * 64 * 512),
         "conv1_wgrad": (lambda: call("ppo_conv1_wgrad", dz1.data_ptr(), obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, z1,
                                      slab.data_ptr(), slab_b.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
+        "conv1_fwd_f32": (lambda: call("ppo_conv1_fwd_f32", obs32.data_ptr(), idx.data_ptr(), 0, B, w1.data_ptr(),
+                                       b1.data_ptr(), a1.data_ptr(), m1.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
+        "conv1_fwd_rgb": (lambda: call("ppo_conv1_fwd_rgb", frames.data_ptr(), idx.data_ptr(), 0, B, mean.data_ptr(),
+                                       36.31282043457031, w1.data_ptr(), b1.data_ptr(), a1.data_ptr(), m1.data_ptr(),
+                                       s), 2.0 * B * 400 * 32 * 256),
+        "conv1_wgrad_f32": (lambda: call("ppo_conv1_wgrad_f32", dz1.data_ptr(), obs32.data_ptr(), idx.data_ptr(), 0, B,
+                                         z1c, slab.data_ptr(), slab_b.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
+        "conv1_wgrad_rgb": (lambda: call("ppo_conv1_wgrad_rgb", dz1.data_ptr(), frames.data_ptr(), idx.data_ptr(), 0,
+                                         B, mean.data_ptr(), 36.31282043457031, z1c, slab.data_ptr(),
+                                         slab_b.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
         "conv1_wreduce": (lambda: call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), z1, 32, 256, 0, 0, 0,
                                        gw.data_ptr(), gb.data_ptr(), 1.0 / 255, 0, s), 0.0),
     }
