@@ -75,6 +75,12 @@ __device__ __forceinline__ float gray3(float r, float g, float b, bool u8) {
   return u8 ? (float)(uint8_t)v : v;
 }
 
+// workgroup barrier that publishes LDS writes (lgkmcnt(0)) but leaves global loads
+// in flight: __syncthreads' fence would wait for every outstanding load (vmcnt(0)),
+// i.e. for the register prefetch of the next items; the compiler still waits for
+// those loads where their registers are used
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // 4 fp32 -> the three bf16 planes' 4-element pieces (uint2 each), each part the
 // RNE of the remaining residual (v_cvt_pk_bf16_f32); NPL 1: hi only
 template <int NPL>
@@ -366,7 +372,7 @@ __global__ __launch_bounds__(512) void conv1_fwd_x6_kernel(const void* __restric
       fetch_frame(0);
       store_frame();
       fetch_frame(1);
-      __syncthreads();
+      lds_barrier();
     }
     prefetch(0);
     put(0, 0);
@@ -380,7 +386,7 @@ __global__ __launch_bounds__(512) void conv1_fwd_x6_kernel(const void* __restric
         if ((it + 1) % NPART == 0) {   // the next item starts a new frame: every put of this one is done
           store_frame();
           fetch_frame((it + 1) / NPART + 1);
-          __syncthreads();
+          lds_barrier();
         }
       }
       if (!late) {
@@ -393,36 +399,230 @@ __global__ __launch_bounds__(512) void conv1_fwd_x6_kernel(const void* __restric
       put(it + 1, st ^ 1);
       prefetch(it + 2);
     }
-    __syncthreads();   // partials complete; stage st ^ 1 complete
+    lds_barrier();   // partials complete; stage st ^ 1 complete
     epilogue(it);
-    __syncthreads();   // partials consumed before the next item writes them
+    lds_barrier();   // partials consumed before the next item writes them
   }
 }
 
+
+// Forward, full-K form (default; conv1_fwd tune 4 selects the K-split kernel
+// above): 10 waves, wave w = (column tile w & 1, row tile w >> 1) of the part
+// computes its 16 x 16 output tile over all 256 k (8 k-steps, one kernel row
+// each) with all 8 x 3 weight fragments resident (96 VGPRs), so no partial sums
+// cross waves: the epilogue (bias, ReLU, stores, mask bits) follows the wave's
+// own MFMAs and one barrier per part remains.  The price is the SIMD balance
+// (3, 3, 2, 2 waves): at most 5/6 of the MFMA rate.
+template <int SRC, bool MASK, int NP>
+__global__ __launch_bounds__(640) void conv1_fwd_x6w_kernel(const void* __restrict__ obs, const int64_t* __restrict__ idx,
+                                                            long long row0, int B, const float* __restrict__ mean,
+                                                            double stdv, double rstd, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, float* __restrict__ out,
+                                                            uint32_t* __restrict__ mbits, int dbg) {
+  const bool no_mma = dbg & 1, no_put = dbg & 2, no_ld = dbg & 4, no_epi = dbg & 8;
+  constexpr int NTH = 640;
+  constexpr int NPL = NP == 1 ? 1 : 3;
+  constexpr int NPW = NP == 1 ? 1 : 3;
+  __shared__ __attribute__((aligned(16))) uint16_t X[2][NPL][PLANE];
+  __shared__ __attribute__((aligned(16))) uint8_t R8[SRC == SRC_RGB ? RGBB + 16 : 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ct = wave & 1, rt = wave >> 1, i16 = lane & 15, g = lane >> 4;
+  const bool late = ((wave >> 2) & 1) != 0 && !(dbg & 16);
+  const int G = gridDim.x;
+  const int nimg = (int)blockIdx.x < B ? (B - 1 - (int)blockIdx.x) / G + 1 : 0, nit = NPART * nimg;
+  const int col = 16 * ct + i16;
+  // k-step ky: 32 k = 4 channels (lane group g) x 8 kx; B[k][n] = W[n][g][ky][j]
+  bf16x8 wf[8][3];
+#pragma unroll
+  for (int ky = 0; ky < 8; ++ky) {
+    const float* wp = w + (size_t)col * 256 + 64 * g + 8 * ky;
+    uint32_t h[8], m[8], l[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (NPW == 3) split_bf16x3(wp[j], h[j], m[j], l[j]);
+      else h[j] = bf16_rne_bits(wp[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      wf[ky][0][j] = __builtin_bit_cast(__bf16, (uint16_t)h[j]);
+      if constexpr (NPW == 3) {
+        wf[ky][1][j] = __builtin_bit_cast(__bf16, (uint16_t)m[j]);
+        wf[ky][2][j] = __builtin_bit_cast(__bf16, (uint16_t)l[j]);
+      }
+    }
+  }
+  const float bv = bias[col];
+  wait_vm0();
+
+  f32x4 xr[3];
+  auto fetch_f32 = [&](int it) __attribute__((always_inline)) {
+    if (it >= nit || no_ld) return;
+    const int k = it / NPART, p = it - NPART * k;
+    const float* base = reinterpret_cast<const float*>(obs) + obs_row(idx, row0, (int)blockIdx.x + k * G) * (4LL * IMG2) +
+                        p * 16 * IMG;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int f = tid + NTH * j;
+      if (f < 1680) {
+        const int c = f / 420, rem = f - 420 * c, yl = rem / 21, q = rem - 21 * yl;
+        xr[j] = *reinterpret_cast<const f32x4*>(base + c * IMG2 + yl * IMG + 4 * q);
+      }
+    }
+  };
+  auto put_f32 = [&](int st) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int f = tid + NTH * j;
+      if (f < 1680) {
+        const int c = f / 420, rem = f - 420 * c, yl = rem / 21, q = rem - 21 * yl;
+        uint2 o[3];
+        split4<NPL>(xr[j], o);
+        const int off = c * CSTR + yl * IMG + 4 * q;
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) *reinterpret_cast<uint2*>(&X[st][pl][off]) = o[pl];
+      }
+    }
+  };
+  uint4 fr[3];
+  auto fetch_frame = [&](int k) __attribute__((always_inline)) {
+    if (k >= nimg || no_ld) return;
+    const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(obs) +
+                                                      obs_row(idx, row0, (int)blockIdx.x + k * G) * (long long)RGBB);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int c = tid + NTH * j;
+      if (c < RGBB / 16) fr[j] = src[c];
+    }
+  };
+  auto store_frame = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int c = tid + NTH * j;
+      if (c < RGBB / 16) *reinterpret_cast<uint4*>(R8 + 16 * c) = fr[j];
+    }
+  };
+  f32x4 mA[3], mB[3];   // means of the thread's items tid, tid + 640 of the next part
+  auto fetch_means = [&](int it) __attribute__((always_inline)) {
+    if (it >= nit || mean == nullptr || no_ld) return;
+    const int p = it % NPART;
+    rgb_means(tid, p, mean, mA);
+    rgb_means(tid + NTH, p, mean, mB);
+  };
+  auto put = [&](int it, int st) __attribute__((always_inline)) {
+    if (no_put) return;
+    if constexpr (SRC == SRC_F32) {
+      put_f32(st);
+    } else {
+      const int p = it % NPART;
+      rgb_item<NPL>(tid, p, R8, mean != nullptr, mA, stdv, rstd, &X[st][0][0], CSTR, PLANE);
+      rgb_item<NPL>(tid + NTH, p, R8, mean != nullptr, mB, stdv, rstd, &X[st][0][0], CSTR, PLANE);
+    }
+  };
+  auto prefetch = [&](int it) __attribute__((always_inline)) {
+    if constexpr (SRC == SRC_F32) fetch_f32(it);
+    else fetch_means(it);
+  };
+  // the lane's A row: output pixel 16 rt + i16 of the part; k-step ky adds ky rows
+  const int px = 16 * rt + i16, oyl = px / 20, ox = px - 20 * oyl;
+  const int pix = g * CSTR + 4 * oyl * IMG + 4 * ox;
+  auto compute = [&](int it) __attribute__((always_inline)) {
+    const int st = it & 1;
+    f32x4 acc = zero4();
+    if (!no_mma) {
+#pragma unroll
+      for (int ky = 0; ky < 8; ++ky) {
+        bf16x8 a[3];
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) {
+          const uint2* p2 = reinterpret_cast<const uint2*>(&X[st][pl][pix + IMG * ky]);
+          const uint2 lo = p2[0], hi = p2[1];
+          a[pl] = __builtin_bit_cast(bf16x8, uint4{lo.x, lo.y, hi.x, hi.y});
+        }
+        acc = mma_set<NP>(a, wf[ky], acc);
+      }
+    }
+    if (no_epi) return;
+    const int k = it / NPART, p = it - NPART * k, b = (int)blockIdx.x + k * G;
+    float* o = out + ((size_t)b * 400 + 80 * p + 16 * rt) * 32 + col;
+    uint64_t bal[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = fmaxf(acc[r] + bv, 0.f);
+      o[(4 * g + r) * 32] = v;
+      if constexpr (MASK) bal[r] = __builtin_amdgcn_ballot_w64(v > 0.f);
+    }
+    if constexpr (MASK) {   // lane (g, i16) of ballot r: pixel 4 g + r, channel col; lane j < 16 stores pixel j's 16 bits
+      if (lane < 16) {
+        const int r = lane & 3, gg = lane >> 2;
+        const uint64_t bsel = r == 0 ? bal[0] : r == 1 ? bal[1] : r == 2 ? bal[2] : bal[3];
+        reinterpret_cast<uint16_t*>(mbits)[((size_t)b * 400 + 80 * p + 16 * rt + lane) * 2 + ct] =
+            (uint16_t)(bsel >> (16 * gg));
+      }
+    }
+  };
+
+  if (nit > 0) {
+    if constexpr (SRC == SRC_RGB) {
+      fetch_frame(0);
+      store_frame();
+      fetch_frame(1);
+      lds_barrier();
+    }
+    prefetch(0);
+    put(0, 0);
+    prefetch(1);
+  }
+  __syncthreads();
+  for (int it = 0; it < nit; ++it) {
+    const bool more = it + 1 < nit;
+    if constexpr (SRC == SRC_RGB) {
+      if (more && (it + 1) % NPART == 0) {
+        store_frame();
+        fetch_frame((it + 1) / NPART + 1);
+        lds_barrier();
+      }
+    }
+    if (more && !late) {
+      put(it + 1, (it + 1) & 1);
+      prefetch(it + 2);
+    }
+    compute(it);
+    if (more && late) {
+      put(it + 1, (it + 1) & 1);
+      prefetch(it + 2);
+    }
+    lds_barrier();
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Weight gradient: dW[co][(c, ky, kx)] = Σ_px dz1[px][co] · x[c][4oy+ky][4ox+kx]
 // (the backward of model.py:177 in loss.backward(), algo/ppo.py:80-81), for the
 // same two sources.  M = 32 output channels, N = 256 columns, K = pixels, on
 // v_mfma_f32_32x32x16_bf16, both operands split three ways (NP part products).
-// An image is 5 parts of 4 output rows (80 px = 5 k-steps).  Per part:
-//   S  the part's 20 input rows of all 4 channels as fp32, [c][20][88] (the row
-//      stride of 88 dwords = 24 mod 32 banks puts a fragment's four kernel rows
-//      on disjoint banks): SRC_F32 copies them from registers (one part ahead),
-//      SRC_RGB normalises them from the u8 frame in LDS — the exact decode, the
-//      grey plane transposed;
-//   D  dz of the part split once into three bf16 planes [32 co][88] (A
-//      fragments, ds_read_b128).
-// A B fragment is 8 pixels of one column (c, ky, kx): 8 stride-4 ds_read_b32
-// of S, split into the three bf16 planes by the MFMA wave itself (no expanded
-// staging copy).  16 waves: wave w takes the column tiles 2 (w & 3), +1
-// (channel w & 3, both kernel-row halves: the dz fragment feeds two tiles) and
-// the k-steps ≡ w >> 2 (mod 4) of the part sequence; the four k-group partials
-// are summed in a fixed order at the end.  Per SIMD one wave stages the next
-// part before its MFMAs and one after.  Output: the split-K slab [Z][32][256]
-// and bias partials [Z][32] (fp32 values: reduce with scale 1).
-constexpr int SRS = 88, SCH = PROWS * SRS, SPART = 4 * SCH;   // fp32 S: row / channel / part strides
-constexpr int DZS = 88, DZPL = 32 * DZS;                      // bf16 per dz plane
+// An image is 5 parts of 4 output rows (80 px = 5 k-steps).  Per part, double
+// buffered:
+//   S  the part's 20 input rows of all 4 channels, split once into the three
+//      bf16 planes [plane][c][20][96] — SRC_F32 from registers (one part ahead),
+//      SRC_RGB normalised from the u8 frame in LDS (the exact decode, the grey
+//      plane transposed);
+//   D  dz of the part split into three bf16 planes [32 co][88] (A fragments,
+//      ds_read_b128).
+// The im2col B fragment (8 pixels x 32 columns (ky, kx) of one channel) comes
+// straight from S with two ds_read_b64_tr_b16 per plane: in each 16-lane group,
+// lane 4q + p addresses pixel q's 4 consecutive kx (4 (p & 1) .. +3) of kernel
+// row 2 (lane group & 1) + (p >> 1) — 8 contiguous, 8-B aligned bytes of an
+// image row — and lane i receives column i of the 4 pixels.  No expanded copy,
+// no VALU on the image operand.  Row stride 96 (48 dwords): the four kernel rows
+// of one read sit 0 / 48 / 32 / 16 banks apart, conflict-free.
+// 16 waves: wave w takes the column tiles of channel w & 3 (both kernel-row
+// halves: one dz fragment feeds two tiles) and the k-steps ≡ w >> 2 (mod 4) of
+// the part sequence; the four k-group partials are summed in a fixed order at
+// the end.  Per SIMD one wave stages the next part before its MFMAs, one after.
+// Output: the split-K slab [Z][32][256] and bias partials [Z][32] (fp32 values:
+// reduce with scale 1).
+constexpr int SRS = 96, SCH = PROWS * SRS, SPL = 4 * SCH;   // bf16 S: row / channel / plane strides
+constexpr int DZS = 88, DZPL = 32 * DZS;                    // bf16 per dz plane
 constexpr int WMAXIMG = 512;
 
 template <int NP>
@@ -447,16 +647,6 @@ __device__ __forceinline__ f32x16 mma32_set(const bf16x8 (&a)[3], const bf16x8 (
   return c;
 }
 
-// 8 fp32 -> NPL bf16x8 planes (RNE of the remaining residual)
-template <int NPL>
-__device__ __forceinline__ void split8x(const float (&v)[8], bf16x8 (&o)[3]) {
-  uint2 q[2][3];
-  split4<NPL>(f32x4{v[0], v[1], v[2], v[3]}, q[0]);
-  split4<NPL>(f32x4{v[4], v[5], v[6], v[7]}, q[1]);
-#pragma unroll
-  for (int pl = 0; pl < NPL; ++pl) o[pl] = __builtin_bit_cast(bf16x8, uint4{q[0][pl].x, q[0][pl].y, q[1][pl].x, q[1][pl].y});
-}
-
 template <int SRC, int NP>
 __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __restrict__ dz1,
                                                               const void* __restrict__ obs,
@@ -468,7 +658,7 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
   // 4 the global loads, 16 the stagger
   const bool no_mma = dbg & 1, no_put = dbg & 2, no_ld = dbg & 4;
   constexpr int NPL = NP == 1 ? 1 : 3;
-  __shared__ __attribute__((aligned(16))) float S[2][SPART];
+  __shared__ __attribute__((aligned(16))) uint16_t S[2][3][SPL];   // 3 planes even at NPL 1: the k-group scratch
   __shared__ __attribute__((aligned(16))) uint16_t D[2][NPL][DZPL];
   __shared__ __attribute__((aligned(16))) uint8_t R8[SRC == SRC_RGB ? RGBB + 16 : 16];
   __shared__ int rowtab[WMAXIMG];
@@ -480,9 +670,11 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
   const int nimg = (int)blockIdx.x < B ? (B - 1 - (int)blockIdx.x) / G + 1 : 0;
   const int nit = NPART * nimg;
   for (int k = tid; k < nimg; k += 1024) rowtab[k] = (int)obs_row(idx, row0, (int)blockIdx.x + k * G);
-  // B column of this lane in tile t: ky = 4 t + (l32 >> 3), kx = l32 & 7; its S offset
-  // for output pixel (oyl, ox): c * SCH + (4 oyl + ky) * SRS + 4 ox + kx
-  const int bcol = wc * SCH + (l32 >> 3) * SRS + (l32 & 7);
+  // tr-read lane roles: 16-lane group lg = lane >> 4 (columns 16 (lg & 1) .., k half
+  // lg >> 1), lane 4 tq + tp of it: pixel tq of the read, kernel row
+  // 2 (lg & 1) + (tp >> 1) of the tile, kx 4 (tp & 1) .. +3
+  const int lg = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int tcol = wc * SCH + (2 * (lg & 1) + (tp >> 1)) * SRS + 4 * (tp & 1);
   const int aoff = l32 * DZS + 8 * h;   // + 16 ls
   const bool d_on = tid >= 512 && tid < 832;
   const int dit = d_on ? tid - 512 : 0, dco = dit & 31, doc = dit >> 5;
@@ -535,7 +727,7 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
   auto fetch_means = [&](int it) __attribute__((always_inline)) {
     if (it < nit && mean != nullptr && !no_ld) rgb_means(tid, it % NPART, mean, mr);
   };
-  // ---------------- put part it into stage it & 1: S rows and the dz planes
+  // ---------------- put part it into stage it & 1: S planes and the dz planes
   auto put = [&](int it) __attribute__((always_inline)) {
     if (no_put) return;
     const int st = it & 1;
@@ -545,11 +737,15 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
         const int f = tid + 1024 * j;
         if (f < 1680) {
           const int c = f / 420, rem = f - 420 * c, yl = rem / 21, q = rem - 21 * yl;
-          *reinterpret_cast<f32x4*>(&S[st][c * SCH + yl * SRS + 4 * q]) = xr[j];
+          uint2 o[3];
+          split4<NPL>(xr[j], o);
+          const int off = c * SCH + yl * SRS + 4 * q;
+#pragma unroll
+          for (int pl = 0; pl < NPL; ++pl) *reinterpret_cast<uint2*>(&S[st][pl][off]) = o[pl];
         }
       }
     } else {
-      rgb_item<0>(tid, it % NPART, R8, mean != nullptr, mr, stdv, rstd, &S[st][0], SCH, 0, SRS);
+      rgb_item<NPL>(tid, it % NPART, R8, mean != nullptr, mr, stdv, rstd, &S[st][0][0], SCH, SPL, SRS);
     }
     if (d_on) {
       Frag3 fr3;
@@ -568,6 +764,7 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
     if constexpr (SRC == SRC_RGB) fetch_means(it);
   };
 
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
   f32x16 acc[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -576,25 +773,31 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
   auto compute = [&](int it) __attribute__((always_inline)) {
     if (no_mma) return;
     const int st = it & 1;
-    // the wave's k-steps of this part: ls ≡ kg - 5 it (mod 4), at most two (kept rolled: registers)
+    // the wave's k-steps of this part: ls ≡ kg - 5 it (mod 4), at most two
     const int ls0 = (kg - 5 * it) & 3;
 #pragma unroll 1
     for (int ls = ls0; ls < 5; ls += 4) {
       bf16x8 a[3];
 #pragma unroll
       for (int pl = 0; pl < NPL; ++pl) a[pl] = *reinterpret_cast<const bf16x8*>(&D[st][pl][aoff + 16 * ls]);
-      int po[8];   // S offsets of the lane's 8 pixels 16 ls + 8 h + j (at most one output-row wrap)
-      const int px0 = 16 * ls + 8 * h, oy0 = px0 / 20, ox0 = px0 - 20 * oy0;
-      const int p0 = bcol + 4 * oy0 * SRS + 4 * ox0;
+      int ro[2];   // S offset of this lane's tr-read row: pixel 16 ls + 8 (lg >> 1) + 4 rd + tq
 #pragma unroll
-      for (int j = 0; j < 8; ++j) po[j] = p0 + 4 * j + (ox0 + j >= 20 ? 4 * SRS - 80 : 0);
+      for (int rd = 0; rd < 2; ++rd) {
+        const int px = 16 * ls + 8 * (lg >> 1) + 4 * rd + tq, oyl = px / 20, ox = px - 20 * oyl;
+        ro[rd] = tcol + 4 * oyl * SRS + 4 * ox;
+      }
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = S[st][po[j] + 4 * t * SRS];
+      for (int t = 0; t < 2; ++t) {   // kernel-row half t: ky = 4 t + (column >> 3)
         bf16x8 b[3];
-        split8x<NPL>(v, b);
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) {
+          s16x4 v[2];
+#pragma unroll
+          for (int rd = 0; rd < 2; ++rd)
+            v[rd] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(&S[st][pl][ro[rd] + 4 * t * SRS]));
+          b[pl] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7));
+        }
         acc[t] = mma32_set<NP>(a, b, acc[t]);
       }
     }
@@ -606,7 +809,7 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
       fetch_frame(0);
       store_frame();
       fetch_frame(1);
-      __syncthreads();   // frame 0
+      lds_barrier();   // frame 0
     }
     prefetch(0);
     put(0);
@@ -619,7 +822,7 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
       if (more && (it + 1) % NPART == 0) {   // part it + 1 opens a new frame: every put of this one is done
         store_frame();
         fetch_frame((it + 1) / NPART + 1);
-        __syncthreads();
+        lds_barrier();
       }
     }
     if (more && !late) {
@@ -631,11 +834,11 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
       put(it + 1);
       prefetch(it + 2);
     }
-    __syncthreads();
+    lds_barrier();
   }
   // k-group partials -> (k0 + k2) + (k1 + k3) in three rounds through one 32-KB
   // slot of the S space (free now): k1 += k3; k0 += k2; k0 += k1
-  float* X = &S[0][0];
+  float* X = reinterpret_cast<float*>(&S[0][0][0]);
   static_assert(sizeof(S) >= 4 * 2 * 16 * 64 * 4, "k-group scratch");
   auto xo = [&](int t, int r) { return ((wc * 2 + t) * 16 + r) * 64 + lane; };
   auto round = [&](int src, int dst) __attribute__((always_inline)) {
@@ -699,11 +902,18 @@ static int conv1_fwd_x6_launch(int src, const void* obs, const int64_t* idx, lon
   const bool prof = ppo_prof_begin(src == SRC_F32 ? "conv1_fwd_f32" : "conv1_fwd_rgb", st, &slot);
   const double rs = 1.0 / stdv;
   const int dbg = ppo_tune_get("stagger") >> 4;   // timing anatomy (kbench --tune stagger=16*dbg)
+  // kernel form: fp32 rows take the full-K 10-wave kernel (3.3 vs 3.9 ms per 65,536-image
+  // minibatch); RGB frames the K-split 8-wave one (5.8-5.9 vs 6.5 ms: the full-K form's
+  // 96 weight VGPRs plus the decode's means spill there).  conv1_fwd tune 4 / 5 forces
+  // the K-split / full-K form (A/B)
+  const int tv = ppo_tune_get("conv1_fwd");
+  const bool ksplit = tv == 4 || (tv != 5 && src == SRC_RGB);
 #define L1(S, M, N)                                                                                           \
-  conv1_fwd_x6_kernel<S, M, N><<<nb, 512, 0, st>>>(obs, idx, row0, B, mean, stdv, rs, w1, b1, out, mbits, dbg)
+  if (ksplit) conv1_fwd_x6_kernel<S, M, N><<<nb, 512, 0, st>>>(obs, idx, row0, B, mean, stdv, rs, w1, b1, out, mbits, dbg); \
+  else conv1_fwd_x6w_kernel<S, M, N><<<nb, 640, 0, st>>>(obs, idx, row0, B, mean, stdv, rs, w1, b1, out, mbits, dbg)
 #define L2(S, N)         \
-  if (mbits) L1(S, true, N); \
-  else L1(S, false, N)
+  if (mbits) { L1(S, true, N); } \
+  else { L1(S, false, N); }
 #define L3(S)                      \
   if (np == 1) { L2(S, 1); }        \
   else if (np == 9) { L2(S, 9); }   \
