@@ -1981,6 +1981,8 @@ static inline void set_planes(P& p, const float* seg, long long n, int rows, int
 
 static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
                           const float* w1, const float* b1, float* out, uint16_t* mbits, void* stream);
+int conv1_wgrad_u8_tr(const float* dz1, const uint8_t* obs, const int64_t* idx, long long row0, int B, int Z,
+                      float* slab, float* slab_bias, void* stream);   // conv1f.hip
 
 // conv1 forward: out [B][20][20][32] = relu(conv(obs rows, W1 torch layout) + b1)
 PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
@@ -2416,6 +2418,8 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
   }
   if (!obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] != 9 && ((uintptr_t)obs & 15) == 0)   // conv1f.hip
     return ppo_conv1_wgrad_f32(dz1, (const float*)obs, idx, row0, B, Z, slab, slab_bias, stream);
+  if (obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] == 6)   // conv1f.hip, tr_b16 im2col (A/B)
+    return conv1_wgrad_u8_tr(dz1, (const uint8_t*)obs, idx, row0, B, Z, slab, slab_bias, stream);
   if (obs_is_u8) {
     if (g_tune[TK_CONV1_WGRAD] == 9) {
       Conv1Wgrad<uint8_t, CfgW32n> p;

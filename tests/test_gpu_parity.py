@@ -1291,7 +1291,7 @@ def test_gru_persistent_sequence_equals_steps(gpu, T, n, H, use_idx):
                                                       (outs[0][k] != outs[1][k]).sum().item())
 
 
-@pytest.mark.parametrize("variant", [3, 4, 5, 9])
+@pytest.mark.parametrize("variant", [3, 4, 5, 6, 9])
 def test_conv1_wgrad_variants_vs_torch(gpu, variant):
     """conv1 weight + bias gradient from u8 observations gathered by index (the
     minibatch path): the part-pipelined bf16x3 kernel with 8 (3) and 16

@@ -88,11 +88,9 @@ def test_half_minibatch_gradient_vs_float64(gpu, obs_dtype):
     # rounding flips a clip decision: the fp32 error of every implementation here
     # is input-dependent at the 1e-5 level (torch's own ranges 2e-6 .. 1e-4 across
     # builds of the same inputs), so the ratio test gets a 2e-5 floor.
-    if obs_dtype == torch.uint8:
-        check_grads(cap32.grad.cpu().numpy(), grads, O.cnn_param_shapes(H), fp32_flat=g32, floor=2e-5)
-    else:   # float observations take conv1's fp32-MFMA tile path (not the exact u8 one)
-        check_grads(cap32.grad.cpu().numpy(), grads, O.cnn_param_shapes(H), fp32_flat=g32, fro_tol=1e-4,
-                    max_tol=2e-4, ratio=3.0, floor=5e-5)
+    # float observations (the fp16 plane widened to fp32 rows) take conv1's
+    # image-resident split kernels (csrc/conv1f.hip): the same bar as u8 frames
+    check_grads(cap32.grad.cpu().numpy(), grads, O.cnn_param_shapes(H), fp32_flat=g32, floor=2e-5)
 
 
 def test_half_precision_run_py_flow(gpu):
