@@ -103,6 +103,12 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// workgroup barrier that publishes LDS writes (lgkmcnt(0)) but leaves global loads
+// in flight: __syncthreads' fence would wait for every outstanding load (vmcnt(0)),
+// i.e. for the register prefetch of the next items; the compiler still waits for
+// those loads where their registers are used
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Range-checked buffer stores: a store whose byte offset is out of the
 // resource's range (e.g. -1) is dropped by the hardware — predication without an
 // exec-mask branch.  dword3 0x00020000: raw 32-bit buffer on gfx9 (gfx950).

@@ -75,11 +75,6 @@ __device__ __forceinline__ float gray3(float r, float g, float b, bool u8) {
   return u8 ? (float)(uint8_t)v : v;
 }
 
-// workgroup barrier that publishes LDS writes (lgkmcnt(0)) but leaves global loads
-// in flight: __syncthreads' fence would wait for every outstanding load (vmcnt(0)),
-// i.e. for the register prefetch of the next items; the compiler still waits for
-// those loads where their registers are used
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // 4 fp32 -> the three bf16 planes' 4-element pieces (uint2 each), each part the
 // RNE of the remaining residual (v_cvt_pk_bf16_f32); NPL 1: hi only

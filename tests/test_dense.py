@@ -1,0 +1,97 @@
+"""CNNBase fc GEMMs (GPU): the 32x32x16 LDS-DMA kernel of csrc/dense_x32.h
+(ppo_tune_set("fc_fwd" / "fc_dgrad", 6)) and the generic tile core, through the
+C ABI, vs torch float64 — the fc forward (model.py:181, Linear(32*7*7, H) + ReLU)
+and its input gradient masked by conv3's ReLU (threshold_backward of the
+flatten/ReLU in CNNBase.main).  Bar: 1e-5 of max|ref| with the fp32-accurate
+split (6 / 9 products), bf16-operand rounding (2e-2) in half-precision mode (1)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _hip():
+    from a2c_ppo_acktr import _hip
+    return _hip
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _packed(gpu, H, seed):
+    H_ = _hip()
+    g = torch.Generator().manual_seed(seed)
+    w2 = torch.randn(64, 32, 4, 4, generator=g) * 0.05
+    w3 = torch.randn(32, 64, 3, 3, generator=g) * 0.05
+    w4 = torch.randn(H, 1568, generator=g) * 0.03
+    packed = torch.empty(H_.call("ppo_packed_weights_size", H), device=gpu)
+    offs = torch.zeros(6, dtype=torch.int64)
+    H_.call("ppo_packed_offsets", H, offs.data_ptr())
+    d = [t.cuda() for t in (w2, w3, w4)]
+    H_.call("ppo_pack_weights", d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), H, packed.data_ptr(), _s())
+    pk = [packed.data_ptr() + 4 * int(o) for o in offs]
+    # the packed fc weight's columns follow the engine's HWC activation layout
+    # ([B][7][7][32]); torch's flatten is CHW
+    return w4.view(H, 32, 7, 7).permute(0, 2, 3, 1).reshape(H, 1568), packed, pk
+
+
+def _with_tune(key, value, products, fn):
+    H_ = _hip()
+    old, oldp = H_.call("ppo_tune_get", key), H_.call("ppo_tune_get", b"products")
+    H_.call("ppo_tune_set", key, value)
+    H_.call("ppo_tune_set", b"products", products)
+    try:
+        fn()
+        torch.cuda.synchronize()
+    finally:
+        H_.call("ppo_tune_set", key, old)
+        H_.call("ppo_tune_set", b"products", oldp)
+
+
+@pytest.mark.parametrize("variant", [0, 6, 7])
+@pytest.mark.parametrize("products", [6, 9, 1])
+@pytest.mark.parametrize("B,H", [(300, 512), (77, 64), (129, 256)])
+def test_fc_fwd_vs_float64(gpu, variant, products, B, H):
+    """relu(x W^T + b) with B not a multiple of the 128-row tile and H = 64 (waves
+    without weight rows), written into a wider output (ldo = H + 8)."""
+    H_ = _hip()
+    w4, packed, pk = _packed(gpu, H, 3 + H)
+    g = torch.Generator().manual_seed(B)
+    x = torch.relu(torch.randn(B, 1568, generator=g))
+    b = torch.randn(H, generator=g) * 0.1
+    ldo = H + 8
+    out = torch.full((B, ldo), float("nan"), device=gpu)
+    xd, bd = x.cuda(), b.cuda()
+    _with_tune(b"fc_fwd", variant, products,
+               lambda: H_.call("ppo_fc_fwd", xd.data_ptr(), B, pk[2], bd.data_ptr(), H, out.data_ptr(), ldo, _s()))
+    ref = torch.relu(x.double() @ w4.double().t() + b.double())
+    got = out[:, :H].cpu().double()
+    tol = 1e-5 if products != 1 else 2e-2
+    err = (got - ref).abs().max().item()
+    assert err <= tol * ref.abs().max().item(), err
+    assert torch.isnan(out[:, H:]).all()   # the padding columns are untouched
+
+
+@pytest.mark.parametrize("variant", [0, 6, 7])
+@pytest.mark.parametrize("products", [6, 9, 1])
+@pytest.mark.parametrize("B,H", [(300, 512), (77, 64)])
+def test_fc_dgrad_mask_vs_float64(gpu, variant, products, B, H):
+    """dx = [a3 > 0] * (dh W): N = 1568 = 6 full 256-row weight blocks + 32 rows."""
+    H_ = _hip()
+    w4, packed, pk = _packed(gpu, H, 5 + H)
+    g = torch.Generator().manual_seed(B + 1)
+    dh = torch.randn(B, H, generator=g)
+    a3 = torch.relu(torch.randn(B, 1568, generator=g))
+    dx = torch.full((B, 1568), float("nan"), device=gpu)
+    dhd, a3d = dh.cuda(), a3.cuda()
+    _with_tune(b"fc_dgrad", variant, products,
+               lambda: H_.call("ppo_linear_dgrad_mask", dhd.data_ptr(), B, H, pk[3], 1568, a3d.data_ptr(),
+                               dx.data_ptr(), _s()))
+    ref = (dh.double() @ w4.double()) * (a3 > 0).double()
+    got = dx.cpu().double()
+    tol = 1e-5 if products != 1 else 2e-2
+    err = (got - ref).abs().max().item()
+    assert err <= tol * ref.abs().max().item(), err
+    assert (got[a3 <= 0] == 0).all()
