@@ -277,6 +277,17 @@ int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float* save_z,
                     const float* save_ghn, const float* save_hin, const float* masks, const int64_t* idx,
                     const float* whhT, int T, int n, int H, float* dgi, float* dgh, float* dhz, float* carry,
                     void* stream);
+/* ppo_gru_seq_bwd with caller-owned synchronisation words (as ppo_gru_seq_fwd_ws):
+ * T > 1 runs step T-1's cell backward, then steps T-1 .. 1 as ONE persistent
+ * launch (gru_seq_bwd16_kernel: W_hh^T slices resident, row groups hand dgh over
+ * through write-through stores and counters; bounded waits set *err, sticky, and
+ * ppo_clip_adam_guarded skips the optimizer step while it is set).  Results equal
+ * the per-step launches (ppo_gru_persist_set(0)) bit for bit.  Replaces the BPTT of
+ * torch.nn.GRU's autograd over T/a2c_ppo_acktr/model.py:116-165. */
+int ppo_gru_seq_bwd_ws(const float* dout, const float* save_r, const float* save_z, const float* save_n,
+                       const float* save_ghn, const float* save_hin, const float* masks, const int64_t* idx,
+                       const float* whhT, int T, int n, int H, float* dgi, float* dgh, float* dhz, float* carry,
+                       int* counters, int* err, void* stream);
 int ppo_gru_step_bwd_cell(const float* dgh, const float* whhT, float* dhz, const float* masks,
                           const int64_t* mask_idx, float* carry, int M, int H, const float* dout_prev,
                           const float* r, const float* z, const float* n, const float* ghn, const float* hin,

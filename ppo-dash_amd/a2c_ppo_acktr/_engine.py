@@ -534,9 +534,10 @@ class RecurrentEngine(CNNEngine):
         dgh = ws.get("dgh", R * 3 * H, device=dev)
         dhz = ws.get("dhz", n * H, device=dev)
         carry = ws.get("carry", n * H, device=dev)
-        call("ppo_gru_seq_bwd", dout.data_ptr(), sv["r"].data_ptr(), sv["z"].data_ptr(), sv["n"].data_ptr(),
+        # persistent BPTT on the same counters (the forward has finished on this stream) and error word
+        call("ppo_gru_seq_bwd_ws", dout.data_ptr(), sv["r"].data_ptr(), sv["z"].data_ptr(), sv["n"].data_ptr(),
              sv["ghn"].data_ptr(), sv["hin"].data_ptr(), masks.data_ptr(), idx.data_ptr(), self.whhT, T, n, H,
-             dgi.data_ptr(), dgh.data_ptr(), dhz.data_ptr(), carry.data_ptr(), s)
+             dgi.data_ptr(), dgh.data_ptr(), dhz.data_ptr(), carry.data_ptr(), cnt.data_ptr(), self.status_ptr(0), s)
         self._dense_wgrad(dgh, sv["hin"], R, 3 * H, H, 0, 0, self.GHH, self.GBH)
         self._dense_wgrad(dgi, x, R, 3 * H, self.Ip, 3, self.I, self.GIH, self.GBI)
         dh = ws.get("dh", R * H, device=dev)

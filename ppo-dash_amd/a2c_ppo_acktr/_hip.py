@@ -94,6 +94,8 @@ SIGNATURES = {
     "ppo_gru_seq_fwd_ws": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                            c_p],
     "ppo_gru_seq_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p],
+    "ppo_gru_seq_bwd_ws": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_p,
+                           c_p, c_p],
     "ppo_gru_step_bwd_cell": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "ppo_gru_pack": [c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p],
     "ppo_concat_cols": [c_p, c_p, c_ll, c_int, c_p, c_int, c_int, c_int, c_p],

@@ -7,8 +7,8 @@
 // Weights are the MFMA A operand (rows n, the pre-split bf16 planes of
 // ppo_pack_weights), activations the B operand (columns m, fp32, split into
 // hi / mid / lo at fragment-read time): the accumulator lane then holds four
-// consecutive n of one m.  Block tile 256 n x 128 m, 8 waves of 64 x 64 (2 x 2
-// tiles of 32 x 32, 64 accumulator VGPRs), BK 32, two LDS stages of 64 KB
+// consecutive n of one m.  Block tile 256 n x 128 m, 8 waves of 128 n x 32 m (4
+// tiles of 32 x 32, 64 accumulator VGPRs: each split activation fragment feeds 4 x NP MFMAs), BK 32, two LDS stages of 64 KB
 // filled by LDS-DMA (global_load_lds_dwordx4: no staging registers, no VALU,
 // no ds_write) — the generic tile core (igemm_x9.h) stages through registers,
 // splits with every wave and holds 128 x 128 tiles, so the fc input was read 4x.
@@ -38,7 +38,7 @@ struct DenseX32Args {
   const float* bias;                    // DX_BIAS_RELU: out = relu(v + bias[n])
   const float* act; long long ldact;    // DX_MASK: out = act[m][n] > 0 ? v : 0
   int M, N, K, mblocks;
-  int dbg;   // timing anatomy only (wrong results): 4 no epilogue, 8 no DMA
+  int dbg;   // timing anatomy only (wrong results): 4 no epilogue, 8 no DMA, 16 all blocks on tile 0
 };
 
 constexpr int DX_BN = 256, DX_BM = 128;
@@ -64,12 +64,12 @@ __global__ __launch_bounds__(512) void dense_x32_kernel(const DenseX32Args a) {
   static_assert(NS * STG * 16 <= 131072 && WBLK >= 1 && XBLK >= 1, "dense_x32 stages");
   __shared__ __attribute__((aligned(16))) uint4 L[NS * STG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
-  const int wn = wave & 3, wm = wave >> 2;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int wn = wave & 1, wm = wave >> 1;   // 128 weight rows x 32 activation rows per wave
+  const int tile = (a.dbg & 16) ? 0 : xcd_remap(blockIdx.x, gridDim.x);   // dbg 16: every block on tile 0 (L2-resident operands)
   const int nb = tile / a.mblocks, mb = tile - nb * a.mblocks;
   const int n0 = nb * DX_BN, m0 = mb * DX_BM;
   const int nk = a.K / BK;
-  const bool wactive = n0 + 64 * wn < a.N;   // wave-uniform: the wave's weight rows exist
+  const bool wactive = n0 + 128 * wn < a.N;   // wave-uniform: the wave's weight rows exist
 
   // DMA of k-step kt into stage st: per wave 2 x NPL weight blocks + 2 activation
   // blocks of 64 slots (rows past N / M re-read the last row; never stored)
@@ -97,43 +97,40 @@ __global__ __launch_bounds__(512) void dense_x32_kernel(const DenseX32Args a) {
     }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[4];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
-  // one k-sub (16 k) of fragments: weights 2 tiles x NPL planes, activations 2
-  // tiles split into hi / mid / lo
+  // one k-sub (16 k) of fragments: weights 4 tiles x NPL planes, the activation
+  // tile split into hi / mid / lo (each split feeds 4 x NP MFMAs)
   struct Frags {
-    bf16x8 w[2][3];
-    Frag3 x[2];
+    bf16x8 w[4][3];
+    Frag3 x;
   };
   auto load = [&](int kt, int kk, Frags& f) __attribute__((always_inline)) {
     const uint4* S = L + (kt % NS) * STG;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int o = dx_slot<WQ>(64 * wn + 32 * t + l32, 2 * kk + hh);
+    for (int t = 0; t < 4; ++t) {
+      const int o = dx_slot<WQ>(128 * wn + 32 * t + l32, 2 * kk + hh);
 #pragma unroll
       for (int p = 0; p < NPL; ++p) f.w[t][p] = __builtin_bit_cast(bf16x8, S[p * WPL + o]);
     }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int row = 64 * wm + 32 * u + l32, c = 4 * kk + 2 * hh;
+    {
+      const int row = 32 * wm + l32, c = 4 * kk + 2 * hh;
       const f32x4 x0 = __builtin_bit_cast(f32x4, S[3 * WPL + dx_slot<XQ>(row, c)]);
       const f32x4 x1 = __builtin_bit_cast(f32x4, S[3 * WPL + dx_slot<XQ>(row, c + 1)]);
-      split8(x0, x1, f.x[u], NP == 1);
+      split8(x0, x1, f.x, NP == 1);
     }
   };
   auto mma = [&](const Frags& f) __attribute__((always_inline)) {
 #define PPO_PL_h 0
 #define PPO_PL_m 1
 #define PPO_PL_l 2
-#define PPO_PART(X, Y)                                                                                        \
-  _Pragma("unroll") for (int t = 0; t < 2; ++t) _Pragma("unroll") for (int u = 0; u < 2; ++u) acc[t][u] = \
-      __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.w[t][PPO_PL_##Y], f.x[u].X, acc[t][u], 0, 0, 0);
+#define PPO_PART(X, Y)                                 \
+  _Pragma("unroll") for (int t = 0; t < 4; ++t) acc[t] = \
+      __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.w[t][PPO_PL_##Y], f.x.X, acc[t], 0, 0, 0);
     PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
 #undef PPO_PL_h
@@ -146,8 +143,8 @@ __global__ __launch_bounds__(512) void dense_x32_kernel(const DenseX32Args a) {
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-      if (i < 2 * NPL + 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 LDS read
-      __builtin_amdgcn_sched_group_barrier(0x002, NP == 1 ? 8 : 3, 0);   // VALU (split)
+      if (i < 4 * NPL + 2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 LDS read
+      __builtin_amdgcn_sched_group_barrier(0x002, NP == 1 ? 6 : 2, 0);   // VALU (split)
     }
   };
 
@@ -169,73 +166,93 @@ __global__ __launch_bounds__(512) void dense_x32_kernel(const DenseX32Args a) {
 #undef PPO_VMCNT
   int issued = -1;
   for (int j = 0; j < NS && j < nk; ++j) dma(issued = j);
+  // PIPE: the next k-sub's fragments are read and split while this one's MFMAs
+  // run (two fragment sets); otherwise one set, the two waves of a SIMD overlap
+  // each other's split with their MFMAs
+  constexpr bool PIPE = false;
   Frags fa, fb;
-  if (nk > 0) {
-    wait_landed(0, issued);
-    load(0, 0, fa);
+  if constexpr (PIPE) {
+    if (nk > 0) {
+      wait_landed(0, issued);
+      load(0, 0, fa);
+    }
   }
   const int nsub = nk * KSUB;
-  // k-sub i: k-step i / KSUB.  Unrolled by two (fa / fb alternate).
   for (int i = 0; i < nsub; i += 2) {
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
       const int ii = i + h2;
       if (ii >= nsub) break;
-      Frags& cur = h2 == 0 ? fa : fb;
-      Frags& nxt = h2 == 0 ? fb : fa;
-      const int nx = ii + 1;
-      if (nx < nsub) {
-        const int kt = nx / KSUB, kk = nx - KSUB * kt;
-        if (kk == 0) {   // k-step kt opens: it must have landed; the slot of kt - 1 is free after the barrier
+      if constexpr (PIPE) {
+        Frags& cur = h2 == 0 ? fa : fb;
+        Frags& nxt = h2 == 0 ? fb : fa;
+        const int nx = ii + 1;
+        if (nx < nsub) {
+          const int kt = nx / KSUB, kk = nx - KSUB * kt;
+          if (kk == 0) {   // k-step kt opens: it must have landed; the slot of kt - 1 is free after the barrier
+            wait_landed(kt, issued);
+            if (kt + NS - 1 < nk && kt + NS - 1 > issued) dma(issued = kt + NS - 1);
+          }
+          if (wactive) {   // one basic block: the scheduler interleaves the two
+            load(kt, kk, nxt);
+            mma(cur);
+            interleave();
+          }
+        } else if (wactive) {
+          mma(cur);
+        }
+      } else {
+        const int kt = ii / KSUB, kk = ii - KSUB * kt;
+        if (kk == 0) {
           wait_landed(kt, issued);
           if (kt + NS - 1 < nk && kt + NS - 1 > issued) dma(issued = kt + NS - 1);
         }
-        if (wactive) {   // one basic block: the scheduler interleaves the two
-          load(kt, kk, nxt);
-          mma(cur);
-          interleave();
+        if (wactive) {
+          load(kt, kk, fa);
+          mma(fa);
         }
-      } else if (wactive) {
-        mma(cur);
       }
     }
   }
-  __syncthreads();   // the stages are free: the output tile goes through them
-
-  // output tile [128 m][256 n] fp32, 16-B unit c of row m at c ^ (m & 63)
+  // Epilogue: the output tile [128 m][256 n] fp32 goes through the (free) stages in
+  // chunks of CH rows (1 KB each), 16-B unit c of row m at c ^ (m & 63); every
+  // wave-instruction then stores one whole 1-KB row.
+  constexpr int CH = NS * STG / 64 < DX_BM ? NS * STG / 64 : DX_BM;
+  static_assert(DX_BM % CH == 0 && CH % 32 == 0, "epilogue chunks");
   uint4* T = L;
-  if (wactive) {
+#pragma unroll 1
+  for (int c0 = 0; c0 < DX_BM; c0 += CH) {
+    __syncthreads();   // the stages (or the previous chunk) are free
+    const int m = 32 * wm + l32 - c0;
+    if (wactive && m >= 0 && m < CH) {   // wave-uniform (32-row waves, chunks of 32k rows)
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int m = 64 * wm + 32 * u + l32;
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int c = (64 * wn + 32 * t + 8 * j + 4 * hh) >> 2;
+          const int c = (128 * wn + 32 * t + 8 * j + 4 * hh) >> 2;
           T[64 * m + (c ^ (m & 63))] = __builtin_bit_cast(
-              uint4, f32x4{acc[t][u][4 * j], acc[t][u][4 * j + 1], acc[t][u][4 * j + 2], acc[t][u][4 * j + 3]});
+              uint4, f32x4{acc[t][4 * j], acc[t][4 * j + 1], acc[t][4 * j + 2], acc[t][4 * j + 3]});
         }
-      }
-  }
-  __syncthreads();
-#pragma unroll 4
-  for (int i = 0; i < 16; ++i) {   // wave-instruction: one 1-KB row
-    const int g = tid + 512 * i, m = g >> 6, c = g & 63;
-    const int mg = m0 + m, n = n0 + 4 * c;
-    if (mg >= a.M || n >= a.N || (a.dbg & 4)) continue;
-    const f32x4 v = __builtin_bit_cast(f32x4, T[64 * m + (c ^ (m & 63))]);
-    f32x4 y;
-    if constexpr (EPI == DX_BIAS_RELU) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(a.bias + n);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + b[r], 0.f);
-    } else {
-      const f32x4 g4 = *reinterpret_cast<const f32x4*>(a.act + (long long)mg * a.ldact + n);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) y[r] = g4[r] > 0.f ? v[r] : 0.f;
     }
-    *reinterpret_cast<f32x4*>(a.out + (long long)mg * a.ldo + n) = y;
+    __syncthreads();
+#pragma unroll 4
+    for (int i = 0; i < CH / 8; ++i) {   // wave-instruction: one 1-KB row
+      const int g = tid + 512 * i, mr = g >> 6, c = g & 63;
+      const int mg = m0 + c0 + mr, n = n0 + 4 * c;
+      if (mg >= a.M || n >= a.N || (a.dbg & 4)) continue;
+      const f32x4 v = __builtin_bit_cast(f32x4, T[64 * mr + (c ^ (mr & 63))]);
+      f32x4 y;
+      if constexpr (EPI == DX_BIAS_RELU) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(a.bias + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + b[r], 0.f);
+      } else {
+        const f32x4 g4 = *reinterpret_cast<const f32x4*>(a.act + (long long)mg * a.ldact + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[r] = g4[r] > 0.f ? v[r] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(a.out + (long long)mg * a.ldo + n) = y;
+    }
   }
 }
 
@@ -248,15 +265,17 @@ static int dense_x32_launch(DenseX32Args a, hipStream_t st, const char* name, in
   PPO_REQUIRE(((uintptr_t)a.x & 15) == 0 && ((uintptr_t)a.out & 15) == 0 && ((uintptr_t)a.wpl & 15) == 0,
               "%s: operands must be 16-B aligned", name);
   a.mblocks = (a.M + DX_BM - 1) / DX_BM;
-  a.dbg = (g_stagger >> 9) & 15;
+  a.dbg = (g_stagger >> 9) & 31;
   const long long nblk = (long long)a.mblocks * ((a.N + DX_BN - 1) / DX_BN);
   PPO_REQUIRE(nblk < 0x7fffffffLL, "%s: grid too large (M=%d)", name, a.M);
   int slot;
   const bool prof = ppo_prof_begin(name, st, &slot);
-  // shape 0: BK 32 x 2 stages; 1: BK 16 x 4 stages
-#define PPO_DX(NP_)                                                                           \
-  (shape == 1 ? dense_x32_kernel<NP_, EPI, 16, 4><<<(unsigned)nblk, 512, 0, st>>>(a)          \
-              : dense_x32_kernel<NP_, EPI, 32, 2><<<(unsigned)nblk, 512, 0, st>>>(a))
+  // shape 0: BK 32 x 2 stages (128 KB); 1: BK 16 x 4 stages (128 KB); 2: BK 16 x 2
+  // stages (64 KB: two blocks per CU)
+#define PPO_DX(NP_)                                                                                 \
+  (shape == 1   ? dense_x32_kernel<NP_, EPI, 16, 4><<<(unsigned)nblk, 512, 0, st>>>(a)              \
+   : shape == 2 ? dense_x32_kernel<NP_, EPI, 16, 2><<<(unsigned)nblk, 512, 0, st>>>(a)              \
+                : dense_x32_kernel<NP_, EPI, 32, 2><<<(unsigned)nblk, 512, 0, st>>>(a))
   if (g_products == 9) PPO_DX(9);
   else if (g_products == 1) PPO_DX(1);
   else PPO_DX(6);

@@ -2379,7 +2379,7 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
   PPO_REQUIRE(H > 0 && H % 8 == 0 && ldo >= H, "ppo_fc_fwd: H=%d ldo=%d", H, ldo);
   const int K = 1568;
   if (M > 0 && M <= g_small_b) return small_linear_fwd(x, nullptr, M, K, K, w4p, b, H, out, ldo, 1, as_stream(stream));
-  if (use_x9() && (g_tune[TK_FC_FWD] == 6 || g_tune[TK_FC_FWD] == 7) && ldo % 4 == 0) {   // dense_x32.h
+  if (use_x9() && (g_tune[TK_FC_FWD] >= 6 && g_tune[TK_FC_FWD] <= 8) && ldo % 4 == 0) {   // dense_x32.h
     DenseX32Args a{};
     a.wpl = planes_of(w4p, (long long)H * K); a.wps = (long long)H * K;
     a.x = x; a.ldx = K; a.out = out; a.ldo = ldo; a.bias = b; a.M = M; a.N = H; a.K = K;
@@ -2498,7 +2498,7 @@ PPO_API int ppo_transpose(const float* src, int rows, int cols, float* dst, void
 PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
                                   void* stream) {
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 4", K);
-  if (use_x9() && (g_tune[TK_FC_DGRAD] == 6 || g_tune[TK_FC_DGRAD] == 7) && K % 32 == 0 && N % 4 == 0) {
+  if (use_x9() && (g_tune[TK_FC_DGRAD] >= 6 && g_tune[TK_FC_DGRAD] <= 8) && K % 32 == 0 && N % 4 == 0) {
     DenseX32Args a{};
     a.wpl = planes_of(wt, (long long)N * K); a.wps = (long long)N * K;
     a.x = dy; a.ldx = K; a.out = dx; a.ldo = N; a.act = act; a.ldact = N; a.M = M; a.N = N; a.K = K;

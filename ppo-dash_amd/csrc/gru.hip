@@ -112,22 +112,40 @@ struct GruBwdStep : C_ {
 //   dn = dh'(1-z), dz = dh'(h_in - n), da_n = dn(1-n²), dr = da_n·ghn,
 //   da_r = dr·r(1-r), da_z = dz·z(1-z);  dgi = [da_r, da_z, da_n],
 //   dgh = [da_r, da_z, da_n·r];  dhz = dh'·z
-__device__ __forceinline__ void gru_cell_bwd_elem(float dh, float rr, float zz, float nn, float ghn, float hin,
-                                                  size_t i, size_t g, int H, float* __restrict__ dgi,
-                                                  float* __restrict__ dgh, float* __restrict__ dhz) {
+// (dgh·W_hh + dh'·z)·m(t), rounded as written
+__device__ __forceinline__ float gru_carry(float v, float dhz, float m) {
+#pragma clang fp contract(off)
+  return (v + dhz) * m;
+}
+
+// explicitly rounded (no FMA contraction): the same bits in every kernel that
+// inlines it (step launches, fused step + cell, persistent BPTT)
+struct GruCellGrad {
+  float dar, daz, dan, dghn, dhz;
+};
+__device__ __forceinline__ GruCellGrad gru_cell_grad(float dh, float rr, float zz, float nn, float ghn, float hin) {
+#pragma clang fp contract(off)
+  // plain operators under the pragma (HIP's __fmul_rn & co. are plain operators
+  // compiled outside it, so they would still contract)
   const float dn = dh * (1.0f - zz);
   const float dz = dh * (hin - nn);
   const float dan = dn * (1.0f - nn * nn);
   const float dr = dan * ghn;
   const float dar = dr * rr * (1.0f - rr);
   const float daz = dz * zz * (1.0f - zz);
-  dgi[g] = dar;
-  dgi[g + H] = daz;
-  dgi[g + 2 * H] = dan;
-  dgh[g] = dar;
-  dgh[g + H] = daz;
-  dgh[g + 2 * H] = dan * rr;
-  dhz[i] = dh * zz;
+  return {dar, daz, dan, dan * rr, dh * zz};
+}
+__device__ __forceinline__ void gru_cell_bwd_elem(float dh, float rr, float zz, float nn, float ghn, float hin,
+                                                  size_t i, size_t g, int H, float* __restrict__ dgi,
+                                                  float* __restrict__ dgh, float* __restrict__ dhz) {
+  const GruCellGrad c = gru_cell_grad(dh, rr, zz, nn, ghn, hin);
+  dgi[g] = c.dar;
+  dgi[g + H] = c.daz;
+  dgi[g + 2 * H] = c.dan;
+  dgh[g] = c.dar;
+  dgh[g + H] = c.daz;
+  dgh[g + 2 * H] = c.dghn;
+  dhz[i] = c.dhz;
 }
 
 __global__ __launch_bounds__(256) void gru_cell_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ carry,
@@ -484,7 +502,7 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
     const int rt = ml >> 4, ir = ml & 15, ln = jl + 16 * (ir >> 2), rg = ir & 3;
     const float v = ((P[0][rt][ln][rg] + P[1][rt][ln][rg]) + P[2][rt][ln][rg]) + P[3][rt][ln][rg];
     const size_t o = (size_t)m * H + j;
-    const float cv = (v + pd[e]) * pm[e];
+    const float cv = gru_carry(v, pd[e], pm[e]);
     carry[o] = cv;
     if (cp.dout)   // the previous step's cell backward for this element (gru_cell_bwd_kernel, fused)
       gru_cell_bwd_elem(pc[e][0] + cv, pc[e][1], pc[e][2], pc[e][3], pc[e][4], pc[e][5], o,
@@ -492,10 +510,147 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
   }
 }
 
+// Persistent backward through time (model.py:116-165 reversed): the blocks of
+// gru_step_bwd16_kernel stay resident for steps T-1 .. 1, each with its W_hhᵀ
+// slice in registers (loaded once).  Step t of row group x needs dgh(t) of its 32
+// rows over all 3H columns, written by all H/16 unit blocks of the group in the
+// previous iteration (the cell backward of step t fused into step t+1's epilogue;
+// step T-1's by the ppo_gru_cell_bwd launch before this kernel): the same R1
+// hand-off as gru_seq16_kernel — dgh(t-1) stored write-through (sc1), drained,
+// one relaxed counter increment of the group; dgh loaded with sc1 loads; bounded,
+// fail-safe waits on the shared error word.  The per-element arithmetic, the
+// K-quarter / K-half order and the MFMA sequence are those of the step kernel, so
+// the results equal the T - 1 step launches bit for bit.
+template <int H>
+__global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
+    const float* __restrict__ dout, const float* __restrict__ sr, const float* __restrict__ sz,
+    const float* __restrict__ sn, const float* __restrict__ sghn, const float* __restrict__ shin,
+    const float* __restrict__ masks, const int64_t* __restrict__ idx, const float* __restrict__ whhT, int T, int n,
+    float* __restrict__ dgi, float* __restrict__ dgh, float* __restrict__ dhz, float* __restrict__ carry,
+    int* __restrict__ cnt, int* __restrict__ err, int spin_max) {
+  constexpr int KW = 3 * H / 16;
+  constexpr int NH = KW % 8 == 0 ? 2 : 1, KH = KW / NH;
+  __shared__ f32x4 P[4][2][64];
+  __shared__ int s_abort;
+  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
+  const int grp = blockIdx.x, m0 = grp * 32, j0 = blockIdx.y * 16, need = H / 16;
+  const int k0 = q * 4 * KW + g * KW;
+  if (tid == 0) s_abort = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_abort) return;
+  float b[KW];   // W_hhᵀ row j0 + c, k0 .. k0 + KW - 1
+  {
+    const float* bs = whhT + (size_t)(j0 + c) * 3 * H + k0;
+#pragma unroll
+    for (int s = 0; s < KW; s += 4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(bs + s);
+      b[s] = v[0]; b[s + 1] = v[1]; b[s + 2] = v[2]; b[s + 3] = v[3];
+    }
+  }
+  const uint32_t gbytes = (uint32_t)((size_t)n * 3 * H * 4);
+  for (int t = T - 1; t >= 1; --t) {
+    if (t < T - 1) {   // dgh(t) of the group's rows complete
+      if (tid == 0) {
+        const int target = need * (T - 1 - t);
+        int it = 0, ab = 0;
+        while (__hip_atomic_load(cnt + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+            ab = 1;
+            break;
+          }
+          if (++it > spin_max) {
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ab = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        s_abort = ab;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: dgh loads stay below the poll
+      __syncthreads();
+      if (s_abort) return;
+    }
+    const size_t o = (size_t)t * n * H, op = o - (size_t)n * H;
+    const float* mk = masks && !idx ? masks + (size_t)t * n : masks;
+    const int64_t* mi = idx ? idx + (size_t)t * n : nullptr;
+    const auto rs = make_rsrc(dgh + 3 * o, gbytes);
+    // epilogue operands (in flight during the MFMAs)
+    float pd[2], pm[2], pc[2][6];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int p = tid + 256 * e, m = min(m0 + (p >> 4), n - 1), j = j0 + (p & 15);
+      const size_t oe = (size_t)m * H + j;
+      pd[e] = dhz[oe];
+      pm[e] = mk ? mk[mi ? mi[m] : m] : 1.0f;
+      pc[e][0] = dout[op + oe]; pc[e][1] = sr[op + oe]; pc[e][2] = sz[op + oe];
+      pc[e][3] = sn[op + oe]; pc[e][4] = sghn[op + oe]; pc[e][5] = shin[op + oe];
+    }
+    f32x4 acc[2] = {zero4(), zero4()};
+#pragma unroll
+    for (int half = 0; half < NH; ++half) {
+      float a[2][KH];
+      const int kb = k0 + half * KH;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const int m = m0 + 16 * rt + c;
+        const bool ok = m < n;
+#pragma unroll
+        for (int s = 0; s < KH; s += 4) {
+          f32x4 v = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((ok ? m : 0) * 3 * H + kb + s) * 4, 0, 16));
+          v = ok ? v : zero4();
+          a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < KH; ++s)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+          acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], b[half * KH + s], acc[rt], 0, 0, 0);
+    }
+    P[q][0][lane] = acc[0];
+    P[q][1][lane] = acc[1];
+    __syncthreads();
+    float* dgh_p = dgh + 3 * op;
+    const auto rsp = make_rsrc(dgh_p, gbytes);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int p = tid + 256 * e, ml = p >> 4, jl = p & 15, m = m0 + ml, j = j0 + jl;
+      if (m >= n) continue;
+      const int rt = ml >> 4, ir = ml & 15, ln = jl + 16 * (ir >> 2), rg = ir & 3;
+      const float v = ((P[0][rt][ln][rg] + P[1][rt][ln][rg]) + P[2][rt][ln][rg]) + P[3][rt][ln][rg];
+      const size_t oe = (size_t)m * H + j;
+      const float cv = gru_carry(v, pd[e], pm[e]);
+      carry[oe] = cv;
+      // gru_cell_bwd_elem for step t - 1, dgh stored write-through for the group
+      const GruCellGrad cg = gru_cell_grad(pc[e][0] + cv, pc[e][1], pc[e][2], pc[e][3], pc[e][4], pc[e][5]);
+      const size_t gg = (size_t)m * 3 * H + j;
+      float* dgi_p = dgi + 3 * op;
+      dgi_p[gg] = cg.dar;
+      dgi_p[gg + H] = cg.daz;
+      dgi_p[gg + 2 * H] = cg.dan;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dar), rsp, (int)gg * 4, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.daz), rsp, (int)(gg + H) * 4, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dghn), rsp, (int)(gg + 2 * H) * 4, 0, 16);
+      dhz[oe] = cg.dhz;
+    }
+    if (t > 1) {   // publish dgh(t - 1) of this tile
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // also: every wave has read P before the next step rewrites it
+      if (tid == 0) __hip_atomic_fetch_add(cnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // 0: register-tiled step kernels where H allows; 1: the tile-GEMM steps (A/B)
 static int g_gru_variant = 0;
-// whole-sequence forward as one persistent launch (gru_seq16_kernel) where its
-// grid fits one block per CU; 0: one step kernel per step
+// persistent whole-sequence launches where the grid fits one block per CU, bit 0:
+// forward (gru_seq16_kernel), bit 1: backward (gru_seq_bwd16_kernel); clear bits
+// run one step kernel per step.  Default forward only: the persistent BPTT is
+// bit-identical but measured slower (12.6 vs 10.9 us per step at n = 512, H = 256:
+// the per-step dgh hand-off through write-through stores and the group counter
+// costs more than a kernel boundary there)
 static int g_gru_persist = 1;
 
 // bounded-wait length of the persistent kernels (polls of ~64 clocks each)
@@ -583,6 +738,19 @@ int launch_step_bwd16(const float* dgh, const float* whhT, const float* dhz, con
   dim3 grid((unsigned)ceil_div(M, 32), H / 16);
   gru_step_bwd16_kernel<H><<<grid, 256, 0, st>>>(dgh, whhT, dhz, masks, mask_idx, carry, M, cp);
   PPO_LAUNCH_CHECK("gru_step_bwd16_kernel");
+  return 0;
+}
+
+template <int H>
+int launch_seq_bwd16(const float* dout, const float* sr, const float* sz, const float* sn, const float* sghn,
+                     const float* shin, const float* masks, const int64_t* idx, const float* whhT, int T, int n,
+                     float* dgi, float* dgh, float* dhz, float* carry, int* cnt, int* err, hipStream_t st) {
+  const int groups = ceil_div(n, 32);
+  PPO_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)groups * sizeof(int), st), "ppo_gru_seq_bwd: counter reset");
+  dim3 grid((unsigned)groups, H / 16);
+  gru_seq_bwd16_kernel<H><<<grid, 256, 0, st>>>(dout, sr, sz, sn, sghn, shin, masks, idx, whhT, T, n, dgi, dgh, dhz,
+                                                carry, cnt, err, g_gru_spin);
+  PPO_LAUNCH_CHECK("gru_seq_bwd16_kernel");
   return 0;
 }
 
@@ -681,7 +849,7 @@ PPO_API int ppo_gru_seq_fwd_ws(const float* h0, const float* masks, const int64_
                                void* stream) {
   PPO_REQUIRE(T >= 0 && n >= 0 && H > 0 && H % 32 == 0, "ppo_gru_seq_fwd: T=%d n=%d H=%d", T, n, H);
   ProfScope prof("gru_seq_fwd", as_stream(stream), 2.0 * T * n * 3.0 * H * H);
-  if (T > 0 && n > 0 && g_gru_variant == 0 && g_gru_persist && (long long)ceil_div(n, 32) * (H / 16) <= gru_cus() &&
+  if (T > 0 && n > 0 && g_gru_variant == 0 && (g_gru_persist & 1) && (long long)ceil_div(n, 32) * (H / 16) <= gru_cus() &&
       (H == 64 || H == 128 || H == 256 || H == 512)) {
     PPO_REQUIRE(counters != nullptr && err != nullptr, "ppo_gru_seq_fwd_ws: the persistent launch needs counters "
                                                        "(ppo_gru_seq_counters(n) ints) and an error word");
@@ -712,7 +880,7 @@ PPO_API int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* 
                             const float* bhh, const float* gi, int T, int n, int H, float* hout, float* save_r,
                             float* save_z, float* save_n, float* save_ghn, float* save_hin, void* stream) {
   int* w = nullptr;
-  if (T > 0 && n > 0 && g_gru_persist) {
+  if (T > 0 && n > 0 && (g_gru_persist & 1)) {
     w = persist_words(as_stream(stream), ppo_gru_seq_counters(n));
     PPO_REQUIRE(w != nullptr, "ppo_gru_seq_fwd: counter allocation failed");
   }
@@ -720,13 +888,28 @@ PPO_API int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* 
                             w ? w + 1 : nullptr, w, stream);
 }
 
-PPO_API int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float* save_z, const float* save_n,
-                            const float* save_ghn, const float* save_hin, const float* masks, const int64_t* idx,
-                            const float* whhT, int T, int n, int H, float* dgi, float* dgh, float* dhz, float* carry,
-                            void* stream) {
+PPO_API int ppo_gru_seq_bwd_ws(const float* dout, const float* save_r, const float* save_z, const float* save_n,
+                               const float* save_ghn, const float* save_hin, const float* masks, const int64_t* idx,
+                               const float* whhT, int T, int n, int H, float* dgi, float* dgh, float* dhz,
+                               float* carry, int* counters, int* err, void* stream) {
   PPO_REQUIRE(T >= 0 && n >= 0 && H > 0 && H % 4 == 0, "ppo_gru_seq_bwd: T=%d n=%d H=%d", T, n, H);
   ProfScope prof("gru_seq_bwd", as_stream(stream), 2.0 * T * n * 3.0 * H * H);
   const bool fused = (H == 64 || H == 128 || H == 256 || H == 512) && g_gru_variant == 0;
+  if (T > 1 && n > 0 && fused && (g_gru_persist & 2) && (long long)ceil_div(n, 32) * (H / 16) <= gru_cus()) {
+    PPO_REQUIRE(counters != nullptr && err != nullptr, "ppo_gru_seq_bwd_ws: the persistent launch needs counters "
+                                                       "(ppo_gru_seq_counters(n) ints) and an error word");
+    const size_t o = (size_t)(T - 1) * n * H;   // step T - 1's cell backward (no carry), then steps T-1 .. 1
+    int rc = ppo_gru_cell_bwd(dout + o, carry, save_r + o, save_z + o, save_n + o, save_ghn + o, save_hin + o,
+                              dgi + 3 * o, dgh + 3 * o, dhz, n, H, 0, stream);
+    if (rc) return rc;
+    hipStream_t st = as_stream(stream);
+    switch (H) {
+      case 64: return launch_seq_bwd16<64>(dout, save_r, save_z, save_n, save_ghn, save_hin, masks, idx, whhT, T, n, dgi, dgh, dhz, carry, counters, err, st);
+      case 128: return launch_seq_bwd16<128>(dout, save_r, save_z, save_n, save_ghn, save_hin, masks, idx, whhT, T, n, dgi, dgh, dhz, carry, counters, err, st);
+      case 256: return launch_seq_bwd16<256>(dout, save_r, save_z, save_n, save_ghn, save_hin, masks, idx, whhT, T, n, dgi, dgh, dhz, carry, counters, err, st);
+      default: return launch_seq_bwd16<512>(dout, save_r, save_z, save_n, save_ghn, save_hin, masks, idx, whhT, T, n, dgi, dgh, dhz, carry, counters, err, st);
+    }
+  }
   for (int t = T - 1; t >= 0; --t) {
     const size_t o = (size_t)t * n * H, op = o - (size_t)n * H;
     int rc = 0;
@@ -746,9 +929,23 @@ PPO_API int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float*
   return 0;
 }
 
+// the same with the library's per-(device, stream) words (ppo_gru_persist_timeouts reads them)
+PPO_API int ppo_gru_seq_bwd(const float* dout, const float* save_r, const float* save_z, const float* save_n,
+                            const float* save_ghn, const float* save_hin, const float* masks, const int64_t* idx,
+                            const float* whhT, int T, int n, int H, float* dgi, float* dgh, float* dhz, float* carry,
+                            void* stream) {
+  int* w = nullptr;
+  if (T > 1 && n > 0 && (g_gru_persist & 2)) {
+    w = persist_words(as_stream(stream), ppo_gru_seq_counters(n));
+    PPO_REQUIRE(w != nullptr, "ppo_gru_seq_bwd: counter allocation failed");
+  }
+  return ppo_gru_seq_bwd_ws(dout, save_r, save_z, save_n, save_ghn, save_hin, masks, idx, whhT, T, n, H, dgi, dgh, dhz,
+                            carry, w ? w + 1 : nullptr, w, stream);
+}
+
 // persistent whole-sequence kernels on (1) / off (0)
 PPO_API int ppo_gru_persist_set(int v) {
-  PPO_REQUIRE(v == 0 || v == 1, "ppo_gru_persist_set: %d", v);
+  PPO_REQUIRE(v >= 0 && v <= 3, "ppo_gru_persist_set: %d (bit 0 forward, bit 1 backward)", v);
   g_gru_persist = v;
   return 0;
 }

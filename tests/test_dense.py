@@ -50,7 +50,7 @@ def _with_tune(key, value, products, fn):
         H_.call("ppo_tune_set", b"products", oldp)
 
 
-@pytest.mark.parametrize("variant", [0, 6, 7])
+@pytest.mark.parametrize("variant", [0, 6, 7, 8])
 @pytest.mark.parametrize("products", [6, 9, 1])
 @pytest.mark.parametrize("B,H", [(300, 512), (77, 64), (129, 256)])
 def test_fc_fwd_vs_float64(gpu, variant, products, B, H):
@@ -74,7 +74,7 @@ def test_fc_fwd_vs_float64(gpu, variant, products, B, H):
     assert torch.isnan(out[:, H:]).all()   # the padding columns are untouched
 
 
-@pytest.mark.parametrize("variant", [0, 6, 7])
+@pytest.mark.parametrize("variant", [0, 6, 7, 8])
 @pytest.mark.parametrize("products", [6, 9, 1])
 @pytest.mark.parametrize("B,H", [(300, 512), (77, 64)])
 def test_fc_dgrad_mask_vs_float64(gpu, variant, products, B, H):

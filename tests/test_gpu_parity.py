@@ -1292,6 +1292,102 @@ def test_gru_persistent_sequence_equals_steps(gpu, T, n, H, use_idx):
                                                       (outs[0][k] != outs[1][k]).sum().item())
 
 
+@pytest.mark.parametrize("T,n,H,use_idx", [(24, 512, 256, True), (9, 37, 64, False), (5, 100, 128, True),
+                                            (3, 16, 512, False), (2, 64, 256, True)])
+def test_gru_persistent_bptt_equals_steps(gpu, T, n, H, use_idx):
+    """ppo_gru_seq_bwd_ws as one persistent launch (gru_seq_bwd16_kernel: W_hh^T
+    slices resident, dgh handed over between the unit blocks of a row group) equals
+    the T - 1 step launches bit for bit — dgi and dgh over all T steps, the final
+    dhz and carry — with masks direct or through the minibatch index, and the error
+    word stays clear."""
+    Hh = _hip()
+    g = torch.Generator().manual_seed(T * n + H + 1)
+    N = 3 * n
+    R = T * n
+    dout = torch.randn(R, H, generator=g).cuda()
+    sv = {"r": torch.rand(R, H, generator=g), "z": torch.rand(R, H, generator=g),
+          "n": torch.rand(R, H, generator=g) * 2 - 1, "ghn": torch.randn(R, H, generator=g),
+          "hin": torch.randn(R, H, generator=g)}
+    sv = {k: v.cuda() for k, v in sv.items()}
+    whhT = (torch.randn(H, 3 * H, generator=g) / H ** 0.5).cuda()
+    if use_idx:
+        masks = (torch.rand(T * N, generator=g) > 0.1).float().cuda()
+        idx = torch.randint(0, T * N, (R,), generator=g).cuda()
+    else:
+        masks = (torch.rand(R, generator=g) > 0.1).float().cuda()
+        idx = None
+    cnt = torch.zeros(Hh.call("ppo_gru_seq_counters", n), dtype=torch.int32, device=gpu)
+    err = torch.zeros(1, dtype=torch.int32, device=gpu)
+    outs = {}
+    for persist in (0, 3):
+        o = {"dgi": torch.full((R, 3 * H), float("nan"), device=gpu), "dgh": torch.full((R, 3 * H), float("nan"),
+                                                                                       device=gpu),
+             "dhz": torch.zeros(n, H, device=gpu), "carry": torch.zeros(n, H, device=gpu)}
+        Hh.call("ppo_gru_persist_set", persist)
+        try:
+            Hh.call("ppo_gru_seq_bwd_ws", dout.data_ptr(), sv["r"].data_ptr(), sv["z"].data_ptr(), sv["n"].data_ptr(),
+                    sv["ghn"].data_ptr(), sv["hin"].data_ptr(), masks.data_ptr(),
+                    None if idx is None else idx.data_ptr(), whhT.data_ptr(), T, n, H, o["dgi"].data_ptr(),
+                    o["dgh"].data_ptr(), o["dhz"].data_ptr(), o["carry"].data_ptr(), cnt.data_ptr(), err.data_ptr(),
+                    _s())
+            torch.cuda.synchronize()
+        finally:
+            Hh.call("ppo_gru_persist_set", 1)
+        outs[persist] = o
+    assert err.item() == 0
+    outs[1] = outs.pop(3)
+    for k in outs[0]:
+        assert torch.isfinite(outs[1][k]).all(), k
+        bad = (outs[0][k] != outs[1][k]).nonzero()
+        if bad.numel():
+            rows = bad[:, 0].cpu()
+            print(k, "mismatches", bad.shape[0], "steps", torch.unique(rows // n).tolist()[:20],
+                  "cols", torch.unique(bad[:, 1].cpu() % H).tolist()[:20], "gate", torch.unique(bad[:, 1].cpu() // H).tolist())
+        assert torch.equal(outs[0][k], outs[1][k]), (k, (outs[0][k] - outs[1][k]).abs().max().item())
+
+
+def test_gru_persistent_bptt_timeout_sets_error(gpu):
+    """a bounded wait of the persistent BPTT that runs out (spin bound 0) sets the
+    error word and the launch returns; a launch that starts with the word set
+    returns at once (outputs untouched), and with the default bound it completes."""
+    Hh = _hip()
+    T, n, H = 6, 256, 256
+    g = torch.Generator().manual_seed(9)
+    R = T * n
+    args = [torch.randn(R, H, generator=g).cuda() for _ in range(6)]
+    masks = torch.ones(R, device=gpu)
+    whhT = (torch.randn(H, 3 * H, generator=g) / 16).cuda()
+    dgi = torch.zeros(R, 3 * H, device=gpu)
+    dgh = torch.zeros(R, 3 * H, device=gpu)
+    dhz = torch.zeros(n, H, device=gpu)
+    carry = torch.zeros(n, H, device=gpu)
+    cnt = torch.zeros(Hh.call("ppo_gru_seq_counters", n), dtype=torch.int32, device=gpu)
+    err = torch.zeros(1, dtype=torch.int32, device=gpu)
+
+    def run():
+        Hh.call("ppo_gru_seq_bwd_ws", *[a.data_ptr() for a in args], masks.data_ptr(), None, whhT.data_ptr(), T, n,
+                H, dgi.data_ptr(), dgh.data_ptr(), dhz.data_ptr(), carry.data_ptr(), cnt.data_ptr(), err.data_ptr(),
+                _s())
+        torch.cuda.synchronize()
+    Hh.call("ppo_gru_persist_set", 3)
+    Hh.call("ppo_gru_persist_spin_set", 0)
+    try:
+        run()
+    finally:
+        Hh.call("ppo_gru_persist_spin_set", 1 << 21)
+    assert err.item() == 1
+    dgi.zero_()
+    run()                       # sticky: returns at once
+    assert err.item() == 1
+    assert (dgi[: (T - 1) * n] == 0).all()
+    err.zero_()
+    try:
+        run()
+    finally:
+        Hh.call("ppo_gru_persist_set", 1)
+    assert err.item() == 0 and torch.isfinite(dgi).all() and (dgi[: n] != 0).any()
+
+
 @pytest.mark.parametrize("variant", [3, 4, 5, 6, 9])
 def test_conv1_wgrad_variants_vs_torch(gpu, variant):
     """conv1 weight + bias gradient from u8 observations gathered by index (the
