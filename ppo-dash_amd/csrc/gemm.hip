@@ -719,10 +719,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
                                                            const uint16_t* __restrict__ wpl,
                                                            const float* __restrict__ bias,
                                                            float* __restrict__ out,
-                                                           uint16_t* __restrict__ mbits, int dbg = 0) {
-  // dbg (timing anatomy only, wrong results): 16 skips the MFMAs, 32 the epilogue,
-  // 64 the staging of the next image
-  const bool no_mma = dbg & 16, no_epi = dbg & 32, no_stage = dbg & 64, no_split = dbg & 128, no_put = dbg & 256;
+                                                           uint16_t* __restrict__ mbits) {
   constexpr int U = 400, PLN = 4 * U, STG = 3 * PLN, MT = 6, KS = 8, WN = 64 * 512;
   constexpr int UNITS = 4 * U, UPER = (UNITS + 511) / 512;   // 4 units per thread (the 4th: wave 0)
   __shared__ __attribute__((aligned(16))) bf16x8 S[2 * STG];
@@ -775,15 +772,8 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
     }
   };
   auto put_hm = [&](int j, int st) {   // hi / mid parts now, lo part held
-    if (no_put) return;
     Frag3 f;
-    if (no_split) {
-      f.h = __builtin_bit_cast(bf16x8, stg[j][0]);
-      f.m = __builtin_bit_cast(bf16x8, stg[j][1]);
-      f.l = f.h;
-    } else {
-      split8(stg[j][0], stg[j][1], f, NP == 1);
-    }
+    split8(stg[j][0], stg[j][1], f, NP == 1);
     lo[j] = f.l;
     if (j < UPER - 1 || has_last) {
       bf16x8* d = S + st * STG + udst[j];
@@ -792,7 +782,6 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
     }
   };
   auto put_l = [&](int j, int st) {
-    if (no_put) return;
     if constexpr (NP > 1)
       if (j < UPER - 1 || has_last) S[st * STG + 2 * PLN + udst[j]] = lo[j];
   };
@@ -840,14 +829,13 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
         }
 #define PPO_PART(X, Y) \
   _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(w.Y, a[u].X, acc[t0 + u]);
-        if (!no_mma) { PPO_PRODUCTS(NP, PPO_PART) }
-        else { _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] += __builtin_bit_cast(f32x4, a[u].h); }
+        PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       }
-      if (s < UPER && nxt && !no_stage) put_hm(s, cur ^ 1);
-      if (s == UPER && nn && !no_stage) fetch(b + 2 * G);
+      if (s < UPER && nxt) put_hm(s, cur ^ 1);
+      if (s == UPER && nn) fetch(b + 2 * G);
       if (s == 5) lds_barrier();   // mid-image: the previous image's partials (lo plane of stage cur ^ 1) are read
-      if (s >= 6 && nxt && !no_stage) {
+      if (s >= 6 && nxt) {
 #pragma unroll
         for (int j = 0; j < UPER; ++j)
           if ((j & 1) == s - 6) put_l(j, cur ^ 1);
@@ -860,7 +848,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
       for (int t = 0; t < MT; ++t) R[(nt * MT + t) * 64 + lane] = acc[t];
     }
     lds_barrier();   // B: partials in LDS
-    if (kh == 0 && !no_epi) {
+    if (kh == 0) {
       const auto rs = make_rsrc(out + (size_t)b * (81 * 64), 81 * 64 * 4);
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
@@ -877,202 +865,6 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
           const int w16 = nib | (__shfl_down(nib, 16, 64) << 4) | (__shfl_down(nib, 32, 64) << 8) |
                           (__shfl_down(nib, 48, 64) << 12);
           if (g == 0 && m >= 0) mbits[((size_t)b * 81 + m) * 4 + nt] = (uint16_t)w16;
-        }
-      }
-    }
-    cur ^= 1;
-  }
-}
-
-// conv2 forward on v_mfma_f32_32x32x16_bf16 (ppo_tune_set("conv2_fwd", 13)): the
-// compact parity layout and two LDS stages of conv2_fwd_x9c_kernel, but each wave
-// owns 32 output channels (ct = w & 1) for a quarter of K (taps 4 kq .. +3,
-// kq = w >> 1): every B fragment read (16 channels x 32 pixels of one plane)
-// feeds 32 co instead of 16, so the fragment reads per MFMA cycle halve (the
-// x9c kernel's k loop measured 1.62 ms per 65,536 images with no staging at all
-// against a 0.98 ms MFMA floor: exposed LDS latency at 2 waves per SIMD).  The
-// fragments of the next (k-step, pixel tile) are read while the current one's
-// MFMAs run.  Pixel tile T = the 16-row tiles 2T, 2T + 1 of the x9c layout.
-//   * The four K-quarter partials are reduce-scattered through the stage the
-//     image has just left (73,728 B): wave (ct, kq) owns accumulator row group
-//     kq (channels 32 ct + 8 kq + [0, 8)) of every tile, writes its other three
-//     groups, sums its own three incoming ones in a fixed order (source kq
-//     ascending), stores 16 B per lane and tile, and the mask bits as one byte
-//     (8 channels) per pixel.
-//   * The next image is staged whole at k-steps 6-7, after a mid-image barrier
-//     (k-step 5) that retires the previous image's partial reads from that stage;
-//     the image after it is then fetched into registers (a whole image of lead).
-template <int NP, bool MASK = false>
-__global__ __launch_bounds__(512) void conv2_fwd_x32_kernel(const float* __restrict__ a1, int B,
-                                                           const uint16_t* __restrict__ wpl,
-                                                           const float* __restrict__ bias,
-                                                           float* __restrict__ out,
-                                                           uint8_t* __restrict__ mbytes, int dbg = 0) {
-  const bool no_epi = dbg & 32, no_stage = dbg & 64;
-  constexpr int U = 400, PLN = 4 * U, STG = 3 * PLN, KS = 8, WN = 64 * 512, NPL = NP == 1 ? 1 : 3;
-  constexpr int UNITS = 4 * U, UPER = (UNITS + 511) / 512;
-  __shared__ __attribute__((aligned(16))) bf16x8 S[2 * STG];
-  __shared__ int vtab[6][16];
-  __shared__ int otab[6][16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, hh = lane >> 5;
-  const int ct = wave & 1, kq = wave >> 1;
-  if (tid < 16) {
-    int t = 0;
-    for (int v = tid; v <= 88; v += 16)
-      if (v % 10 != 9) {
-        vtab[t][tid] = v;
-        otab[t][tid] = 9 * (v / 10) + v % 10;
-        ++t;
-      }
-    for (; t < 6; ++t) {
-      vtab[t][tid] = tid;
-      otab[t][tid] = -1;
-    }
-  }
-  // A fragments (weights, pre-split planes): row co = 32 ct + l32, k-step s =
-  // (local tap s >> 1, channel half s & 1), k 8 hh .. +7 of it
-  bf16x8 bw[KS][NPL];
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int p = 0; p < NPL; ++p)
-      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + (32 * ct + l32) * 512 +
-                                                  (4 * kq + (s >> 1)) * 32 + 16 * (s & 1) + 8 * hh);
-  const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 32 * ct + 8 * kq + 4 * hh);
-  wait_vm0();
-  // staging unit u = tid + 512 j (x9c mapping), recomputed where used
-  auto unit = [&](int j, int& src, int& dst) __attribute__((always_inline)) {
-    const int u = min(tid + 512 * j, UNITS - 1), rho = 8 * (u >> 5) + (u & 7), c = (u >> 3) & 3;
-    const int par = rho / 100, rem = rho - 100 * par, yh = rem / 10, xh = rem - 10 * yh;
-    const int y = 2 * yh + (par >> 1), x = 2 * xh + (par & 1);
-    src = (y * 20 + x) * 8 + 2 * c;
-    dst = c * U + rho;
-  };
-  const bool has_last = tid + 512 * (UPER - 1) < UNITS;
-  f32x4 stg[UPER][2];
-  auto fetch = [&](int b) __attribute__((always_inline)) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
-#pragma unroll
-    for (int j = 0; j < UPER; ++j) {
-      int us, ud;
-      unit(j, us, ud);
-      stg[j][0] = src[us];
-      stg[j][1] = src[us + 1];
-    }
-  };
-  auto put = [&](int j, int st) __attribute__((always_inline)) {
-    Frag3 f;
-    split8(stg[j][0], stg[j][1], f, NP == 1);
-    if (j < UPER - 1 || has_last) {
-      int us, ud;
-      unit(j, us, ud);
-      bf16x8* d = S + st * STG + ud;
-      d[0] = f.h;
-      if constexpr (NP > 1) {
-        d[PLN] = f.m;
-        d[2 * PLN] = f.l;
-      }
-    }
-  };
-  __syncthreads();   // vtab / otab
-  int vrow[3];       // unit of this lane's B row in pixel tile T, chunk hh (k-step chunk 2 (s & 1) + hh)
-#pragma unroll
-  for (int T = 0; T < 3; ++T) vrow[T] = vtab[2 * T + (l32 >> 4)][l32 & 15] + hh * U;
-  const int G = gridDim.x;
-  int b = blockIdx.x, cur = 0;
-  if (b < B) {
-    fetch(b);
-#pragma unroll
-    for (int j = 0; j < UPER; ++j) put(j, 0);
-    if (b + G < B) fetch(b + G);
-  }
-  __syncthreads();
-  for (; b < B; b += G) {
-    const bool nxt = b + G < B, nn = b + 2 * G < B;
-    const bf16x8* Sc = S + cur * STG;
-    f32x16 acc[3];
-#pragma unroll
-    for (int T = 0; T < 3; ++T)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[T][r] = 0.f;
-    Frag3 fr[2];
-    auto rd = [&](int i, Frag3& f) __attribute__((always_inline)) {   // (k-step, tile) step i = 3 s + T
-      const int s = i / 3, T = i - 3 * s, tap = 4 * kq + (s >> 1), ky = tap >> 2, kx = tap & 3;
-      const int toff = 100 * (2 * (ky & 1) + (kx & 1)) + 10 * (ky >> 1) + (kx >> 1) + 2 * U * (s & 1);
-      const bf16x8* q = Sc + vrow[T] + toff;
-      f.h = q[0];
-      if constexpr (NP > 1) {
-        f.m = q[PLN];
-        f.l = q[2 * PLN];
-      }
-    };
-    rd(0, fr[0]);
-#pragma unroll
-    for (int i = 0; i < 3 * KS; ++i) {
-      const int s = i / 3, T = i - 3 * s;
-      if (i + 1 < 3 * KS) rd(i + 1, fr[(i + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);   // the next step's reads go out before this step's MFMAs
-      const Frag3& a = fr[i & 1];
-      const bf16x8* w = bw[s];
-#define PPO_PART(X, Y) acc[T] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[PPO_PL_##Y], a.X, acc[T], 0, 0, 0);
-#define PPO_PL_h 0
-#define PPO_PL_m 1
-#define PPO_PL_l 2
-      PPO_PRODUCTS(NP, PPO_PART)
-      __builtin_amdgcn_sched_barrier(0);   // keep the one-step read lead (no hoisting of later reads)
-#undef PPO_PART
-#undef PPO_PL_h
-#undef PPO_PL_m
-#undef PPO_PL_l
-      if (T == 2 && s == 5) lds_barrier();   // mid-image: the previous image's partials (stage cur ^ 1) are read
-      if (T == 2 && s >= 6 && nxt && !no_stage) {
-#pragma unroll
-        for (int j = 0; j < UPER; ++j)
-          if ((j >> 1) == s - 6) put(j, cur ^ 1);
-        if (s == 7 && nn) fetch(b + 2 * G);
-      }
-    }
-    lds_barrier();   // A: stage cur consumed; stage cur ^ 1 complete
-    // reduce-scatter of the K quarters through stage cur: owner (ct, j) of row
-    // group j, tile T, source slot (kq < j ? kq : kq - 1)
-    f32x4* R = reinterpret_cast<f32x4*>(S + cur * STG);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j != kq) {
-        const int src = kq < j ? kq : kq - 1;
-#pragma unroll
-        for (int T = 0; T < 3; ++T)
-          R[(((ct * 4 + j) * 3 + T) * 3 + src) * 64 + lane] =
-              f32x4{acc[T][4 * j], acc[T][4 * j + 1], acc[T][4 * j + 2], acc[T][4 * j + 3]};
-      }
-    lds_barrier();   // B: partials in LDS
-    if (!no_epi) {
-      const auto rs = make_rsrc(out + (size_t)b * (81 * 64), 81 * 64 * 4);
-#pragma unroll
-      for (int T = 0; T < 3; ++T) {
-        f32x4 v = zero4();
-        // fixed order: the K quarters ascending (the owner's own in its place)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          f32x4 part;
-          if (q == kq) {
-            part = f32x4{acc[T][4 * kq], acc[T][4 * kq + 1], acc[T][4 * kq + 2], acc[T][4 * kq + 3]};
-          } else {
-            part = R[(((ct * 4 + kq) * 3 + T) * 3 + (q < kq ? q : q - 1)) * 64 + lane];
-          }
-          v += part;
-        }
-        const int m = otab[2 * T + (l32 >> 4)][l32 & 15];
-        f32x4 y;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
-        bstore_f32x4(y, rs, m >= 0 ? 4 * (m * 64 + 32 * ct + 8 * kq + 4 * hh) : -1);
-        if constexpr (MASK) {   // channels 32 ct + 8 kq .. +7 of pixel m: one byte of its u64 word
-          int nib = 0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) nib |= (y[r] > 0.f ? 1 : 0) << r;
-          const int byte = nib | (__shfl_down(nib, 32, 64) << 4);
-          if (hh == 0 && m >= 0) mbytes[((size_t)b * 81 + m) * 8 + 4 * ct + kq] = (uint8_t)byte;
         }
       }
     }
@@ -1109,9 +901,7 @@ template <int NP>
 __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __restrict__ dz2,
                                                             const float* __restrict__ a1, int B,
                                                             float* __restrict__ slab,
-                                                            float* __restrict__ slab_bias, int dbg = 0) {
-  // dbg (timing anatomy only, wrong results): 16 skips the MFMAs, 64 the staging
-  const bool no_mma = dbg & 16, no_stage = dbg & 64;
+                                                            float* __restrict__ slab_bias) {
   constexpr int XPL = 400 * 32, DR = 112, DPL = 64 * DR;
   constexpr int XU = 1600, XPER = (XU + 511) / 512, DU = 64 * 12, DPER = (DU + 511) / 512;
   __shared__ __attribute__((aligned(16))) uint16_t X[3 * XPL];
@@ -1231,14 +1021,13 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
         bf.l = __builtin_bit_cast(bf16x8, __builtin_shufflevector(t[2][0], t[2][1], 0, 1, 2, 3, 4, 5, 6, 7));
 #define PPO_PART(XX, YY) \
   _Pragma("unroll") for (int mt = 0; mt < 4; ++mt) acc[j][mt] = mma(a[mt].XX, bf.YY, acc[j][mt]);
-        if (!no_mma) { PPO_PRODUCTS(NP, PPO_PART) }
-        else { _Pragma("unroll") for (int mt = 0; mt < 4; ++mt) acc[j][mt] += __builtin_bit_cast(f32x4, a[mt].h) + __builtin_bit_cast(f32x4, bf.h); }
+        PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       }
     }
     __syncthreads();   // the image is consumed
-    if (b + Z < B && !no_stage) put();
-    if (b + 2 * Z < B && !no_stage) fetch(b + 2 * Z);
+    if (b + Z < B) put();
+    if (b + 2 * Z < B) fetch(b + 2 * Z);
     __syncthreads();   // the next image is in LDS
   }
   // this block's partial: C row 4g + r of co tile mt, column i16 of n tile j
@@ -2288,31 +2077,13 @@ PPO_API int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const f
 static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float* b2, float* out, uint16_t* mbits,
                           void* stream) {
   if (!mbits && B > 0 && B <= g_small_b) return small_conv2_fwd(a1, B, w2p, b2, out, as_stream(stream));
-  if (mbits && g_tune[TK_CONV2_FWD] != 12 && g_tune[TK_CONV2_FWD] != 13) {   // no fused mask epilogue
+  if (mbits && g_tune[TK_CONV2_FWD] != 12) {   // no fused mask epilogue
     const int rc = conv2_fwd_impl(a1, B, w2p, b2, out, nullptr, stream);
     if (rc != 0 || B <= 0) return rc;
     const long long halves = (long long)B * 81 * 4;
     const long long nb = (halves + 255) / 256;
     relu_bits_kernel<<<(unsigned)(nb < 8192 ? nb : 8192), 256, 0, as_stream(stream)>>>(out, halves, mbits);
     PPO_LAUNCH_CHECK("relu_bits_kernel");
-    return 0;
-  }
-  if (g_tune[TK_CONV2_FWD] == 13) {   // 32x32x16 MFMA, K quarters reduce-scattered
-    if (B <= 0) return 0;
-    const int n_cu = device_cus();
-    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
-    int slot;
-    const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
-    const uint16_t* wpl = planes_of(w2p, 64 * 512);
-    hipStream_t st = as_stream(stream);
-    uint8_t* mb = reinterpret_cast<uint8_t*>(mbits);
-    const int dbg = g_stagger & 0x70;
-    if (mbits && g_products == 9) conv2_fwd_x32_kernel<9, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mb, dbg);
-    else if (mbits && g_products == 1) conv2_fwd_x32_kernel<1, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mb, dbg);
-    else if (mbits) conv2_fwd_x32_kernel<6, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mb, dbg);
-    else PPO_LAUNCH_NP(conv2_fwd_x32_kernel, nb, 512, st, a1, B, wpl, b2, out, nullptr, dbg);
-    if (prof) ppo_prof_end(slot, st, 2.0 * B * 81 * 64 * 512);
-    PPO_LAUNCH_CHECK("conv2_fwd_x32_kernel");
     return 0;
   }
   if (g_tune[TK_CONV2_FWD] == 12) {   // two LDS stages, staging inside the k-steps
@@ -2323,11 +2094,10 @@ static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float*
     const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
     const uint16_t* wpl = planes_of(w2p, 64 * 512);
     hipStream_t st = as_stream(stream);
-    const int dbg = g_stagger & 0x1f0;
-    if (mbits && g_products == 9) conv2_fwd_x9c_kernel<9, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits, dbg);
-    else if (mbits && g_products == 1) conv2_fwd_x9c_kernel<1, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits, dbg);
-    else if (mbits) conv2_fwd_x9c_kernel<6, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits, dbg);
-    else PPO_LAUNCH_NP(conv2_fwd_x9c_kernel, nb, 512, st, a1, B, wpl, b2, out, nullptr, dbg);
+    if (mbits && g_products == 9) conv2_fwd_x9c_kernel<9, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+    else if (mbits && g_products == 1) conv2_fwd_x9c_kernel<1, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+    else if (mbits) conv2_fwd_x9c_kernel<6, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+    else PPO_LAUNCH_NP(conv2_fwd_x9c_kernel, nb, 512, st, a1, B, wpl, b2, out, nullptr);
     if (prof) ppo_prof_end(slot, st, 2.0 * B * 81 * 64 * 512);
     PPO_LAUNCH_CHECK("conv2_fwd_x9c_kernel");
     return 0;
@@ -2688,7 +2458,7 @@ PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, flo
     if (B <= 0 || Z <= 0) return 0;
     int slot;
     const bool prof = ppo_prof_begin("conv2_wgrad", as_stream(stream), &slot);
-    PPO_LAUNCH_NP(conv2_wgrad_x9_kernel, Z, 512, as_stream(stream), dz2, a1, B, slab, slab_bias, g_stagger & 0x50);
+    PPO_LAUNCH_NP(conv2_wgrad_x9_kernel, Z, 512, as_stream(stream), dz2, a1, B, slab, slab_bias);
     if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
     PPO_LAUNCH_CHECK("conv2_wgrad_x9_kernel");
     return 0;
