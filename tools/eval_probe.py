@@ -34,3 +34,14 @@ for name, fn in (("eager", lambda h: pol.act(obs, vec, h, m, deterministic=True)
             _, a, _, h = fn(h)
         a.item()
     print(name, (time.perf_counter() - t0) * 10, "ms per act", flush=True)
+ga2 = GraphedActor(pol, carry_hidden=True)
+ga2.obs.copy_(obs)
+ga2.vec.copy_(vec)
+for _ in range(10):
+    ga2.replay()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(100):
+    out = ga2.replay()
+    out[1].item()
+print("replay", (time.perf_counter() - t0) * 10, "ms per act", flush=True)
