@@ -191,7 +191,7 @@ def gae_roofline(device, lanes, T=128, reps=10):
     nv = torch.randn(lanes, device=device, generator=g)
     ret = torch.empty(T + 1, lanes, device=device)
     adv = torch.empty(T, lanes, device=device)
-    parts = torch.empty(2 * call("ppo_gae_partials_count", lanes), dtype=torch.float64, device=device)
+    parts = torch.empty(3 * call("ppo_gae_partials_count", lanes), dtype=torch.float64, device=device)
     s = stream()
     args = (r.data_ptr(), v.data_ptr(), m.data_ptr(), m.data_ptr(), nv.data_ptr(), ret.data_ptr(), adv.data_ptr(),
             parts.data_ptr(), T, lanes, 0.99, 0.95, 1, 0, s)

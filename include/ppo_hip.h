@@ -49,7 +49,7 @@ int ppo_prof_collect_one(int idx, double* out3);          /* the idx-th listed n
 /* storage.py:82-121 RolloutStorage.compute_returns (all four branches,
  * bit-identical).  adv/partials (both or neither): also write
  * adv = returns[:-1] - value_preds[:-1] (algo/ppo.py:35) and per-block
- * (Σadv, Σadv²) partials, 2*ppo_gae_partials_count(N) doubles. */
+ * (count, mean, M2) moment partials, 3*ppo_gae_partials_count(N) doubles. */
 int ppo_gae_partials_count(int N);
 int ppo_compute_returns(const float* rewards, float* value_preds, const float* masks, const float* bad_masks,
                         const float* next_value, float* returns, float* adv, double* partials, int T, int N,
@@ -57,16 +57,19 @@ int ppo_compute_returns(const float* rewards, float* value_preds, const float* m
 /* time-parallel compute_returns (same arguments and side effects; within
  * tolerance, not bit-exact): each lane's affine recurrence folded per time chunk,
  * chunk carries composed through LDS — for few lanes / long T (c1, c2);
- * partials: 2*ppo_gae_scan_partials_count(N) doubles */
+ * partials: 3*ppo_gae_scan_partials_count(N) doubles */
 int ppo_gae_scan_partials_count(int N);
 int ppo_compute_returns_scan(const float* rewards, float* value_preds, const float* masks, const float* bad_masks,
                              const float* next_value, float* returns, float* adv, double* partials, int T, int N,
                              double gamma, double gae_lambda, int use_gae, int use_proper_time_limits, void* stream);
-/* algo/ppo.py:35 advantages = returns[:-1] - value_preds[:-1] (+ partials) */
+/* algo/ppo.py:35 advantages = returns[:-1] - value_preds[:-1] (+ partials, 3 doubles per block) */
 int ppo_adv_diff_partials_count(long long n);
 int ppo_adv_diff(const float* returns, const float* value_preds, float* adv, double* partials, long long n,
                  void* stream);
-/* algo/ppo.py:36 advantages.mean()/std(): stats = {count, Σ, Σ²} (all-reducible) */
+/* algo/ppo.py:36 advantages.mean()/std(): stats = {count, mean, M2}, merged from the
+ * block partials with Chan et al.'s update in a fixed order (Welford; ranks merge
+ * their triples the same way, _dist.allreduce_stats); count is taken from the
+ * partials (the argument is unused) */
 int ppo_adv_finalize(const double* partials, int nparts, double count, double* stats, void* stream);
 /* algo/ppo.py:36-37 (adv - mean) / (std + 1e-5), std unbiased */
 int ppo_adv_normalize(float* adv, long long n, const double* stats, void* stream);

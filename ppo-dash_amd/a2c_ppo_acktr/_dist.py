@@ -4,8 +4,10 @@ lanes and its own RolloutStorage; torch.distributed with backend "nccl" is
 RCCL over xGMI on ROCm.  Exchanges, all on the current stream:
 
   once per run     broadcast_params   rank 0's flat parameters to every rank
-  once per update  allreduce_stats    {count, Σadv, Σadv²} (3 doubles) -> global
-                                      advantage mean / unbiased std (ppo.py:36)
+  once per update  allreduce_stats    {count, mean, M2} (3 doubles) gathered from
+                                      every rank and merged in rank order (Chan
+                                      et al.) -> global advantage mean / unbiased
+                                      std (ppo.py:36; Welford)
   per minibatch    allreduce_grads    Σ of the flat fp32 gradient; clip + Adam
                                       then run on Σ/G (scale returned here)
   once per update  allreduce_losses   mean of the 3 logged losses over ranks
@@ -50,9 +52,31 @@ def broadcast_params(flat):
         dist.broadcast(flat, src=0)
 
 
+def merge_moments(parts):
+    """Chan et al.'s pairwise merge of (count, mean, M2) triples in the given
+    order — the same update the GPU kernels use (gae.hip mom_merge), on tensors
+    of the caller's device (no host synchronisation)."""
+    n, mean, m2 = parts[0][0], parts[0][1], parts[0][2]
+    for p in parts[1:]:
+        nb, mb, qb = p[0], p[1], p[2]
+        tot = n + nb
+        f = torch.where(tot > 0, nb / torch.where(tot > 0, tot, torch.ones_like(tot)), torch.zeros_like(tot))
+        d = mb - mean
+        mean = mean + d * f
+        m2 = m2 + qb + d * d * n * f
+        n = tot
+    return torch.stack([n, mean, m2])
+
+
 def allreduce_stats(stats):
+    """stats {count, mean, M2} of this rank's advantages -> the global ones, on
+    every rank bit-identically (all ranks merge the same gathered list in rank
+    order); a Welford merge instead of summed moments, so a shard whose mean is
+    large against its spread loses no precision"""
     if active():
-        dist.all_reduce(stats)
+        parts = [torch.empty_like(stats) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, stats)
+        stats.copy_(merge_moments(parts))
     return stats
 
 
@@ -96,8 +120,7 @@ def allreduce_losses(acc):
     return acc
 
 
-def stats_mean_std(count, s, q):
+def stats_mean_std(count, mean, m2):
     """Host restatement of adv_normalize_kernel's statistics (gae.hip)."""
-    mean = s / count
-    var = max((q - s * mean) / (count - 1.0), 0.0)
+    var = max(m2 / (count - 1.0), 0.0)
     return mean, math.sqrt(var)

@@ -165,7 +165,7 @@ class RolloutStorage(object):
                      call("ppo_adv_diff_partials_count", T * N))
         if self._adv is None or self._adv.shape != (T, N) or self._adv.device != dev:
             self._adv = torch.empty(T, N, device=dev)
-            self._adv_partials = torch.empty(2 * nparts, dtype=torch.float64, device=dev)
+            self._adv_partials = torch.empty(3 * nparts, dtype=torch.float64, device=dev)
             self._adv_stats = torch.empty(3, dtype=torch.float64, device=dev)
 
     def normalized_advantages(self):

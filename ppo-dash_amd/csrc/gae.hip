@@ -21,6 +21,63 @@ namespace {
 constexpr int GAE_THREADS = 256;
 constexpr int GAE_U = 8;  // time steps prefetched per chunk
 
+// Advantage moments as (count, mean, M2) (the reference's
+// advantages.mean() / .std(), T/a2c_ppo_acktr/algo/ppo.py:35-37): each thread
+// keeps shifted sums Σ(d - k), Σ(d - k)² about its first value k (exact for a
+// constant series, stable when the mean is large against the spread), and the
+// thread, wave, block, grid and rank results are combined with Chan et al.'s
+// pairwise update — always (lower, higher), so the result is deterministic and
+// identical on every lane of a butterfly.
+struct Mom {
+  double n, mean, m2;
+};
+struct MomAcc {
+  double k = 0.0, s = 0.0, q = 0.0, n = 0.0;
+  __device__ __forceinline__ void add(double d) {
+    if (n == 0.0) k = d;
+    const double e = d - k;
+    s += e;
+    q += e * e;
+    n += 1.0;
+  }
+  __device__ __forceinline__ Mom get() const {
+    if (n == 0.0) return {0.0, 0.0, 0.0};
+    const double m2 = q - s * (s / n);
+    return {n, k + s / n, m2 > 0.0 ? m2 : 0.0};
+  }
+};
+__device__ __forceinline__ Mom mom_merge(const Mom& a, const Mom& b) {
+  const double n = a.n + b.n;
+  if (b.n == 0.0) return a;
+  if (a.n == 0.0) return b;
+  const double d = b.mean - a.mean, f = b.n / n;
+  return {n, a.mean + d * f, a.m2 + b.m2 + d * d * a.n * f};
+}
+__device__ __forceinline__ Mom wave_merge(Mom m) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const Mom p{__shfl_xor(m.n, o, 64), __shfl_xor(m.mean, o, 64), __shfl_xor(m.m2, o, 64)};
+    m = (lane & o) ? mom_merge(p, m) : mom_merge(m, p);
+  }
+  return m;
+}
+// block result -> partials[3 blk .. +2]; WAVES waves, lds scratch of WAVES Mom
+template <int WAVES>
+__device__ __forceinline__ void block_moments(const MomAcc& acc, double* __restrict__ partials) {
+  __shared__ Mom red[WAVES];
+  const Mom w = wave_merge(acc.get());
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Mom t = red[0];
+    for (int i = 1; i < WAVES; ++i) t = mom_merge(t, red[i]);
+    partials[3 * blockIdx.x] = t.n;
+    partials[3 * blockIdx.x + 1] = t.mean;
+    partials[3 * blockIdx.x + 2] = t.m2;
+  }
+}
+
 template <bool USE_GAE, bool PTL, bool FUSE_ADV>
 __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
     const float* __restrict__ rewards, float* __restrict__ value_preds,
@@ -28,7 +85,7 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
     const float* __restrict__ next_value, float* __restrict__ returns,
     float* __restrict__ adv, double* __restrict__ partials, int T, int N, float g, float gl) {
   const int n = blockIdx.x * GAE_THREADS + threadIdx.x;
-  double s = 0.0, q = 0.0;
+  MomAcc mom;
   if (n < N) {
     const size_t NN = (size_t)N;
     const float nv = next_value[n];
@@ -86,27 +143,13 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
           if (FUSE_ADV) {
             const float d = out - vv[j];       // returns[:-1] - value_preds[:-1]
             adv[(size_t)t * NN + n] = d;
-            s += (double)d;
-            q += (double)d * (double)d;
+            mom.add((double)d);
           }
         }
       }
     }
   }
-  if (FUSE_ADV) {
-    __shared__ double red[2][GAE_THREADS / 64];
-    s = wave_sum_d(s);
-    q = wave_sum_d(q);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[0][w] = s; red[1][w] = q; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double ss = 0.0, qq = 0.0;
-      for (int i = 0; i < GAE_THREADS / 64; ++i) { ss += red[0][i]; qq += red[1][i]; }
-      partials[2 * blockIdx.x] = ss;
-      partials[2 * blockIdx.x + 1] = qq;
-    }
-  }
+  if (FUSE_ADV) block_moments<GAE_THREADS / 64>(mom, partials);
 }
 
 // ---------------------------------------------------------------------------
@@ -178,7 +221,7 @@ __global__ __launch_bounds__(SCAN_LANES * SCAN_CH) void gae_scan_kernel(
   float x = USE_GAE ? 0.0f : nv;
   for (int k = SCAN_CH - 1; k > c; --k) x = mapA[k][l] + mapB[k][l] * x;
   // 3. re-walk with the carry; the storage side effects of the exact kernel
-  double s = 0.0, q = 0.0;
+  MomAcc mom;
   if (live) {
     if (t_lo < T && t_hi == T) {   // the last non-empty chunk
       if (USE_GAE) value_preds[(size_t)T * NN + n] = nv;   // storage.py:90/:108
@@ -193,25 +236,11 @@ __global__ __launch_bounds__(SCAN_LANES * SCAN_CH) void gae_scan_kernel(
       if (FUSE_ADV) {
         const float d = out - v;
         adv[(size_t)t * NN + n] = d;
-        s += (double)d;
-        q += (double)d * (double)d;
+        mom.add((double)d);
       }
     }
   }
-  if (FUSE_ADV) {
-    __shared__ double red[2][SCAN_LANES * SCAN_CH / 64];
-    s = wave_sum_d(s);
-    q = wave_sum_d(q);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { red[0][w] = s; red[1][w] = q; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double ss = 0.0, qq = 0.0;
-      for (int i = 0; i < SCAN_LANES * SCAN_CH / 64; ++i) { ss += red[0][i]; qq += red[1][i]; }
-      partials[2 * blockIdx.x] = ss;
-      partials[2 * blockIdx.x + 1] = qq;
-    }
-  }
+  if (FUSE_ADV) block_moments<SCAN_LANES * SCAN_CH / 64>(mom, partials);
 }
 
 // adv = returns - value_preds over the first T rows, plus moment partials
@@ -220,58 +249,44 @@ __global__ __launch_bounds__(256) void adv_diff_kernel(const float* __restrict__
                                                        const float* __restrict__ value_preds,
                                                        float* __restrict__ adv,
                                                        double* __restrict__ partials, long long n) {
-  double s = 0.0, q = 0.0;
+  MomAcc mom;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     const float d = returns[i] - value_preds[i];
     adv[i] = d;
-    s += (double)d;
-    q += (double)d * (double)d;
+    mom.add((double)d);
   }
-  __shared__ double red[2][4];
-  s = wave_sum_d(s);
-  q = wave_sum_d(q);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { red[0][w] = s; red[1][w] = q; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    partials[2 * blockIdx.x] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    partials[2 * blockIdx.x + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-  }
+  block_moments<4>(mom, partials);
 }
 
-// Deterministic fixed-order sum of the block partials -> stats {count, S, Q}.
+// Deterministic fixed-order merge of the block partials -> stats {count, mean, M2}
+// (count: the partials' own; the argument is kept for the ABI).
 __global__ __launch_bounds__(256) void adv_finalize_kernel(const double* __restrict__ partials, int nparts,
                                                            double count, double* __restrict__ stats) {
-  double s = 0.0, q = 0.0;
-  for (int i = threadIdx.x; i < nparts; i += 256) {
-    s += partials[2 * i];
-    q += partials[2 * i + 1];
-  }
-  __shared__ double rs[256], rq[256];
-  rs[threadIdx.x] = s;
-  rq[threadIdx.x] = q;
+  (void)count;
+  Mom m{0.0, 0.0, 0.0};
+  for (int i = threadIdx.x; i < nparts; i += 256) m = mom_merge(m, Mom{partials[3 * i], partials[3 * i + 1],
+                                                                       partials[3 * i + 2]});
+  __shared__ Mom r[256];
+  r[threadIdx.x] = m;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      rs[threadIdx.x] += rs[threadIdx.x + o];
-      rq[threadIdx.x] += rq[threadIdx.x + o];
-    }
+    if (threadIdx.x < o) r[threadIdx.x] = mom_merge(r[threadIdx.x], r[threadIdx.x + o]);
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    stats[0] = count;
-    stats[1] = rs[0];
-    stats[2] = rq[0];
+    stats[0] = r[0].n;
+    stats[1] = r[0].mean;
+    stats[2] = r[0].m2;
   }
 }
 
-// adv = (adv - mean) / (std + 1e-5) in fp32, mean/std from the (possibly
-// all-reduced) stats {count, S, Q}; std is unbiased (torch.std default).
+// adv = (adv - mean) / (std + 1e-5) in fp32, from the (possibly rank-merged)
+// stats {count, mean, M2}; std is unbiased (torch.std default): sqrt(M2 / (n - 1)).
 __global__ __launch_bounds__(256) void adv_normalize_kernel(float* __restrict__ adv, long long n,
                                                             const double* __restrict__ stats) {
   const double cnt = stats[0];
-  const double mean = stats[1] / cnt;
-  double var = (stats[2] - stats[1] * mean) / (cnt - 1.0);
+  const double mean = stats[1];
+  double var = stats[2] / (cnt - 1.0);
   if (var < 0.0) var = 0.0;
   const float mf = (float)mean;
   const float den = (float)sqrt(var) + 1e-5f;

@@ -34,8 +34,8 @@ def _worker(rank, world, port, out):
     val = (3 * rng.standard_normal((T + 1, N))).astype(np.float32)
     lanes = slice(rank * N // world, (rank + 1) * N // world)
     adv = (ret[:-1, lanes] - val[:-1, lanes]).astype(np.float32)
-    stats = torch.tensor([adv.size, adv.astype(np.float64).sum(), (adv.astype(np.float64) ** 2).sum()],
-                         dtype=torch.float64)
+    a64 = adv.astype(np.float64)
+    stats = torch.tensor([adv.size, a64.mean(), ((a64 - a64.mean()) ** 2).sum()], dtype=torch.float64)
     _dist.allreduce_stats(stats)
     mean, std = _dist.stats_mean_std(*stats.tolist())
     norm = (adv - np.float32(mean)) / (np.float32(std) + np.float32(1e-5))
@@ -65,3 +65,22 @@ def test_two_rank_protocol():
     assert err0 < 2e-6 and err1 < 2e-6          # global advantage normalisation
     assert np.array_equal(p0, p1)               # identical step on every rank
     assert np.allclose(l0, [1.5, 2.0, 3.0]) and np.allclose(l1, l0)
+
+
+def test_welford_merge_large_mean_shards():
+    """_dist.merge_moments (the rank merge of allreduce_stats, and the same update
+    as the GPU kernels' mom_merge) on shards whose mean is 1e6 times their spread:
+    count, mean and M2 match a two-pass float64 computation, where summed moments
+    (Σx, Σx²) would lose the variance to cancellation."""
+    from a2c_ppo_acktr import _dist
+    rng = np.random.default_rng(3)
+    shards = [1e5 + 0.01 * rng.standard_normal(n) for n in (1000, 37, 4096)]
+    parts = [torch.tensor([s.size, s.mean(), ((s - s.mean()) ** 2).sum()], dtype=torch.float64) for s in shards]
+    n, mean, m2 = _dist.merge_moments(parts).tolist()
+    allx = np.concatenate(shards)
+    ref_m2 = ((allx - allx.mean()) ** 2).sum()
+    assert n == allx.size
+    np.testing.assert_allclose(mean, allx.mean(), rtol=1e-15)
+    np.testing.assert_allclose(m2, ref_m2, rtol=1e-9)
+    naive = (allx ** 2).sum() - allx.sum() ** 2 / allx.size
+    assert abs(naive - ref_m2) / ref_m2 > 1e-6   # what the summed-moment form would have lost

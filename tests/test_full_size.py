@@ -63,7 +63,9 @@ def _check_returns(st, nv):
     np.testing.assert_allclose(adv.cpu().numpy(), ref, rtol=1e-6, atol=1e-6)
     mean, std = O.adv_stats(eret, ev)
     stats = st._adv_stats.cpu().numpy()
-    np.testing.assert_allclose(stats[1] / stats[0], mean, rtol=1e-6, atol=1e-9)
+    assert stats[0] == st.rewards.numel()   # {count, mean, M2} (Welford / Chan)
+    np.testing.assert_allclose(stats[1], mean, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(np.sqrt(stats[2] / (stats[0] - 1)), std, rtol=1e-5)
     return adv
 
 

@@ -62,7 +62,7 @@ def test_gae_fused_adv_vs_oracle(gpu, T, N):
     ret = torch.zeros(T + 1, N, device=gpu)
     adv = torch.zeros(T, N, device=gpu)
     nparts = H.call("ppo_gae_partials_count", N)
-    parts = torch.zeros(2 * nparts, dtype=torch.float64, device=gpu)
+    parts = torch.zeros(3 * nparts, dtype=torch.float64, device=gpu)
     stats = torch.zeros(3, dtype=torch.float64, device=gpu)
     H.call("ppo_compute_returns", rd.data_ptr(), vd.data_ptr(), md.data_ptr(), bmd.data_ptr(), nvd.data_ptr(),
            ret.data_ptr(), adv.data_ptr(), parts.data_ptr(), T, N, 0.99, 0.95, 1, 0, _s())
@@ -1513,7 +1513,7 @@ def test_gae_time_parallel_scan(gpu, use_gae, ptl, T, N):
     ret = torch.zeros(T + 1, N, device=gpu)
     adv = torch.zeros(T, N, device=gpu)
     nparts = H.call("ppo_gae_scan_partials_count", N)
-    parts = torch.zeros(2 * nparts, dtype=torch.float64, device=gpu)
+    parts = torch.zeros(3 * nparts, dtype=torch.float64, device=gpu)
     stats = torch.zeros(3, dtype=torch.float64, device=gpu)
     H.call("ppo_compute_returns_scan", rd.data_ptr(), vd.data_ptr(), md.data_ptr(), bmd.data_ptr(), nvd.data_ptr(),
            ret.data_ptr(), adv.data_ptr(), parts.data_ptr(), T, N, 0.99, 0.95, int(use_gae), int(ptl), _s())
@@ -1527,8 +1527,10 @@ def test_gae_time_parallel_scan(gpu, use_gae, ptl, T, N):
         assert np.array_equal(got[T], nv)                     # returns[T] = next_value
     d = got[:T].astype(np.float64) - v[:T]
     np.testing.assert_allclose(adv.cpu().numpy(), d, rtol=0, atol=2e-6 * scale)
-    st = stats.cpu().numpy()
-    np.testing.assert_allclose(st[1], d.sum(), rtol=1e-6, atol=1e-6 * scale * d.size)
+    st = stats.cpu().numpy()   # {count, mean, M2} (Welford / Chan)
+    assert st[0] == d.size
+    np.testing.assert_allclose(st[1], d.mean(), rtol=1e-6, atol=1e-6 * scale)
+    np.testing.assert_allclose(st[2], ((d - d.mean()) ** 2).sum(), rtol=1e-5)
 
 
 def test_storage_gae_mode_scan(gpu):

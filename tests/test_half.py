@@ -93,11 +93,16 @@ def test_half_minibatch_gradient_vs_float64(gpu, obs_dtype):
     grads1, _ = TR.minibatch_grads(p1, obs_u8, fl(st.actions), fl(st.action_log_probs), adv.reshape(-1),
                                    fl(st.value_preds), fl(st.returns), idx=idx, clip=HP["clip"],
                                    value_coef=HP["value_coef"], entropy_coef=HP["entropy_coef"])
-    p32 = TR.unflatten(flat1, H, dtype=torch.float32, device=gpu, requires_grad=True)
-    g32, _ = TR.minibatch_grads(p32, obs_u8, fl(st.actions), fl(st.action_log_probs), adv.reshape(-1),
-                                fl(st.value_preds), fl(st.returns), idx=idx, clip=HP["clip"],
+    # the yardstick: torch's fp32 autograd on the host CPU — the reference's own
+    # arithmetic (T/run.py trains on the CPU); deterministic on every box, unlike
+    # the GPU GEMM heuristics
+    cpu = torch.device("cpu")
+    p32 = TR.unflatten(flat1, H, dtype=torch.float32, device=cpu, requires_grad=True)
+    hc = lambda t: t.cpu()  # noqa: E731
+    g32, _ = TR.minibatch_grads(p32, hc(obs_u8), hc(fl(st.actions)), hc(fl(st.action_log_probs)), hc(adv.reshape(-1)),
+                                hc(fl(st.value_preds)), hc(fl(st.returns)), idx=idx.cpu(), clip=HP["clip"],
                                 value_coef=HP["value_coef"], entropy_coef=HP["entropy_coef"])
-    g32 = torch.cat([t.reshape(-1) for t in g32]).cpu().numpy()
+    g32 = torch.cat([t.reshape(-1) for t in g32]).numpy()
     # float observations (the fp16 plane widened to fp32 rows) take conv1's
     # image-resident split kernels (csrc/conv1f.hip): the same bar as u8 frames
     check_grads(cap32.grad.cpu().numpy(), grads1, O.cnn_param_shapes(H), fp32_flat=g32, floor=2e-5)
