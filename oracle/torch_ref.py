@@ -71,19 +71,24 @@ def conv_unfold(x, w, b, stride):
     return out.reshape(B, O, Ho, (Wx - k) // stride + 1)
 
 
-def trunk(p, x, conv=F.conv2d):
-    """CNNBase.main (model.py:176-180): x [B,C,84,84] -> features [B,H] (post-ReLU)"""
+def trunk(p, x, conv=F.conv2d, masks=None):
+    """CNNBase.main (model.py:176-180): x [B,C,84,84] -> features [B,H] (post-ReLU).
+    masks (optional, 4 tensors shaped like the four ReLU outputs): the ReLU
+    decisions to apply instead of (pre-activation > 0) — lets a reference take
+    another implementation's decisions so a gradient comparison measures
+    arithmetic, not which rows sit within a rounding of a ReLU boundary."""
     w1, b1, w2, b2, w3, b3, w4, b4 = p[:8]
-    h = F.relu(conv(x, w1, b1, 4))
-    h = F.relu(conv(h, w2, b2, 2))
-    h = F.relu(conv(h, w3, b3, 1))
-    return F.relu(F.linear(h.reshape(h.shape[0], -1), w4, b4))
+    relu = (lambda z, k: F.relu(z)) if masks is None else (lambda z, k: z * masks[k].to(z.dtype))  # noqa: E731
+    h = relu(conv(x, w1, b1, 4), 0)
+    h = relu(conv(h, w2, b2, 2), 1)
+    h = relu(conv(h, w3, b3, 1), 2)
+    return relu(F.linear(h.reshape(h.shape[0], -1), w4, b4), 3)
 
 
-def cnn_forward(p, x, conv=F.conv2d):
+def cnn_forward(p, x, conv=F.conv2d, masks=None):
     """CNNBase trunk + critic_linear (model.py:185-188) + Categorical's linear
     (distributions.py:54-68): x [B,C,84,84] float -> (value [B,1], logits [B,A])"""
-    h = trunk(p, x, conv)
+    h = trunk(p, x, conv, masks)
     wc, bc, wa, ba = p[8:]
     return F.linear(h, wc, bc), F.linear(h, wa, ba)
 
@@ -119,9 +124,9 @@ def compute_returns(rewards, value_preds, masks, next_value, gamma, gae_lambda):
 
 
 def ppo_loss(p, obs, actions, old_logp, adv, vpred, ret, clip, value_coef, entropy_coef,
-             use_clipped_value_loss=True, conv=F.conv2d):
+             use_clipped_value_loss=True, conv=F.conv2d, masks=None):
     """algo/ppo.py:57-81 for one minibatch -> (loss, value_loss, action_loss, entropy)"""
-    values, logits = cnn_forward(p, obs, conv)
+    values, logits = cnn_forward(p, obs, conv, masks)
     dist = torch.distributions.Categorical(logits=logits)
     logp = dist.log_prob(actions.squeeze(-1)).view(actions.size(0), -1).sum(-1).unsqueeze(-1)
     ent = dist.entropy().mean()
@@ -227,7 +232,7 @@ def _decode(obs, dev, dt):
 
 
 def minibatch_grads(p, obs_u8, actions, old_logp, adv, vpred, ret, *, clip, value_coef, entropy_coef,
-                    idx=None, chunk=2048, use_clipped_value_loss=True, conv=conv_unfold):
+                    idx=None, chunk=2048, use_clipped_value_loss=True, conv=conv_unfold, masks=None):
     """Gradient of the PPO minibatch loss (algo/ppo.py:57-81, mean over all B rows)
     with respect to p, by autograd, accumulated over row chunks: every loss term is
     a mean of per-row terms, so Σ_chunks of the chunk losses scaled by |chunk|/B has
@@ -244,8 +249,9 @@ def minibatch_grads(p, obs_u8, actions, old_logp, adv, vpred, ret, *, clip, valu
         rows = slice(s, e) if idx is None else idx[s:e].to(obs_u8.device)
         x = _decode(obs_u8[rows], dev, dt)
         f = lambda t: t[rows].to(dev, dt).reshape(-1, 1)  # noqa: E731
+        mk = None if masks is None else [m[s:e].to(dev) for m in masks]
         loss, vl, al, ent = ppo_loss(p, x, actions[rows].to(dev).reshape(-1, 1), f(old_logp), f(adv), f(vpred),
-                                     f(ret), clip, value_coef, entropy_coef, use_clipped_value_loss, conv)
+                                     f(ret), clip, value_coef, entropy_coef, use_clipped_value_loss, conv, mk)
         w = (e - s) / B
         g = torch.autograd.grad(loss * w, p)
         for acc, gi in zip(grads, g):
