@@ -234,3 +234,49 @@ def test_recurrent_minibatch_full_size(gpu):
     _check_grads(cap.grad.cpu().numpy(), [g[nm] for nm in names], shapes)
     np.testing.assert_allclose(loss[:3].cpu().numpy(), [lg["value_loss"], lg["action_loss"], lg["entropy"]],
                                rtol=2e-5, atol=1e-7)
+
+
+def test_recurrent_rollout_4096_lanes(gpu):
+    """c5's rollout width: 4096 lanes of GRU acting (H=256, V=14, episode ends
+    resetting the hidden state through masks) for 24 steps.  On a strided subset
+    of lanes the stored values, log-probs of the sampled actions and hidden states
+    vs the float64 forward (trunk -> GRU sequence with the stored masks ->
+    heads: model.py:116-165, 185-188; oracle.gru_sequence)."""
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import SyntheticVecEnv
+    N, T, H, V = 4096, 24, 256, 14
+    torch.manual_seed(5)
+    env = SyntheticVecEnv(N, seed=77, p_done=0.05, device=gpu)
+    pol = M.Policy((4, 84, 84), env.action_space, base=M.CNNBase, base_kwargs={"recurrent": True, "hidden_size": H},
+                   vector_obs_len=V)
+    flat0 = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).clone()
+    pol.to(gpu)
+    st = RolloutStorage(T, N, (4, 84, 84), [V], env.action_space, H, obs_dtype=torch.uint8, device=gpu)
+    env.reset_into(st.obs[0])
+    vec = torch.rand(N, V, generator=torch.Generator().manual_seed(8)).to(gpu)
+    st.vector_obs[0].copy_(vec)
+    _rollout(pol, st, env, T, vec=vec)
+    torch.cuda.synchronize()
+    masks = st.masks[:T, :, 0].cpu().numpy()
+    assert (masks == 0).sum() > 0                   # some lanes reset their hidden state
+    shapes = O.cnn_param_shapes(H, recurrent=True, vector_obs_len=V)
+    names = [nm for nm, _ in shapes]
+    p64 = O.unflatten(flat0.numpy(), shapes)
+    trunk_p = [torch.tensor(p64[nm], device=gpu) for nm in names[4:12]]
+    ns = np.arange(3, N, 61)
+    nsg = torch.from_numpy(ns).to(gpu)
+    with torch.no_grad():
+        obs = st.obs[:T][:, nsg].reshape(T * len(ns), 4, 84, 84)
+        feat = TR.trunk(trunk_p, obs.double() / 255.0, TR.conv_unfold).cpu().numpy()
+    x = np.concatenate([feat, np.broadcast_to(vec.cpu().numpy()[ns].astype(np.float64), (T, len(ns), V))
+                        .reshape(T * len(ns), V)], 1)
+    h0 = st.recurrent_hidden_states[0].cpu().numpy()[ns].astype(np.float64)
+    out, _ = O.gru_sequence(p64, x, h0, masks[:, ns].astype(np.float64))
+    value, logits = O.heads(p64, out)
+    acts = st.actions[:T][:, nsg].cpu().numpy().reshape(-1)
+    lp_ref = np.take_along_axis(O.categorical(logits)["norm_logits"], acts[:, None], 1)[:, 0]
+    np.testing.assert_allclose(st.recurrent_hidden_states[1:T + 1][:, nsg].cpu().numpy().reshape(-1, H),
+                               out, atol=1e-4)
+    np.testing.assert_allclose(st.value_preds[:T][:, nsg].cpu().numpy().reshape(-1), value, atol=1e-4)
+    np.testing.assert_allclose(st.action_log_probs[:T][:, nsg].cpu().numpy().reshape(-1), lp_ref, atol=1e-4)
