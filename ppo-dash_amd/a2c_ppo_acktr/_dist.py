@@ -9,7 +9,13 @@ RCCL over xGMI on ROCm.  Exchanges, all on the current stream:
                                       et al.) -> global advantage mean / unbiased
                                       std (ppo.py:36; Welford)
   per minibatch    allreduce_grads    Σ of the flat fp32 gradient; clip + Adam
-                                      then run on Σ/G (scale returned here)
+                                      then run on Σ/G (scale returned here) —
+                                      CNN policies in two buckets: the fc + heads
+                                      tail (92 % of the bytes, final once the fc
+                                      weight gradient is reduced) on a side stream,
+                                      overlapped with the conv backward, then the
+                                      conv head of the buffer (start_bucket, then
+                                      allreduce_grads finishes the buffer)
   once per update  allreduce_losses   mean of the 3 logged losses over ranks
 
 These helpers are plain torch.distributed calls so they run unchanged under
@@ -96,19 +102,75 @@ def grad_allreduce_times():
     return out
 
 
+def _timed_all_reduce(t):
+    if _TIMING["on"]:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dist.all_reduce(t)
+        e1.record()
+        _TIMING["events"].append((e0, e1, t.numel() * t.element_size()))
+    else:
+        dist.all_reduce(t)
+
+
+_OVERLAP = {"on": True, "stream": {}}
+# started tail buckets: end address of the tail -> (event or None, element count);
+# allreduce_grads of a buffer ending there waits for it and reduces only the rest,
+# so no caller can sum a tail twice
+_PENDING = {}
+
+
+def overlap_buckets(on=True):
+    """enable / disable the bucketed gradient all-reduce (start_bucket)"""
+    _OVERLAP["on"] = bool(on)
+
+
+def _end(t):
+    return t.data_ptr() + t.numel() * t.element_size()
+
+
+def start_bucket(tail):
+    """Start the all-reduce of a finished tail of the flat gradient on a side
+    stream, ordered after everything queued so far on the current stream (the
+    kernels that wrote it); the current stream goes on with the rest of the
+    backward, and the next allreduce_grads of the buffer that ends with this tail
+    waits for it and reduces only the head.  No-op without collectives."""
+    if not active() or not _OVERLAP["on"]:
+        return False
+    if not tail.is_cuda:   # host tensors (gloo): reduced in place now, only the split remains
+        _timed_all_reduce(tail)
+        _PENDING[_end(tail)] = (None, tail.numel())
+        return True
+    cur = torch.cuda.current_stream(tail.device)
+    side = _OVERLAP["stream"].get(tail.device)
+    if side is None:
+        side = _OVERLAP["stream"][tail.device] = torch.cuda.Stream(tail.device)
+    ready = torch.cuda.Event()
+    ready.record(cur)
+    side.wait_event(ready)
+    with torch.cuda.stream(side):
+        _timed_all_reduce(tail)
+        done = torch.cuda.Event()
+        done.record(side)
+    _PENDING[_end(tail)] = (done, tail.numel())
+    return True
+
+
 def allreduce_grads(grad):
     """Sum the flat gradient over ranks; returns the scale (1/G) that turns it
-    into the mean, applied inside the clip + Adam kernels."""
+    into the mean, applied inside the clip + Adam kernels.  A tail of grad already
+    started by start_bucket is waited for (on the current stream), not reduced again."""
     G = world_size()
     if active():
-        if _TIMING["on"]:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            dist.all_reduce(grad)
-            e1.record()
-            _TIMING["events"].append((e0, e1, grad.numel() * grad.element_size()))
+        pending = _PENDING.pop(_end(grad), None)
+        if pending is not None and pending[1] <= grad.numel():
+            done, n = pending
+            if done is not None:
+                torch.cuda.current_stream(grad.device).wait_event(done)
+            if grad.numel() > n:
+                _timed_all_reduce(grad[:grad.numel() - n])
         else:
-            dist.all_reduce(grad)
+            _timed_all_reduce(grad)
     return 1.0 / G
 
 

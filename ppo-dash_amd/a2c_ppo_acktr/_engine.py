@@ -20,6 +20,7 @@ import contextlib
 
 import torch
 
+from . import _dist
 from ._hip import call, ptr, stream
 
 FEAT = 32 * 7 * 7  # conv3 output, flattened
@@ -323,6 +324,10 @@ class CNNEngine:
         dz1 = ws.get("dz1", B * 400 * 32, device=dev)
         call("ppo_linear_dgrad_mask", dh.data_ptr(), B, self.H, self.pk(3), FEAT, a3.data_ptr(), dz3.data_ptr(), s)
         self._wgrad("fc", B, dh, a3, None, s)
+        # the fc + heads tail of the flat gradient (the last parameters in torch order,
+        # 92 % of the bytes at H = 512) is final here: its all-reduce (G > 1) overlaps
+        # the conv backward on a side stream (_dist.start_bucket); PPO's step waits for it
+        _dist.start_bucket(self.grad[self.offsets[self.W4]:])
         bits = getattr(self, "_mask_rows", None) == B   # masks of this minibatch's forward
         if bits and call("ppo_conv3_dgrad_bits_ok"):
             call("ppo_conv3_dgrad_bits", dz3.data_ptr(), B, self.pk(4), ws.bufs["m2bits"].data_ptr(), dz2.data_ptr(),

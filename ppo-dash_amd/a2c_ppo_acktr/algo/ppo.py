@@ -63,7 +63,7 @@ class FlatAdam(object):
         if self._partials is None or self._partials.device != eng.device:   # also after load_state_dict
             self._partials = torch.empty(call("ppo_grad_partials_count", n), dtype=torch.float64, device=eng.device)
             self._norm = torch.zeros(1, dtype=torch.float64, device=eng.device)
-        scale = _dist.allreduce_grads(eng.grad)
+        scale = _dist.allreduce_grads(eng.grad)   # (waits for the fc + heads bucket the backward started)
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         self.step_count += 1

@@ -321,7 +321,11 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
 // (k-group w >> 2 takes global k-steps ≡ w >> 2 mod 4): the dz fragments, the
 // same for every tile, are read from LDS half as often (the kernel is LDS-bound:
 // the staging writes and the fragment reads share the LDS with each other).
-template <int NPD = 3, int NW = 8, int TPW = 1>   // NPD: dz parts summed (3 exact; 1 half-precision mode)
+// BAL (NW = 16, ppo_tune_set("conv1_wgrad", 7)): the 720 staging items (400 E + 320 dz)
+// dealt 60 per wave to waves 0-11, so each SIMD (waves s, s+4, s+8, s+12) stages 180;
+// the round-2 map (E on waves 0-6, dz on 8-12) gave the SIMD of waves 0/4/8/12 four
+// items per lane and the one of 3/7/11/15 two — the busiest SIMD set the part time.
+template <int NPD = 3, int NW = 8, int TPW = 1, bool BAL = false>   // NPD: dz parts summed (3 exact; 1 half-precision mode)
 __global__ __launch_bounds__(NW * 64) void conv1_wgrad_parts_kernel(const float* __restrict__ dz1,
                                                                 const uint8_t* __restrict__ obs,
                                                                 const int64_t* __restrict__ idx, long long row0,
@@ -368,8 +372,11 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_parts_kernel(const float*
   // dz item tid < 320 (co = tid & 31, pixel octet oc = tid >> 5).  Threads without
   // an item DMA item 0's addresses (harmless duplicates) so every wave issues the
   // same DMA count.
-  const bool e_on = tid < 400, d_on = NW == 8 ? tid < 320 : tid >= 512 && tid < 832;
-  const int eit = e_on ? tid : 0, dit = d_on ? tid - (NW == 8 ? 0 : 512) : 0;
+  static_assert(!BAL || NW == 16, "balanced staging map: 16 waves");
+  const int bitem = wave < 12 && lane < 60 ? 60 * wave + lane : 720;   // BAL: item 0-399 E, 400-719 dz
+  const bool e_on = BAL ? bitem < 400 : tid < 400;
+  const bool d_on = BAL ? (bitem >= 400 && bitem < 720) : NW == 8 ? tid < 320 : tid >= 512 && tid < 832;
+  const int eit = e_on ? (BAL ? bitem : tid) : 0, dit = d_on ? (BAL ? bitem - 400 : tid - (NW == 8 ? 0 : 512)) : 0;
   const int er = eit / 5, eQ = eit - 5 * er, ec = er / ER, eyr = er - ER * ec, ef = (eit >> 1) & 7;
   const int dco = dit & 31, doc = dit >> 5;
   float bacc = 0.f;
@@ -1873,9 +1880,10 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
 // ---------------------------------------------------------------------------
 enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_X9,
-       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_FC_DGRAD, TK_FC_WGRAD, TK_N };
+       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_FC_DGRAD, TK_FC_WGRAD, TK_ORDER, TK_N };
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
-                                         "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad", "fc_dgrad", "fc_wgrad"};
+                                         "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad", "fc_dgrad", "fc_wgrad",
+                                         "order"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
@@ -1883,7 +1891,8 @@ static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measure
 // small_b: forwards of at most this many samples (images / linear rows) take the
 // small-batch path of small.hip (an output element per thread or wave, fp32 FMA)
 static int g_small_b = 4;
-static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
+// order: fc tile order override for A/B (0: per-layer default, 1: m fastest, 2: n fastest; igemm_x9.h tile_of)
+static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   if (strcmp(key, "small_b") == 0) {
@@ -1948,6 +1957,12 @@ using XP64 = CfgX<128, 64, 4, 1, true, true, false, false, false, true>;    // w
 using XP128 = CfgX<128, 128, 4, 1, true, true, false, false, false, true>;  // waves 32x128
 using XP128w8 = CfgX<128, 128, 8, 1, true, true, false, false, false, true>;      // 8 waves of 16x128
 using XP128x64w8 = CfgX<128, 64, 8, 1, true, true, false, false, false, true>;    // 8 waves of 16x64 (2 blocks/CU)
+// split-at-staging forms (igemm_x9s_kernel): operands split once per block into bf16 planes in LDS
+using SP128 = CfgS<128, 128, 4, 2, true, true, false, true>;     // 8 waves of 32x64, B planes (96 KB LDS)
+using SP256 = CfgS<256, 128, 4, 2, true, true, false, true>;     // 8 waves of 64x64, B planes (144 KB LDS)
+using SP128x64 = CfgS<128, 64, 4, 2, true, true, false, true>;   // 8 waves of 32x32, B planes (72 KB LDS)
+using SW256x128 = CfgS<256, 128, 4, 2, false, false, true>;      // wgrad: 8 waves of 64x64 (144 KB LDS)
+using SW128 = CfgS<128, 128, 2, 2, false, false, true>;          // wgrad: 4 waves of 64x64 (96 KB LDS)
 // x9 = 1: the split-bf16 core where it measured faster (forward GEMMs, fc dgrad); the gather-heavy
 // conv dgrads and the wgrads stay on fp32 MFMA (their split path is VALU-bound); x9 = 2: everywhere
 // compute units of the current device (persistent-kernel grid size)
@@ -2142,6 +2157,9 @@ PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float*
 
 #include "dense_x32.h"
 
+// tile order of an fc GEMM launch: the layer's measured default unless the "order" knob overrides it
+static int fc_order(int dflt) { return g_tune[TK_ORDER] ? g_tune[TK_ORDER] - 1 : dflt; }
+
 // CNNBase fc (model.py:181): out[m * ldo + n] = relu(x [M][1568] · W4p [H][1568]^T + b), W4p the packed
 // segment of ppo_pack_weights (its bf16 planes follow it)
 PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, int H, float* out, int ldo,
@@ -2168,9 +2186,13 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
     DenseReluFwd<CFG> p;                                                                             \
     p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1; \
     set_planes(p, w4p, (long long)H * K, H, K);                                                      \
+    p.n_fast = fc_order(1);                                                                          \
     return launch_x9(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);                      \
   }
     if (v == 5) PPO_FC(XP128x64w8)
+    if (v == 10) PPO_FC(SP128)      // split-at-staging forms: 0.69 / 0.62 / 0.70 vs 0.58 ms (slower)
+    if (v == 11) PPO_FC(SP256)
+    if (v == 12) PPO_FC(SP128x64)
     PPO_FC(XP128)
 #undef PPO_FC
   }
@@ -2281,8 +2303,11 @@ PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt
     DenseDgradMask<CFG> p;                                                          \
     p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;        \
     set_planes(p, wt, (long long)N * K, N, K);                                      \
+    p.n_fast = fc_order(0);                                                         \
     return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K); \
   }
+    if (g_tune[TK_FC_DGRAD] == 10) PPO_FCD(SP128)   // split-at-staging: 1.06 / 1.00 vs 0.74 ms (slower)
+    if (g_tune[TK_FC_DGRAD] == 11) PPO_FCD(SP256)
     PPO_FCD(XP128w8)   // measured: 0.75 vs 0.87 ms (XP128) at the c3 minibatch
 #undef PPO_FCD
   }
@@ -2406,7 +2431,8 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
   const long long R = (long long)B * 400;
   PPO_REQUIRE(R < 0x7fffffffLL, "ppo_conv1_wgrad: B too large");
   const double fl = 2.0 * R * 32 * C * 64;
-  if (obs_is_u8 && C == 4 && (g_tune[TK_CONV1_WGRAD] >= 3 && g_tune[TK_CONV1_WGRAD] <= 5)) {   // part-pipelined
+  if (obs_is_u8 && C == 4 && ((g_tune[TK_CONV1_WGRAD] >= 3 && g_tune[TK_CONV1_WGRAD] <= 5) ||
+                                g_tune[TK_CONV1_WGRAD] == 7)) {   // part-pipelined
     if (B <= 0 || Z <= 0) return 0;
     PPO_REQUIRE((B + Z - 1) / Z <= 512, "ppo_conv1_wgrad: %d images over %d blocks (at most 512 per block)", B, Z);
     int slot;
@@ -2423,6 +2449,9 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
     else if (g_tune[TK_CONV1_WGRAD] == 5)   // four waves per SIMD, two column tiles per wave
       conv1_wgrad_parts_kernel<3, 16, 2><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
                                                                             slab, slab_bias, g_stagger >> 4);
+    else if (g_tune[TK_CONV1_WGRAD] == 7)   // as 5, staging items balanced over the SIMDs
+      conv1_wgrad_parts_kernel<3, 16, 2, true><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0,
+                                                                                  B, slab, slab_bias, g_stagger >> 4);
     else
       conv1_wgrad_parts_kernel<3><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
                                                                     slab_bias, g_stagger >> 4);
@@ -2515,10 +2544,14 @@ PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int 
   {                                                                                 \
     DenseWgrad<CFG> p;                                                              \
     set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);                                  \
-    p.x = x; p.K = K;                                                               \
+    p.x = x; p.K = K; p.n_fast = fc_order(0);                                       \
     return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K); \
   }
-    PPO_FCW(XW256x128)   // measured: 0.79 vs 0.83 ms (XW128) at the c3 minibatch
+    // fc_wgrad tune: 0 / 10 split-at-staging 256 x 128 (default: 0.727 vs 0.775 ms at the c3
+    // minibatch), 11 split-at-staging 128 x 128 (0.945), 1 the in-loop-split XW256x128
+    if (g_tune[TK_FC_WGRAD] == 1) PPO_FCW(XW256x128)   // 0.79 vs 0.83 ms (XW128), round 2
+    if (g_tune[TK_FC_WGRAD] == 11) PPO_FCW(SW128)
+    PPO_FCW(SW256x128)
 #undef PPO_FCW
   }
   DenseWgrad<CfgWfc> p;

@@ -117,13 +117,17 @@ template <int BM_, int BN_, int WM_, int WN_, bool AKC, bool BKC, bool BIASA = f
 struct CfgX {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NT = 64 * WM_ * WN_, BK = 32;
   static constexpr bool A_KC = AKC, B_KC = BKC, BIAS_FROM_A = BIASA, TILE_EPI = false, B_TILE = false;
-  static constexpr bool A_EXACT = AX_, B_EXACT = BX_, B_PLANES = BP_;
+  static constexpr bool A_EXACT = AX_, B_EXACT = BX_, B_PLANES = BP_, SPLIT_STAGE = false;
   struct ACtx { const float* p; int a; int b; bool ok; };
   struct BCtx { const float* p; int a; bool ok; };
   // B_PLANES: plane p of B[n][k] at bpl[p * bps + n * bld + k] (bf16 bits), n < bnr, k < bld
   const uint16_t* bpl = nullptr;
   long long bps = 0;
   int bld = 0, bnr = 0;
+  // tile order (see igemm_x9_kernel): 1 = (z, m, n) n fastest per XCD, for an A operand
+  // larger than the Infinity Cache shared by N / BN tiles (fc forward); 0 = m fastest
+  // (each XCD sweeps its m range at one n: B tile L2-resident, A from the Infinity Cache)
+  int n_fast = 0;
 };
 
 // LDS swizzles for the 16x16x32 fragment reads.  ds_read_b128 serves a wave in
@@ -147,6 +151,31 @@ __device__ __forceinline__ int pl_off(int row, int q) {   // bf16 element offset
   return row * 32 + 8 * (q ^ ((H4 >> (4 * ((row >> 2) & 3))) & 3));
 }
 
+// Block -> (m0, n0, z) tile.  n_fast 0: m = xcd_remap(blockIdx.x) (each XCD a
+// contiguous m range), n = blockIdx.y, z = blockIdx.z — the dispatcher walks all m
+// at one n before the next n, so the B tile stays L2-resident and A (if it fits the
+// 256 MB Infinity Cache) is re-read from there.  n_fast 1: (z, m, n) with n fastest,
+// dealt out by xcd_remap of the linear block id so the N / BN tiles that share an
+// A row tile (and the tiles of one split-K slice, which share its rows) run at the
+// same time on one XCD and read the common operand from that XCD's L2 — for an A
+// operand larger than the Infinity Cache (fc forward: 411 MB, re-streamed from HBM
+// by each of the 4 tile columns with n_fast 0: 0.625 -> 0.56 ms).
+__device__ __forceinline__ void tile_of(int n_fast, int BM, int BN, int& m0, int& n0, int& z) {
+  if (!n_fast) {
+    m0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
+    n0 = blockIdx.y * BN;
+    z = blockIdx.z;
+    return;
+  }
+  const int gx = (int)gridDim.x, gy = (int)gridDim.y, mn = gx * gy;
+  const int lin = (int)blockIdx.x + gx * ((int)blockIdx.y + gy * (int)blockIdx.z);
+  const int t = xcd_remap(lin, mn * (int)gridDim.z);
+  z = t / mn;
+  const int r = t - z * mn, mt = r / gy;
+  m0 = mt * BM;
+  n0 = (r - mt * gy) * BN;
+}
+
 template <class P, int NP>
 __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
   constexpr int BM = P::BM, BN = P::BN, NT = P::NT, WM = P::WM, WN = P::WN, BK = 32;
@@ -165,9 +194,8 @@ __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
-  const int n0 = blockIdx.y * BN;
-  const int z = blockIdx.z;
+  int m0, n0, z;
+  tile_of(p.n_fast, BM, BN, m0, n0, z);
   int kbeg, kend;
   p.k_range(z, kbeg, kend);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
@@ -306,7 +334,7 @@ __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
     if constexpr (P::BIAS_FROM_A) {   // db partial: thread sums BK/G k of one A row
       static_assert(NT % BM == 0 && BK % (NT / BM) == 0, "bias partials");
       constexpr int G = NT / BM;
-      if (blockIdx.y == 0) {
+      if (n0 == 0) {
         const int row = tid % BM;
 #pragma unroll
         for (int k = (tid / BM) * 4; k < BK; k += 4 * G) {
@@ -354,7 +382,7 @@ __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
       for (int r = 0; r < 4; ++r)
         p.store(m0 + (wm * TM + i) * 16 + 4 * fg + r, n0 + (wn * TN + j) * 16 + fr, z, acc[i][j][r]);
   if constexpr (P::BIAS_FROM_A) {
-    if (blockIdx.y == 0) {   // fixed-order combine of the G partials of each row
+    if (n0 == 0) {   // fixed-order combine of the G partials of each row
       constexpr int G = NT / BM;
       smem[tid] = bias_acc;   // the main loop ended on a barrier
       __syncthreads();
@@ -364,6 +392,229 @@ __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
         for (int g = 1; g < G; ++g) t += smem[g * BM + tid];
         p.store_bias(m0 + tid, z, t);
       }
+    }
+  }
+}
+
+// Split-at-staging form (igemm_x9s_kernel, configs CfgS): the fp32 operands are
+// split ONCE per block, while they are staged, into three bf16 planes in LDS
+// (64-B rows, pl_off swizzle), and the k loop reads plain bf16 fragments — no
+// split VALU in the k loop, and no operand split again by every wave that reads
+// it (igemm_x9_kernel splits each fragment in each wave: with WM x WN waves a B
+// row is split WM times; the fc weight gradient's 4 x 2 waves split B 4x and A 2x
+// per k-step, which made it VALU-issue-bound, 0.32 of the MFMA roofline).
+//   KC operand (row-contiguous k): unit = one row x 8 k (two 16-B loads);
+//   non-KC operand (wgrad: k = sample row): unit = 4 rows x 8 k (eight 16-B loads
+//   of 4 consecutive rows at one k), transposed while split.
+// A and B units are dealt to threads from opposite ends so that the threads the A
+// units leave idle take the B units.  BIAS_FROM_A (wgrad bias partial): each
+// thread sums its A unit's 4 rows over its 8 k per step; the four k-groups of a row
+// are combined in a fixed order at the end.
+template <int BM_, int BN_, int WM_, int WN_, bool AKC, bool BKC, bool BIASA = false, bool BP_ = false>
+struct CfgS : CfgX<BM_, BN_, WM_, WN_, AKC, BKC, BIASA, false, false, BP_> {
+  static constexpr bool SPLIT_STAGE = true;
+};
+
+template <class P, int NP>
+__global__ __launch_bounds__(P::NT) void igemm_x9s_kernel(const P p) {
+  constexpr int BM = P::BM, BN = P::BN, NT = P::NT, WM = P::WM, WN = P::WN, BK = 32;
+  constexpr int TM = BM / (16 * WM), TN = BN / (16 * WN);
+  static_assert(TM * 16 * WM == BM && TN * 16 * WN == BN && WM * WN * 64 == NT, "tile config");
+  static_assert(!P::A_EXACT && !P::B_EXACT, "split staging: fp32 operands");
+  constexpr bool BPL = P::B_PLANES, AKC = P::A_KC, BKC = P::B_KC;
+  constexpr int NPL = NP == 1 ? 1 : 3;                      // planes staged
+  constexpr int PA = BM * BK, PB = BN * BK;                 // bf16 elements per plane
+  constexpr int STAGE = NPL * PA + (BPL ? 3 : NPL) * PB;    // bf16 elements per stage
+  constexpr int UA = AKC ? BM * 4 : (BM / 4) * 4;
+  constexpr int UB = BPL ? BN * 12 : BKC ? BN * 4 : (BN / 4) * 4;
+  constexpr int NUA = (UA + NT - 1) / NT, NUB = (UB + NT - 1) / NT;
+  constexpr int LA = AKC ? 2 : 8, LB = BPL ? 1 : BKC ? 2 : 8;
+  constexpr int BOFF = (NT - UA % NT) % NT;                 // B units start where the A units end
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * STAGE];
+  static_assert(!P::BIAS_FROM_A || (!AKC && UA <= NT && BM * 8 <= 2 * STAGE), "bias partials: wgrad layout");
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  int m0, n0, z;
+  tile_of(p.n_fast, BM, BN, m0, n0, z);
+  int kbeg, kend;
+  p.k_range(z, kbeg, kend);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  typename P::ACtx actx[NUA];
+  typename P::BCtx bctx[NUB];
+  int ak[NUA], arow[NUA], bk[NUB], brow[NUB];
+  bool aon[NUA], bon[NUB];
+#pragma unroll
+  for (int i = 0; i < NUA; ++i) {
+    const int u = tid + i * NT;
+    aon[i] = u < UA;
+    if constexpr (AKC) {
+      arow[i] = u >> 2;
+      ak[i] = 8 * (u & 3);
+    } else {
+      arow[i] = 4 * (u % (BM / 4));
+      ak[i] = 8 * (u / (BM / 4));
+    }
+    actx[i] = p.a_ctx(m0 + (aon[i] ? arow[i] : 0), z);
+  }
+#pragma unroll
+  for (int i = 0; i < NUB; ++i) {
+    const int u = (tid + BOFF) % NT + i * NT;
+    bon[i] = u < UB;
+    if constexpr (BPL) {   // brow = plane row, bk = plane * 4 + 16-B chunk
+      brow[i] = (u % (BN * 4)) / 4;
+      bk[i] = (u / (BN * 4)) * 4 + u % 4;
+      bctx[i] = typename P::BCtx{};
+      continue;
+    }
+    if constexpr (BKC) {
+      brow[i] = u >> 2;
+      bk[i] = 8 * (u & 3);
+    } else {
+      brow[i] = 4 * (u % (BN / 4));
+      bk[i] = 8 * (u / (BN / 4));
+    }
+    bctx[i] = p.b_ctx(n0 + (bon[i] ? brow[i] : 0), z);
+  }
+
+  using ARaw = decltype(p.a_load(actx[0], 0));
+  auto bload = [&](int i, int k) {
+    if constexpr (BPL) {   // k = k0 + bk[i]: plane bk >> 2, chunk bk & 3
+      const int n = n0 + brow[i], pl = (k - (k & ~(BK - 1))) >> 2, kk = (k & ~(BK - 1)) + 8 * (k & 3);
+      if (n >= p.bnr || kk >= p.bld) return uint4{0u, 0u, 0u, 0u};
+      return *reinterpret_cast<const uint4*>(p.bpl + pl * p.bps + (long long)n * p.bld + kk);
+    } else {
+      return p.b_load(bctx[i], k);
+    }
+  };
+  using BRaw = decltype(bload(0, 0));
+  ARaw ra[NUA][LA];
+  BRaw rb[NUB][LB];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < NUA; ++i)
+#pragma unroll
+      for (int j = 0; j < LA; ++j) ra[i][j] = aon[i] ? p.a_load(actx[i], k0 + ak[i] + (AKC ? 4 * j : j)) : ARaw{};
+#pragma unroll
+    for (int i = 0; i < NUB; ++i)
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        if constexpr (BPL) rb[i][j] = bon[i] ? bload(i, k0 + bk[i]) : BRaw{};
+        else rb[i][j] = bon[i] ? bload(i, k0 + bk[i] + (BKC ? 4 * j : j)) : BRaw{};
+      }
+  };
+  float bias_acc[4] = {0.f, 0.f, 0.f, 0.f};   // BIAS_FROM_A: rows arow[0] + q, this thread's k-group
+  // 8 fp32 (k-ordered) -> the planes of one 16-B chunk of row `row`
+  auto put8 = [&](uint16_t* S, int pstride, int row, int q, const f32x4& x0, const f32x4& x1) {
+    Frag3 f;
+    split8(x0, x1, f, NP == 1);
+    const int o = pl_off(row, q);
+    *reinterpret_cast<bf16x8*>(S + o) = f.h;
+    if constexpr (NPL == 3) {
+      *reinterpret_cast<bf16x8*>(S + pstride + o) = f.m;
+      *reinterpret_cast<bf16x8*>(S + 2 * pstride + o) = f.l;
+    }
+  };
+  auto sstore = [&](int buf, bool bias_on) {
+    uint16_t* As = smem + buf * STAGE;
+    uint16_t* Bs = As + NPL * PA;
+#pragma unroll
+    for (int i = 0; i < NUA; ++i) {
+      if (!aon[i]) continue;
+      if constexpr (AKC) {
+        put8(As, PA, arow[i], ak[i] >> 3, to_f32x4(ra[i][0]), to_f32x4(ra[i][1]));
+      } else {
+        f32x4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = to_f32x4(ra[i][j]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 x0 = {v[0][q], v[1][q], v[2][q], v[3][q]}, x1 = {v[4][q], v[5][q], v[6][q], v[7][q]};
+          put8(As, PA, arow[i] + q, ak[i] >> 3, x0, x1);
+          if constexpr (P::BIAS_FROM_A)
+            if (bias_on) bias_acc[q] += ((x0[0] + x0[1]) + (x0[2] + x0[3])) + ((x1[0] + x1[1]) + (x1[2] + x1[3]));
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NUB; ++i) {
+      if (!bon[i]) continue;
+      if constexpr (BPL) {
+        *reinterpret_cast<uint4*>(Bs + (bk[i] >> 2) * PB + pl_off(brow[i], bk[i] & 3)) = rb[i][0];
+      } else if constexpr (BKC) {
+        put8(Bs, PB, brow[i], bk[i] >> 3, to_f32x4(rb[i][0]), to_f32x4(rb[i][1]));
+      } else {
+        f32x4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = to_f32x4(rb[i][j]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          put8(Bs, PB, brow[i] + q, bk[i] >> 3, f32x4{v[0][q], v[1][q], v[2][q], v[3][q]},
+               f32x4{v[4][q], v[5][q], v[6][q], v[7][q]});
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero4();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const bool bias_on = P::BIAS_FROM_A && n0 == 0;
+  if (nk > 0) {
+    gload(kbeg);
+    sstore(0, bias_on);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kbeg + (kt + 1) * BK);
+    const uint16_t* As = smem + buf * STAGE;
+    const uint16_t* Bs = As + NPL * PA;
+    Frag3 fb[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int o = pl_off((wn * TN + j) * 16 + fr, fg);
+      fb[j].h = *reinterpret_cast<const bf16x8*>(Bs + o);
+      if constexpr (NPL == 3) {
+        fb[j].m = *reinterpret_cast<const bf16x8*>(Bs + PB + o);
+        fb[j].l = *reinterpret_cast<const bf16x8*>(Bs + 2 * PB + o);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int o = pl_off((wm * TM + i) * 16 + fr, fg);
+      Frag3 fa;
+      fa.h = *reinterpret_cast<const bf16x8*>(As + o);
+      if constexpr (NPL == 3) {
+        fa.m = *reinterpret_cast<const bf16x8*>(As + PA + o);
+        fa.l = *reinterpret_cast<const bf16x8*>(As + 2 * PA + o);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mma9<false, false, NP>(fa, fb[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1, bias_on);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        p.store(m0 + (wm * TM + i) * 16 + 4 * fg + r, n0 + (wn * TN + j) * 16 + fr, z, acc[i][j][r]);
+  if constexpr (P::BIAS_FROM_A) {
+    if (bias_on) {   // row r: its four k-groups' partials, fixed order (k0 + k1) + (k2 + k3)
+      float* red = reinterpret_cast<float*>(smem);   // the main loop ended on a barrier
+      if (aon[0])
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[(ak[0] >> 3) * BM + arow[0] + q] = bias_acc[q];
+      __syncthreads();
+      if (tid < BM) p.store_bias(m0 + tid, z, (red[tid] + red[BM + tid]) + (red[2 * BM + tid] + red[3 * BM + tid]));
     }
   }
 }
@@ -379,9 +630,15 @@ int launch_x9(const P& p, long long M, int N, int Z, hipStream_t st, const char*
   dim3 grid((unsigned)gx, (unsigned)((N + P::BN - 1) / P::BN), (unsigned)Z);
   int slot;
   const bool prof = ppo_prof_begin(name, st, &slot);
-  if (g_products == 9) igemm_x9_kernel<P, 9><<<grid, P::NT, 0, st>>>(p);
-  else if (g_products == 1) igemm_x9_kernel<P, 1><<<grid, P::NT, 0, st>>>(p);
-  else igemm_x9_kernel<P, 6><<<grid, P::NT, 0, st>>>(p);
+  if constexpr (P::SPLIT_STAGE) {
+    if (g_products == 9) igemm_x9s_kernel<P, 9><<<grid, P::NT, 0, st>>>(p);
+    else if (g_products == 1) igemm_x9s_kernel<P, 1><<<grid, P::NT, 0, st>>>(p);
+    else igemm_x9s_kernel<P, 6><<<grid, P::NT, 0, st>>>(p);
+  } else {
+    if (g_products == 9) igemm_x9_kernel<P, 9><<<grid, P::NT, 0, st>>>(p);
+    else if (g_products == 1) igemm_x9_kernel<P, 1><<<grid, P::NT, 0, st>>>(p);
+    else igemm_x9_kernel<P, 6><<<grid, P::NT, 0, st>>>(p);
+  }
   if (prof) ppo_prof_end(slot, st, flops);
   PPO_LAUNCH_CHECK(name);
   return 0;

@@ -1,5 +1,7 @@
 """CNNBase fc GEMMs (GPU): the 32x32x16 LDS-DMA kernel of csrc/dense_x32.h
-(ppo_tune_set("fc_fwd" / "fc_dgrad", 6)) and the generic tile core, through the
+(ppo_tune_set("fc_fwd" / "fc_dgrad", 6)), the split-at-staging tile kernel
+(igemm_x9s_kernel: fc_fwd 10-12, fc_dgrad 10-11, fc_wgrad 10-11; both tile
+orders) and the generic tile core, through the
 C ABI, vs torch float64 — the fc forward (model.py:181, Linear(32*7*7, H) + ReLU)
 and its input gradient masked by conv3's ReLU (threshold_backward of the
 flatten/ReLU in CNNBase.main).  Bar: 1e-5 of max|ref| with the fp32-accurate
@@ -50,7 +52,7 @@ def _with_tune(key, value, products, fn):
         H_.call("ppo_tune_set", b"products", oldp)
 
 
-@pytest.mark.parametrize("variant", [0, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 6, 7, 8, 10, 11, 12])
 @pytest.mark.parametrize("products", [6, 9, 1])
 @pytest.mark.parametrize("B,H", [(300, 512), (77, 64), (129, 256)])
 def test_fc_fwd_vs_float64(gpu, variant, products, B, H):
@@ -74,7 +76,7 @@ def test_fc_fwd_vs_float64(gpu, variant, products, B, H):
     assert torch.isnan(out[:, H:]).all()   # the padding columns are untouched
 
 
-@pytest.mark.parametrize("variant", [0, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 6, 7, 8, 10, 11])
 @pytest.mark.parametrize("products", [6, 9, 1])
 @pytest.mark.parametrize("B,H", [(300, 512), (77, 64)])
 def test_fc_dgrad_mask_vs_float64(gpu, variant, products, B, H):
@@ -95,3 +97,35 @@ def test_fc_dgrad_mask_vs_float64(gpu, variant, products, B, H):
     err = (got - ref).abs().max().item()
     assert err <= tol * ref.abs().max().item(), err
     assert (got[a3 <= 0] == 0).all()
+
+
+@pytest.mark.parametrize("variant,order", [(0, 0), (1, 0), (10, 1), (10, 2), (11, 0)])
+@pytest.mark.parametrize("products", [6, 1])
+@pytest.mark.parametrize("R,H", [(1000, 512), (333, 256)])
+def test_fc_wgrad_vs_float64(gpu, variant, order, products, R, H):
+    """dW[n][k] = Σ_r dh[r][n] a3[r][k] and db[n] = Σ_r dh[r][n] (the fc layer's
+    weight gradient, model.py:181 under loss.backward()): split-K slabs over the
+    rows, reduced in a fixed order; R not a multiple of the 32-row k-step."""
+    H_ = _hip()
+    g = torch.Generator().manual_seed(R + H)
+    dh = torch.randn(R, H, generator=g)
+    a3 = torch.relu(torch.randn(R, 1568, generator=g))
+    Z = 7
+    slab = torch.full((Z * H * 1568,), float("nan"), device=gpu)
+    slab_b = torch.full((Z * H,), float("nan"), device=gpu)
+    dhd, a3d = dh.cuda(), a3.cuda()
+    old = H_.call("ppo_tune_get", b"order")
+    H_.call("ppo_tune_set", b"order", order)
+    try:
+        _with_tune(b"fc_wgrad", variant, products,
+                   lambda: H_.call("ppo_linear_wgrad", dhd.data_ptr(), a3d.data_ptr(), R, H, 1568, Z, slab.data_ptr(),
+                                   slab_b.data_ptr(), _s()))
+    finally:
+        H_.call("ppo_tune_set", b"order", old)
+    gw = slab.view(Z, H, 1568).sum(0).cpu().double()
+    gb = slab_b.view(Z, H).sum(0).cpu().double()
+    ref_w = dh.double().t() @ a3.double()
+    ref_b = dh.double().sum(0)
+    tol = 1e-5 if products != 1 else 2e-2
+    assert (gw - ref_w).abs().max().item() <= tol * ref_w.abs().max().item()
+    assert (gb - ref_b).abs().max().item() <= 1e-5 * ref_b.abs().max().item()

@@ -48,6 +48,12 @@ def _worker(rank, world, port, out):
     g = g_local.clone()
     scale = _dist.allreduce_grads(g)
     gmean = (g.numpy() * scale).astype(np.float64)
+    # the bucketed form (tail reduced first, as the CNN engines do after the fc weight
+    # gradient, then the head) gives the same sum
+    gb = g_local.clone()
+    assert _dist.start_bucket(gb[30:])
+    assert _dist.allreduce_grads(gb) == scale   # reduces the head only
+    assert torch.equal(gb, g)
     p1, *_ = O.clip_adam(params.numpy().astype(np.float64), gmean, np.zeros(P), np.zeros(P), 1, 1e-3, 1e-5, 0.5)
     losses = torch.tensor([1.0 + rank, 2.0, 3.0], dtype=torch.float64)
     _dist.allreduce_losses(losses)

@@ -6,7 +6,8 @@ all-reduce) forced through a one-rank RCCL communicator, interleaved with the
 engine's raw-stream launches.  A one-rank sum is exact, so one c3 iteration
 must give bit-identical parameters, Adam moments and losses with and without
 the collectives — which fails if RCCL ran out of stream order with the kernels
-that produce or consume the gradient."""
+that produce or consume the gradient (the fc + heads bucket is reduced on a side
+stream while the conv backward runs, _dist.start_bucket)."""
 import os
 import subprocess
 import sys
@@ -28,7 +29,8 @@ def test_forced_rccl_iteration_bit_identical(tmp_path, gpu):
         assert r.returncode == 0, r.stderr[-3000:]
         outs.append(np.load(out))
     a, b = outs
-    assert a["allreduces"].size == 0 and b["allreduces"].size == 3 * 8   # one per minibatch
+    # two per minibatch: the fc + heads bucket on the side stream, then the conv head
+    assert a["allreduces"].size == 0 and b["allreduces"].size == 2 * 3 * 8
     for k in ("flat", "m", "v", "losses"):
         assert np.array_equal(a[k], b[k]), (k, np.abs(a[k] - b[k]).max())
     print("per-minibatch RCCL all-reduce ms:", np.round(b["allreduces"], 4).tolist())

@@ -1,7 +1,8 @@
 #!/bin/bash
-# full GPU suite + smoke + c3 bench (+ forced-RCCL bench); logs under gpurun_out/
 set -e
 mkdir -p gpurun_out
+timeout -k 10 120 python -u tools/kbench.py --reps 5 --only conv1_fwd_f32 > gpurun_out/kb_f32.log 2>&1
+timeout -k 10 120 python -u tools/kbench.py --reps 5 --only conv1_fwd_f32 --tune conv1_fwd=6 >> gpurun_out/kb_f32.log 2>&1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_all.log 2>&1
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 > gpurun_out/b_u8.log 2>&1
