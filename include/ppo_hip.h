@@ -155,6 +155,13 @@ int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, flo
 /* model.py:181 CNNBase fc + ReLU from the packed W4p segment (ppo_pack_weights; its bf16 planes follow it):
  * out[m * ldo + n] = relu(x[m] · W4p[n] + b[n]), x [M][1568] (p, c) order */
 int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, int H, float* out, int ldo, void* stream);
+/* the same with a caller-owned workspace: rollout-sized M (M * H <= 4096 * 1024) runs
+ * split-K (ppo_tune_set("fc_splitk", Z) slices, default 2) into ws and a fixed-order
+ * reduce + bias + ReLU; ws_bytes below ppo_fc_fwd_ws_bytes(M, H) (0: no split) falls
+ * back to ppo_fc_fwd */
+long long ppo_fc_fwd_ws_bytes(int M, int H);
+int ppo_fc_fwd_ws(const float* x, int M, const float* w4p, const float* b, int H, float* out, int ldo, float* ws,
+                  long long ws_bytes, void* stream);
 int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, const float* b, int N, float* out,
                         void* stream);
 /* Linear with row strides, optional A-row gather, bias and activation

@@ -249,7 +249,13 @@ class CNNEngine:
             self._conv1(obs, idx, B, a1, None, s)
             call("ppo_conv2_fwd", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), s)
         call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
-        call("ppo_fc_fwd", a3.data_ptr(), B, self.pk(2), self.pv(self.B4), self.H, out.data_ptr(), ldo, s)
+        nb = call("ppo_fc_fwd_ws_bytes", B, self.H)   # rollout-sized B: split-K into a workspace slab
+        if nb:
+            fws = ws.get("fc_ws", nb // 4, device=dev)
+            call("ppo_fc_fwd_ws", a3.data_ptr(), B, self.pk(2), self.pv(self.B4), self.H, out.data_ptr(), ldo,
+                 fws.data_ptr(), nb, s)
+        else:
+            call("ppo_fc_fwd", a3.data_ptr(), B, self.pk(2), self.pv(self.B4), self.H, out.data_ptr(), ldo, s)
         return out
 
     def _check_obs(self, obs):

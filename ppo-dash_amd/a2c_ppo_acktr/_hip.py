@@ -55,6 +55,8 @@ SIGNATURES = {
     "ppo_conv3_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_linear_relu_fwd": [c_p, c_int, c_int, c_p, c_p, c_int, c_p, c_p],
     "ppo_fc_fwd": [c_p, c_int, c_p, c_p, c_int, c_p, c_int, c_p],
+    "ppo_fc_fwd_ws_bytes": [c_int, c_int],
+    "ppo_fc_fwd_ws": [c_p, c_int, c_p, c_p, c_int, c_p, c_int, c_p, c_ll, c_p],
     "ppo_linear_dgrad_mask": [c_p, c_int, c_int, c_p, c_int, c_p, c_p, c_p],
     "ppo_conv3_dgrad": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv3_dgrad_bits_ok": [],
@@ -112,10 +114,10 @@ SIGNATURES = {
     "ppo_clip_adam_guarded": [c_p, c_p, c_p, c_p, c_ll, c_p, c_f, c_d, c_d, c_d, c_d, c_d, c_ll, c_p, c_p, c_p, c_p,
                               c_p],
 }
-_RESTYPES = {"ppo_last_error": ctypes.c_char_p, "ppo_packed_weights_size": c_ll}
+_RESTYPES = {"ppo_last_error": ctypes.c_char_p, "ppo_packed_weights_size": c_ll, "ppo_fc_fwd_ws_bytes": c_ll}
 # functions whose int return value is a result, not a status
 _VALUE_FUNCS = {"ppo_abi_version", "ppo_gae_partials_count", "ppo_gae_scan_partials_count", "ppo_adv_diff_partials_count",
-                "ppo_packed_weights_size", "ppo_wgrad_splits", "ppo_heads_train_blocks", "ppo_grad_partials_count",
+                "ppo_packed_weights_size", "ppo_fc_fwd_ws_bytes", "ppo_wgrad_splits", "ppo_heads_train_blocks", "ppo_grad_partials_count",
                 "ppo_conv2_dgrad_bits_ok", "ppo_conv3_dgrad_bits_ok", "ppo_tune_get",
                 "ppo_gru_persist_get", "ppo_gru_persist_timeouts", "ppo_gru_seq_counters"}
 

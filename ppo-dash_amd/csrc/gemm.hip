@@ -321,11 +321,7 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
 // (k-group w >> 2 takes global k-steps ≡ w >> 2 mod 4): the dz fragments, the
 // same for every tile, are read from LDS half as often (the kernel is LDS-bound:
 // the staging writes and the fragment reads share the LDS with each other).
-// BAL (NW = 16, ppo_tune_set("conv1_wgrad", 7)): the 720 staging items (400 E + 320 dz)
-// dealt 60 per wave to waves 0-11, so each SIMD (waves s, s+4, s+8, s+12) stages 180;
-// the round-2 map (E on waves 0-6, dz on 8-12) gave the SIMD of waves 0/4/8/12 four
-// items per lane and the one of 3/7/11/15 two — the busiest SIMD set the part time.
-template <int NPD = 3, int NW = 8, int TPW = 1, bool BAL = false>   // NPD: dz parts summed (3 exact; 1 half-precision mode)
+template <int NPD = 3, int NW = 8, int TPW = 1>   // NPD: dz parts summed (3 exact; 1 half-precision mode)
 __global__ __launch_bounds__(NW * 64) void conv1_wgrad_parts_kernel(const float* __restrict__ dz1,
                                                                 const uint8_t* __restrict__ obs,
                                                                 const int64_t* __restrict__ idx, long long row0,
@@ -372,11 +368,8 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_parts_kernel(const float*
   // dz item tid < 320 (co = tid & 31, pixel octet oc = tid >> 5).  Threads without
   // an item DMA item 0's addresses (harmless duplicates) so every wave issues the
   // same DMA count.
-  static_assert(!BAL || NW == 16, "balanced staging map: 16 waves");
-  const int bitem = wave < 12 && lane < 60 ? 60 * wave + lane : 720;   // BAL: item 0-399 E, 400-719 dz
-  const bool e_on = BAL ? bitem < 400 : tid < 400;
-  const bool d_on = BAL ? (bitem >= 400 && bitem < 720) : NW == 8 ? tid < 320 : tid >= 512 && tid < 832;
-  const int eit = e_on ? (BAL ? bitem : tid) : 0, dit = d_on ? (BAL ? bitem - 400 : tid - (NW == 8 ? 0 : 512)) : 0;
+  const bool e_on = tid < 400, d_on = NW == 8 ? tid < 320 : tid >= 512 && tid < 832;
+  const int eit = e_on ? tid : 0, dit = d_on ? tid - (NW == 8 ? 0 : 512) : 0;
   const int er = eit / 5, eQ = eit - 5 * er, ec = er / ER, eyr = er - ER * ec, ef = (eit >> 1) & 7;
   const int dco = dit & 31, doc = dit >> 5;
   float bacc = 0.f;
@@ -1880,10 +1873,10 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
 // ---------------------------------------------------------------------------
 enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_X9,
-       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_FC_DGRAD, TK_FC_WGRAD, TK_ORDER, TK_N };
+       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_FC_DGRAD, TK_FC_WGRAD, TK_ORDER, TK_FC_SPLITK, TK_N };
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
                                          "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad", "fc_dgrad", "fc_wgrad",
-                                         "order"};
+                                         "order", "fc_splitk"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
@@ -1892,7 +1885,8 @@ static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measure
 // small-batch path of small.hip (an output element per thread or wave, fp32 FMA)
 static int g_small_b = 4;
 // order: fc tile order override for A/B (0: per-layer default, 1: m fastest, 2: n fastest; igemm_x9.h tile_of)
-static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
+// fc_splitk: K slices of the rollout-sized fc forward with a workspace (ppo_fc_fwd_ws; <= 1: unsplit)
+static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0, 0, 2};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 PPO_API int ppo_tune_set(const char* key, int value) {
   if (strcmp(key, "small_b") == 0) {
@@ -2201,6 +2195,73 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
   return launch(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);
 }
 
+// Split-K fc forward for rollout-sized M (4,096 rows): 49 k-steps of one 128 x 64 tile
+// per CU are latency-bound (0.28 of the MFMA roofline); Z K-slices run Z blocks per
+// tile (two resident per CU), their partials go to the caller's workspace slab
+// [Z][M][H] and fc_splitk_reduce_kernel sums them in a fixed order, adds the bias
+// and applies ReLU.
+template <class C_>
+struct DenseFwdSplitK : DenseReluFwd<C_> {
+  float* slab = nullptr;
+  int chunk = 0;   // k per slice, a multiple of 32
+  __device__ void k_range(int z, int& b, int& e) const {
+    b = z * chunk < this->K ? z * chunk : this->K;
+    e = b + chunk < this->K ? b + chunk : this->K;
+  }
+  __device__ void store(int m, int n, int z, float v) const {
+    if (m < this->M && n < this->N) slab[((size_t)z * this->M + m) * this->N + n] = v;
+  }
+};
+
+__global__ __launch_bounds__(256) void fc_splitk_reduce_kernel(const float* __restrict__ slab, int Z, int M, int N,
+                                                               const float* __restrict__ bias, float* __restrict__ out,
+                                                               int ldo) {
+  const int n4 = N >> 2;
+  const long long total = (long long)M * n4;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int m = (int)(i / n4), q = (int)(i - (long long)m * n4);
+    const f32x4* src = reinterpret_cast<const f32x4*>(slab + (size_t)m * N) + q;
+    f32x4 v = src[0];
+    for (int z = 1; z < Z; ++z) v += src[(size_t)z * M * n4];
+    const f32x4 b = reinterpret_cast<const f32x4*>(bias)[q];
+    f32x4 y;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + b[r], 0.f);
+    *reinterpret_cast<f32x4*>(out + (size_t)m * ldo + 4 * q) = y;
+  }
+}
+
+// ppo_fc_fwd with a caller-owned workspace (ws, ws_bytes): rollout-sized M takes the
+// split-K form when ws holds its slab (ppo_fc_fwd_ws_bytes), else ppo_fc_fwd
+PPO_API long long ppo_fc_fwd_ws_bytes(int M, int H) {
+  const int Z = g_tune[TK_FC_SPLITK];
+  if (Z <= 1 || M <= g_small_b || (long long)M * H > 4096LL * 1024) return 0;
+  return 4LL * Z * M * H;
+}
+
+PPO_API int ppo_fc_fwd_ws(const float* x, int M, const float* w4p, const float* b, int H, float* out, int ldo,
+                          float* ws, long long ws_bytes, void* stream) {
+  const long long need = ppo_fc_fwd_ws_bytes(M, H);
+  if (!use_x9() || need == 0 || ws == nullptr || ws_bytes < need || ldo % 4 != 0 || H % 4 != 0 ||
+      ((uintptr_t)out & 15) != 0 || ((uintptr_t)ws & 15) != 0 || ((uintptr_t)b & 15) != 0)
+    return ppo_fc_fwd(x, M, w4p, b, H, out, ldo, stream);
+  const int K = 1568, Z = g_tune[TK_FC_SPLITK];
+  hipStream_t st = as_stream(stream);
+  DenseFwdSplitK<XP128x64w8> p;
+  p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1;
+  set_planes(p, w4p, (long long)H * K, H, K);
+  p.n_fast = fc_order(1);
+  p.slab = ws;
+  p.chunk = ((K + Z - 1) / Z + 31) / 32 * 32;
+  int rc = launch_x9(p, M, H, Z, st, "fc_fwd", 2.0 * M * H * K);
+  if (rc) return rc;
+  const long long n = (long long)M * (H / 4);
+  fc_splitk_reduce_kernel<<<(unsigned)std::min<long long>((n + 255) / 256, 4096), 256, 0, st>>>(ws, Z, M, H, b, out,
+                                                                                               ldo);
+  PPO_LAUNCH_CHECK("fc_splitk_reduce_kernel");
+  return 0;
+}
+
 // Linear + ReLU: out [M][N] = relu(x [M][K] · w [N][K]^T + b)
 PPO_API int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, const float* b, int N, float* out,
                                 void* stream) {
@@ -2431,8 +2492,7 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
   const long long R = (long long)B * 400;
   PPO_REQUIRE(R < 0x7fffffffLL, "ppo_conv1_wgrad: B too large");
   const double fl = 2.0 * R * 32 * C * 64;
-  if (obs_is_u8 && C == 4 && ((g_tune[TK_CONV1_WGRAD] >= 3 && g_tune[TK_CONV1_WGRAD] <= 5) ||
-                                g_tune[TK_CONV1_WGRAD] == 7)) {   // part-pipelined
+  if (obs_is_u8 && C == 4 && (g_tune[TK_CONV1_WGRAD] >= 3 && g_tune[TK_CONV1_WGRAD] <= 5)) {   // part-pipelined
     if (B <= 0 || Z <= 0) return 0;
     PPO_REQUIRE((B + Z - 1) / Z <= 512, "ppo_conv1_wgrad: %d images over %d blocks (at most 512 per block)", B, Z);
     int slot;
@@ -2449,9 +2509,6 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
     else if (g_tune[TK_CONV1_WGRAD] == 5)   // four waves per SIMD, two column tiles per wave
       conv1_wgrad_parts_kernel<3, 16, 2><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
                                                                             slab, slab_bias, g_stagger >> 4);
-    else if (g_tune[TK_CONV1_WGRAD] == 7)   // as 5, staging items balanced over the SIMDs
-      conv1_wgrad_parts_kernel<3, 16, 2, true><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0,
-                                                                                  B, slab, slab_bias, g_stagger >> 4);
     else
       conv1_wgrad_parts_kernel<3><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
                                                                     slab_bias, g_stagger >> 4);

@@ -129,3 +129,38 @@ def test_fc_wgrad_vs_float64(gpu, variant, order, products, R, H):
     tol = 1e-5 if products != 1 else 2e-2
     assert (gw - ref_w).abs().max().item() <= tol * ref_w.abs().max().item()
     assert (gb - ref_b).abs().max().item() <= 1e-5 * ref_b.abs().max().item()
+
+
+@pytest.mark.parametrize("Z", [2, 3, 4])
+@pytest.mark.parametrize("B,H", [(4096, 512), (1000, 256), (77, 64)])
+def test_fc_fwd_splitk_vs_float64(gpu, Z, B, H):
+    """ppo_fc_fwd_ws: the rollout-sized split-K fc forward (Z K-slices into the
+    workspace, fixed-order reduce + bias + ReLU) vs torch float64, and vs the
+    unsplit kernel within fp32 summation-order noise; a short workspace falls back."""
+    H_ = _hip()
+    w4, packed, pk = _packed(gpu, H, 7 + H)
+    g = torch.Generator().manual_seed(B + Z)
+    x = torch.relu(torch.randn(B, 1568, generator=g))
+    b = torch.randn(H, generator=g) * 0.1
+    xd, bd = x.cuda(), b.cuda()
+    old = H_.call("ppo_tune_get", b"fc_splitk")
+    H_.call("ppo_tune_set", b"fc_splitk", Z)
+    try:
+        nb = H_.call("ppo_fc_fwd_ws_bytes", B, H)
+        assert nb == 4 * Z * B * H
+        ws = torch.full((nb // 4,), float("nan"), device=gpu)
+        out = torch.full((B, H), float("nan"), device=gpu)
+        H_.call("ppo_fc_fwd_ws", xd.data_ptr(), B, pk[2], bd.data_ptr(), H, out.data_ptr(), H, ws.data_ptr(), nb, _s())
+        ref_ub = torch.empty(B, H, device=gpu)
+        H_.call("ppo_fc_fwd", xd.data_ptr(), B, pk[2], bd.data_ptr(), H, ref_ub.data_ptr(), H, _s())
+        short = torch.empty(B, H, device=gpu)
+        H_.call("ppo_fc_fwd_ws", xd.data_ptr(), B, pk[2], bd.data_ptr(), H, short.data_ptr(), H, ws.data_ptr(), nb - 4,
+                _s())
+        torch.cuda.synchronize()
+    finally:
+        H_.call("ppo_tune_set", b"fc_splitk", old)
+    ref = torch.relu(x.double() @ w4.double().t() + b.double())
+    got = out.cpu().double()
+    assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    assert (got - ref_ub.cpu().double()).abs().max().item() <= 2e-6 * ref.abs().max().item()
+    assert torch.equal(short, ref_ub)   # too small a workspace: the unsplit kernel

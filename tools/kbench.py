@@ -78,6 +78,7 @@ def main():
     z1 = a.z1 or z1
     z3 = a.z3 or z3
     z4 = a.z4 or z4
+    fws = torch.empty(max(call("ppo_fc_fwd_ws_bytes", B, H) // 4, 4), device=dev)
     obs32 = frames = mean = None
     if any(k.endswith(("_f32", "_rgb")) for k in a.only.split(",")):
         obs32 = (torch.randn(rows, 4, 84, 84, device=dev, generator=g) * 0.8).contiguous()
@@ -92,6 +93,8 @@ def main():
                       2.0 * B * 49 * 32 * 576),
         "fc_fwd": (lambda: call("ppo_fc_fwd", a3.data_ptr(), B, pk[2], b4.data_ptr(), H, h.data_ptr(), H, s),
                    2.0 * B * 1568 * H),
+        "fc_fwd_ws": (lambda: call("ppo_fc_fwd_ws", a3.data_ptr(), B, pk[2], b4.data_ptr(), H, h.data_ptr(), H,
+                                   fws.data_ptr(), fws.numel() * 4, s), 2.0 * B * 1568 * H),
         "fc_fwd_generic": (lambda: call("ppo_linear_relu_fwd", a3.data_ptr(), B, 1568, pk[2], b4.data_ptr(), H,
                                         h.data_ptr(), s), 2.0 * B * 1568 * H),
         "fc_dgrad": (lambda: call("ppo_linear_dgrad_mask", dh.data_ptr(), B, H, pk[3], 1568, a3.data_ptr(),
