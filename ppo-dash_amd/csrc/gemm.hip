@@ -1888,7 +1888,13 @@ static int g_small_b = 4;
 // fc_splitk: K slices of the rollout-sized fc forward with a workspace (ppo_fc_fwd_ws; <= 1: unsplit)
 static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0, 0, 2};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
+int heads_lds_knob(int set, int value);   // heads.hip (the LDS-weight heads_train kernel, default on)
+
 PPO_API int ppo_tune_set(const char* key, int value) {
+  if (strcmp(key, "heads_lds") == 0) {
+    heads_lds_knob(1, value);
+    return 0;
+  }
   if (strcmp(key, "small_b") == 0) {
     PPO_REQUIRE(value >= 0, "ppo_tune_set: small_b must be >= 0, got %d", value);
     g_small_b = value;
@@ -1913,6 +1919,7 @@ PPO_API int ppo_tune_set(const char* key, int value) {
 }
 
 PPO_API int ppo_tune_get(const char* key) {
+  if (strcmp(key, "heads_lds") == 0) return heads_lds_knob(0, 0);
   if (strcmp(key, "small_b") == 0) return g_small_b;
   if (strcmp(key, "stagger") == 0) return g_stagger;
   if (strcmp(key, "products") == 0) return g_products;

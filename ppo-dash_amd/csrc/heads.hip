@@ -360,6 +360,179 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
   }
 }
 
+// heads_train_kernel for CNNBase / the GRU policy at H = 512, A = 8 (TrainArgs'
+// FAST case) with the head weights in LDS instead of registers: a lane holds the
+// columns 4·lane + q + 256·c2 (q < 4, c2 < 2: float4 loads and stores of the
+// features and their gradient) and reads the 9 weight rows of those columns as
+// 18 ds_read_b128 per row pass.  The register version held 72 weight VGPRs next
+// to the 72 gradient accumulators (256 VGPRs: one wave per SIMD, every row's
+// dependent chain — 9 wave reductions, the softmax, the loss — exposed); this one
+// fits two waves per SIMD.  Same arithmetic per element, same partial layout.
+__global__ __launch_bounds__(64 * HW) void heads_train_lds_kernel(const TrainArgs a) {
+  constexpr int A = 8, H = 512;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ f32x4 Wl[9][128];   // row 0: critic, rows 1..8: actor logits
+  for (int i = threadIdx.x; i < 9 * 128; i += 64 * HW) {
+    const int o = i >> 7, q = i & 127;
+    Wl[o][q] = o == 0 ? reinterpret_cast<const f32x4*>(a.wc)[q] : reinterpret_cast<const f32x4*>(a.wa + (o - 1) * H)[q];
+  }
+  const float b0 = a.bc[0];
+  float ba[A];
+#pragma unroll
+  for (int o = 0; o < A; ++o) ba[o] = a.ba[o];
+  __syncthreads();
+  f32x4 gw[9][2];   // Σ_rows g_o · f (o = 0: critic), this lane's columns
+#pragma unroll
+  for (int o = 0; o < 9; ++o) gw[o][0] = gw[o][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float gbc = 0.f, gba[A];
+#pragma unroll
+  for (int o = 0; o < A; ++o) gba[o] = 0.f;
+  float s_vl = 0.f, s_al = 0.f, s_ent = 0.f, s_bad = 0.f;
+  const float clip = a.clip;
+  const long long r0 = ((long long)blockIdx.x * HW + wave) * a.rows_per_wave;
+  int q_act = 0;
+  float q_adv = 0.f, q_olp = 0.f, q_vo = 0.f, q_ret = 0.f;
+  if (lane < a.rows_per_wave && r0 + lane < a.B) {
+    const long long sr = a.idx ? (long long)a.idx[r0 + lane] : a.row0 + r0 + lane;
+    q_act = (int)a.actions[sr];
+    q_adv = a.adv[sr];
+    q_olp = a.old_logp[sr];
+    q_vo = a.vpred[sr];
+    q_ret = a.ret[sr];
+  }
+  auto bcast = [](float x, int j) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j)); };
+  f32x4 fn[2];
+  auto load_row = [&](long long row) {
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2)
+      fn[c2] = row < a.B ? reinterpret_cast<const f32x4*>(a.feat + row * H)[lane + 64 * c2] : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  load_row(r0);
+  for (int rr = 0; rr < a.rows_per_wave; ++rr) {
+    const long long row = r0 + rr;
+    if (row >= a.B) break;
+    const f32x4 f[2] = {fn[0], fn[1]};
+    if (rr + 1 < a.rows_per_wave) load_row(row + 1);
+    float dots[9];
+#pragma unroll
+    for (int o = 0; o < 9; ++o) {
+      float t = 0.f;
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        const f32x4 w = Wl[o][lane + 64 * c2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t += f[c2][q] * w[q];
+      }
+      dots[o] = wave_sum(t);
+    }
+    const float value = dots[0] + b0;
+    float z[A], nl[A], p[A];
+#pragma unroll
+    for (int o = 0; o < A; ++o) z[o] = dots[1 + o] + ba[o];
+    categorical(z, A, nl, p);
+    const int act = __builtin_amdgcn_readlane(q_act, rr);
+    s_bad += (unsigned)act < (unsigned)A ? 0.f : 1.f;
+    float lp = 0.f, ent = 0.f;
+#pragma unroll
+    for (int o = 0; o < A; ++o) {
+      if (o == act) lp = nl[o];
+      ent -= nl[o] * p[o];
+    }
+    // action loss (ppo.py:61-66)
+    const float adv = bcast(q_adv, rr);
+    const float ratio = expf(lp - bcast(q_olp, rr));
+    const float surr1 = ratio * adv;
+    const float rc = fminf(fmaxf(ratio, 1.0f - clip), 1.0f + clip);
+    const float surr2 = rc * adv;
+    const float w1 = surr1 < surr2 ? 1.f : (surr1 == surr2 ? 0.5f : 0.f);
+    const float inr = (ratio >= 1.0f - clip && ratio <= 1.0f + clip) ? 1.f : 0.f;
+    const float g_logp = -a.inv_b * (w1 * adv + (1.f - w1) * adv * inr) * ratio;
+    // value loss (ppo.py:68-77)
+    const float vo = bcast(q_vo, rr), R = bcast(q_ret, rr);
+    float g_v, vl_row;
+    if (a.use_clipped_value_loss) {
+      const float dv = value - vo;
+      const float vpc = vo + fminf(fmaxf(dv, -clip), clip);
+      const float l1 = (value - R) * (value - R);
+      const float l2 = (vpc - R) * (vpc - R);
+      vl_row = fmaxf(l1, l2);
+      const float u1 = l1 > l2 ? 1.f : (l1 == l2 ? 0.5f : 0.f);
+      const float vin = (dv >= -clip && dv <= clip) ? 1.f : 0.f;
+      g_v = a.value_coef * 0.5f * a.inv_b * (u1 * 2.f * (value - R) + (1.f - u1) * 2.f * (vpc - R) * vin);
+    } else {
+      vl_row = (R - value) * (R - value);
+      g_v = a.value_coef * a.inv_b * (value - R);
+    }
+    s_vl += vl_row;
+    s_al += fminf(surr1, surr2);
+    s_ent += ent;
+    float g[9];   // g[0] = dL/dvalue, g[1 + o] = dL/dlogit o
+    g[0] = g_v;
+    const float ce = a.entropy_coef * a.inv_b;
+#pragma unroll
+    for (int o = 0; o < A; ++o) g[1 + o] = g_logp * ((o == act ? 1.f : 0.f) - p[o]) + ce * p[o] * (nl[o] + ent);
+    // dL/dfeature of this lane's columns (masked by the activation), head gradients
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2) {
+      f32x4 d = Wl[0][lane + 64 * c2] * g[0];
+#pragma unroll
+      for (int o = 1; o < 9; ++o) {
+        const f32x4 w = Wl[o][lane + 64 * c2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d[q] += g[o] * w[q];
+      }
+      f32x4 y;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y[q] = act_grad(d[q], f[c2][q], a.feat_act);
+      reinterpret_cast<f32x4*>(a.dfeat + row * H)[lane + 64 * c2] = y;
+#pragma unroll
+      for (int o = 0; o < 9; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gw[o][c2][q] += g[o] * f[c2][q];
+    }
+    gbc += g_v;
+#pragma unroll
+    for (int o = 0; o < A; ++o) gba[o] += g[1 + o];
+  }
+  // block reduction of the head-gradient partials across the HW waves (fixed order)
+  __shared__ f32x4 red[HW][128];
+  __shared__ float redb[HW][A + 5];
+  for (int o = 0; o < 9; ++o) {
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2) red[wave][lane + 64 * c2] = gw[o][c2];
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        f32x4 t = red[0][lane + 64 * c2];
+        for (int q = 1; q < HW; ++q) t += red[q][lane + 64 * c2];
+        reinterpret_cast<f32x4*>(a.part_w + ((size_t)blockIdx.x * 9 + o) * H)[lane + 64 * c2] = t;
+      }
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {
+    redb[wave][0] = gbc;
+#pragma unroll
+    for (int o = 0; o < A; ++o) redb[wave][1 + o] = gba[o];
+    redb[wave][A + 1] = s_vl;
+    redb[wave][A + 2] = s_al;
+    redb[wave][A + 3] = s_ent;
+    redb[wave][A + 4] = s_bad;
+  }
+  __syncthreads();
+  if (threadIdx.x < 9) {
+    float t = 0.f;
+    for (int q = 0; q < HW; ++q) t += redb[q][threadIdx.x];
+    a.part_b[(size_t)blockIdx.x * 9 + threadIdx.x] = t;
+  }
+  if (threadIdx.x < 4) {
+    float t = 0.f;
+    for (int q = 0; q < HW; ++q) t += redb[q][A + 1 + threadIdx.x];
+    a.part_loss[(size_t)blockIdx.x * 4 + threadIdx.x] = t;
+  }
+}
+
 // loss partials -> acc[0..3] += {0.5·Σvl/B, -Σal/B, Σent/B, # bad actions} (double, fixed order)
 __global__ __launch_bounds__(256) void loss_reduce_kernel(const float* __restrict__ part_loss, int nblk,
                                                           double* __restrict__ loss_acc, double inv_b) {
@@ -436,8 +609,17 @@ int dispatch_act(int HC, const float* feat, const float* feat_v, int N, int H, c
   return PPO_EARG;
 }
 
+static int g_heads_lds = 1;   // ppo_tune_set("heads_lds", 0): the register-weight kernel (A/B)
+
 template <int HC, int AMAX>
 int launch_train(const TrainArgs& a, int blocks, hipStream_t st) {
+  if (g_heads_lds && HC == 8 && AMAX == 8 && a.A == 8 && a.H == 512 && !a.feat_v && !a.dfeat_v &&
+      ((uintptr_t)a.feat & 15) == 0 && ((uintptr_t)a.dfeat & 15) == 0 && ((uintptr_t)a.wc & 15) == 0 &&
+      ((uintptr_t)a.wa & 15) == 0 && ((uintptr_t)a.part_w & 15) == 0) {
+    heads_train_lds_kernel<<<blocks, 64 * HW, 0, st>>>(a);
+    PPO_LAUNCH_CHECK("heads_train_lds_kernel");
+    return 0;
+  }
   if (a.A == AMAX && a.H == 64 * HC && !a.feat_v && !a.dfeat_v)
     heads_train_kernel<HC, AMAX, true><<<blocks, 64 * HW, 0, st>>>(a);
   else
@@ -481,6 +663,11 @@ PPO_API int ppo_heads_act(const float* feat, const float* feat_v, int N, int H, 
                            action, logp, entropy, st);
   return dispatch_act<16>(HC, feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter, deterministic, given, value,
                           action, logp, entropy, st);
+}
+
+int heads_lds_knob(int set, int value) {   // gemm.hip's ppo_tune_set / _get ("heads_lds")
+  if (set) g_heads_lds = value;
+  return g_heads_lds;
 }
 
 PPO_API int ppo_heads_train_blocks(int B) {

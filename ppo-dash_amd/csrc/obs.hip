@@ -31,16 +31,29 @@ __device__ __forceinline__ float gray_f32(float r, float g, float b) {
   return __fadd_rn(__fadd_rn(__fmul_rn(r, 0.299f), __fmul_rn(g, 0.587f)), __fmul_rn(b, 0.114f));
 }
 
-// NormalizeWrapper value of byte u at element e of the (y, x, c) frame, float64
-__device__ __forceinline__ double norm_value(uint32_t u, int mode, const double* __restrict__ mean, double inv_or_std,
-                                             long long e) {
-  if (mode == 2) return ((double)u - mean[e]) / inv_or_std;
-  if (mode == 1) return (double)u / 255.0;
-  return (double)u;
+// fl32(fl64(d / s)) without a float64 divide per element: q = d·(1/s) differs from
+// the IEEE quotient by at most a few units of its last bit, so it rounds to the same
+// fp32 unless the 29 bits the fp32 rounding drops lie within 4 units of the
+// midpoint pattern — there the IEEE division decides (the same test conv1f.hip's
+// fused decode uses; bit-identity with the reference chain: tests/test_obs_boundary.py)
+__device__ __attribute__((noinline)) double obs_ieee_div(double d, double s) { return d / s; }
+__device__ __forceinline__ float div_to_f32(double d, double s, double rs) {
+  double q = d * rs;
+  const uint32_t lo = (uint32_t)__double2loint(q) & 0x1FFFFFFFu;
+  if (__builtin_expect(lo - 0x0FFFFFFCu < 8u, 0)) q = obs_ieee_div(d, s);
+  return (float)q;
+}
+
+// NormalizeWrapper value of byte u at element e of the (y, x, c) frame, float64, as fp32
+__device__ __forceinline__ float norm_value(uint32_t u, int mode, const double* __restrict__ mean, double stdv,
+                                            double rstd, long long e) {
+  if (mode == 2) return div_to_f32((double)u - mean[e], stdv, rstd);
+  if (mode == 1) return div_to_f32((double)u, 255.0, 1.0 / 255.0);
+  return (float)u;
 }
 
 // One block per frame (blocks walk frames): the frame's bytes are staged in LDS
-// with coalesced dword loads, every pixel is normalised once (3 float64 divides),
+// with coalesced dword loads, every pixel is normalised once (3 reciprocal products),
 // the colour planes are written straight out and the grey value goes to LDS, from
 // where the transposed mono plane is written (coalesced on the output side).
 // Dynamic LDS: S*S*3 bytes (frame, rounded to dwords) + S*S floats (grey).
@@ -49,6 +62,7 @@ __global__ __launch_bounds__(OBS_THREADS) void obs_preprocess_kernel(
     double stdv, int mono, float* __restrict__ dst, long long dst_stride, int aligned) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int px = S * S, nb = px * 3, nw = (nb + 3) / 4;
+  const double rstd = 1.0 / stdv;
   uint32_t* fw = reinterpret_cast<uint32_t*>(lds);
   float* gray = reinterpret_cast<float*>(lds + 4 * nw);
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
@@ -66,7 +80,7 @@ __global__ __launch_bounds__(OBS_THREADS) void obs_preprocess_kernel(
       float v[3];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        v[c] = (float)norm_value(lds[3 * p + c], mode, mean, stdv, 3LL * p + c);
+        v[c] = norm_value(lds[3 * p + c], mode, mean, stdv, rstd, 3LL * p + c);
         o[(size_t)c * px + p] = v[c];
       }
       if (mono) {
@@ -80,6 +94,92 @@ __global__ __launch_bounds__(OBS_THREADS) void obs_preprocess_kernel(
       for (int p = threadIdx.x; p < px; p += OBS_THREADS) {
         const int y = p / S, x = p - y * S;
         o[(size_t)3 * px + p] = gray[x * S + y];   // transposed pixel (see header)
+      }
+    }
+  }
+}
+
+// Frame-walking form (S <= 84: at most PPT pixels per thread): each thread owns
+// the same PPT pixels of every frame its block walks, so the float64 means of
+// those pixels are loaded once per block into registers — the one-block-per-frame
+// kernel above re-read the 169 KB mean array (84 x 84 x 3 float64) for every frame,
+// more bytes than the frame itself moves.  The grey plane sits in LDS with row
+// stride S + 1, so the transposed read (stride S + 1 between lanes) and the
+// row-order write are both bank-conflict-free.
+constexpr int PPT = 7, WALK_THREADS = 1024;
+__global__ __launch_bounds__(WALK_THREADS) void obs_preprocess_walk_kernel(
+    const uint8_t* __restrict__ src, long long src_stride, int N, int S, int mode, const double* __restrict__ mean,
+    double stdv, int mono, float* __restrict__ dst, long long dst_stride, int aligned) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int px = S * S, nb = px * 3, nw = (nb + 3) / 4, tid = threadIdx.x;
+  uint32_t* fw = reinterpret_cast<uint32_t*>(lds);
+  float* gray = reinterpret_cast<float*>(lds + 4 * nw);   // [S][S + 1]
+  const double rstd = 1.0 / stdv;
+  double m[PPT][3];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
+    const int p = tid + WALK_THREADS * j;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) m[j][c] = (mode == 2 && p < px) ? mean[3LL * p + c] : 0.0;
+  }
+  // aligned frames: the next frame's dwords (<= 6 per thread) are loaded into registers
+  // while the current one is computed
+  constexpr int DPT = (PPT * WALK_THREADS * 3 / 4 + WALK_THREADS - 1) / WALK_THREADS;
+  uint32_t nx[DPT];
+  auto fetch = [&](int n) {
+    if (!aligned || n >= N) return;
+    const uint32_t* fs = reinterpret_cast<const uint32_t*>(src + (size_t)n * src_stride);
+#pragma unroll
+    for (int i = 0; i < DPT; ++i) {
+      const int w = tid + WALK_THREADS * i;
+      if (w < nw) nx[i] = fs[w];
+    }
+  };
+  fetch(blockIdx.x);
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    const uint8_t* f = src + (size_t)n * src_stride;
+    float* o = dst + (size_t)n * dst_stride;
+    __syncthreads();   // the previous frame's LDS reads are done
+    if (aligned) {
+#pragma unroll
+      for (int i = 0; i < DPT; ++i) {
+        const int w = tid + WALK_THREADS * i;
+        if (w < nw) fw[w] = nx[i];
+      }
+    } else {
+      for (int b = tid; b < nb; b += WALK_THREADS) lds[b] = f[b];
+    }
+    __syncthreads();
+    fetch(n + gridDim.x);
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) {
+      const int p = tid + WALK_THREADS * j;
+      if (p < px) {
+        float v[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const uint32_t u = lds[3 * p + c];
+          v[c] = mode == 2 ? div_to_f32((double)u - m[j][c], stdv, rstd)
+                           : mode == 1 ? div_to_f32((double)u, 255.0, 1.0 / 255.0) : (float)u;
+          o[(size_t)c * px + p] = v[c];
+        }
+        if (mono) {
+          float gm = gray_f32(v[0], v[1], v[2]);
+          if (mode == 0) gm = (float)(uint8_t)gm;
+          const int y = p / S, x = p - y * S;
+          gray[y * (S + 1) + x] = gm;
+        }
+      }
+    }
+    if (mono) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < PPT; ++j) {
+        const int p = tid + WALK_THREADS * j;
+        if (p < px) {
+          const int y = p / S, x = p - y * S;
+          o[(size_t)3 * px + p] = gray[x * (S + 1) + y];   // transposed pixel (see header)
+        }
       }
     }
   }
@@ -121,8 +221,19 @@ PPO_API int ppo_obs_preprocess(const uint8_t* src, long long src_stride, int N, 
   const int aligned = ((uintptr_t)src % 4 == 0) && (src_stride % 4 == 0) && ((3 * S * S) % 4 == 0);
   int slot;
   const bool prof = ppo_prof_begin("obs_preprocess", as_stream(stream), &slot);
-  obs_preprocess_kernel<<<(unsigned)(N < 4096 ? N : 4096), OBS_THREADS, (size_t)lds_bytes, as_stream(stream)>>>(
-      src, src_stride, N, S, mode, mean, stdv, mono, dst, dst_stride, aligned);
+  if (S * S <= PPT * WALK_THREADS) {   // frame-walking blocks, means in registers (one 16-wave block per CU)
+    const long long walk_lds = 4LL * ((3LL * S * S + 3) / 4) + 4LL * S * (S + 1);
+    int dev = 0, n_cu = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      n_cu = 256;
+    const int grid = N < n_cu ? N : n_cu;
+    obs_preprocess_walk_kernel<<<(unsigned)grid, WALK_THREADS, (size_t)walk_lds, as_stream(stream)>>>(
+        src, src_stride, N, S, mode, mean, stdv, mono, dst, dst_stride, aligned);
+  } else {
+    obs_preprocess_kernel<<<(unsigned)(N < 4096 ? N : 4096), OBS_THREADS, (size_t)lds_bytes, as_stream(stream)>>>(
+        src, src_stride, N, S, mode, mean, stdv, mono, dst, dst_stride, aligned);
+  }
   // algorithmic bytes: 3 u8 in + (3 + mono) f32 out per pixel
   if (prof) ppo_prof_end(slot, as_stream(stream), (double)N * S * S * (3.0 + 4.0 * (3 + (mono ? 1 : 0))));
   PPO_LAUNCH_CHECK("obs_preprocess_kernel");
