@@ -371,10 +371,10 @@ __global__ __launch_bounds__(64 * HW) void heads_train_kernel(const TrainArgs a)
 __global__ __launch_bounds__(64 * HW) void heads_train_lds_kernel(const TrainArgs a) {
   constexpr int A = 8, H = 512;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __shared__ f32x4 Wl[9][128];   // row 0: critic, rows 1..8: actor logits
-  for (int i = threadIdx.x; i < 9 * 128; i += 64 * HW) {
-    const int o = i >> 7, q = i & 127;
-    Wl[o][q] = o == 0 ? reinterpret_cast<const f32x4*>(a.wc)[q] : reinterpret_cast<const f32x4*>(a.wa + (o - 1) * H)[q];
+  __shared__ f32x4 Wl[9][128];   // row 0: critic, rows 1..8: actor logits (the flat parameter
+  for (int i = threadIdx.x; i < 9 * H; i += 64 * HW) {   // buffer places wa at an odd offset: scalar loads)
+    const int o = i / H, k = i - H * o;
+    reinterpret_cast<float*>(&Wl[o][0])[k] = o == 0 ? a.wc[k] : a.wa[(o - 1) * H + k];
   }
   const float b0 = a.bc[0];
   float ba[A];
@@ -614,8 +614,7 @@ static int g_heads_lds = 1;   // ppo_tune_set("heads_lds", 0): the register-weig
 template <int HC, int AMAX>
 int launch_train(const TrainArgs& a, int blocks, hipStream_t st) {
   if (g_heads_lds && HC == 8 && AMAX == 8 && a.A == 8 && a.H == 512 && !a.feat_v && !a.dfeat_v &&
-      ((uintptr_t)a.feat & 15) == 0 && ((uintptr_t)a.dfeat & 15) == 0 && ((uintptr_t)a.wc & 15) == 0 &&
-      ((uintptr_t)a.wa & 15) == 0 && ((uintptr_t)a.part_w & 15) == 0) {
+      ((uintptr_t)a.feat & 15) == 0 && ((uintptr_t)a.dfeat & 15) == 0 && ((uintptr_t)a.part_w & 15) == 0) {
     heads_train_lds_kernel<<<blocks, 64 * HW, 0, st>>>(a);
     PPO_LAUNCH_CHECK("heads_train_lds_kernel");
     return 0;
