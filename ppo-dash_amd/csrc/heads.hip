@@ -579,8 +579,9 @@ int launch_act(const float* feat, const float* feat_v, int N, int H, const float
                const float* ba,
                int A, const float* noise, unsigned long long seed, unsigned long long counter, int det,
                const int64_t* given, float* v, int64_t* act, float* lp, float* ent, hipStream_t st) {
-  // ~2048 waves in flight (8 per CU): a rollout batch of 4096 rows takes 2 per wave
-  const int rpw = (int)std::min<long long>(8, std::max<long long>(1, ceil_div(N, 2048)));
+  // ~4096 waves in flight (4 per SIMD at this kernel's 122-137 VGPRs): a rollout batch of
+  // 4,096 rows takes one row per wave, so no wave runs two rows' dependent chains back to back
+  const int rpw = (int)std::min<long long>(8, std::max<long long>(1, ceil_div(N, 4096)));
   const unsigned blocks = ceil_div(N, HW * rpw);
   if (A == AMAX && H == 64 * HC && !feat_v)
     heads_act_kernel<HC, AMAX, true><<<blocks, 64 * HW, 0, st>>>(feat, feat_v, N, H, wc, bc, wa, ba, A, noise, seed, counter,

@@ -79,6 +79,9 @@ def main():
     z3 = a.z3 or z3
     z4 = a.z4 or z4
     fws = torch.empty(max(call("ppo_fc_fwd_ws_bytes", B, H) // 4, 4), device=dev)
+    hw = rn(9 * H + 9, sc=0.03)                       # heads: wc [H], bc, wa [8][H], ba [8]
+    hv = torch.empty(3 * B, device=dev)
+    ha = torch.empty(B, dtype=torch.int64, device=dev)
     obs32 = frames = mean = None
     if any(k.endswith(("_f32", "_rgb")) for k in a.only.split(",")):
         obs32 = (torch.randn(rows, 4, 84, 84, device=dev, generator=g) * 0.8).contiguous()
@@ -95,6 +98,14 @@ def main():
                    2.0 * B * 1568 * H),
         "fc_fwd_ws": (lambda: call("ppo_fc_fwd_ws", a3.data_ptr(), B, pk[2], b4.data_ptr(), H, h.data_ptr(), H,
                                    fws.data_ptr(), fws.numel() * 4, s), 2.0 * B * 1568 * H),
+        # the c5 GRU input projection x [B][272] . W_ih^T (768 x 272) + b (ppo_linear_fwd_ex)
+        "gru_in": (lambda: call("ppo_linear_fwd_ex", a3.data_ptr(), None, B, 272, 272, w4.data_ptr(), None, 768,
+                                dz3.data_ptr(), 768, 0, s), 2.0 * B * 768 * 272),   # dz3: B x 1568 >= B x 768
+        # the rollout heads (Categorical sample, value, log-prob, entropy) on B rows of H features
+        "heads_act": (lambda: call("ppo_heads_act", h.data_ptr(), None, B, H, hw.data_ptr(), hw.data_ptr() + 4 * H,
+                                   hw.data_ptr() + 4 * (H + 1), hw.data_ptr() + 4 * (9 * H + 1), 8, None, 7, 0, 0,
+                                   None, hv.data_ptr(), ha.data_ptr(), hv.data_ptr() + 4 * B, hv.data_ptr() + 8 * B,
+                                   s), 0.0),
         "fc_fwd_generic": (lambda: call("ppo_linear_relu_fwd", a3.data_ptr(), B, 1568, pk[2], b4.data_ptr(), H,
                                         h.data_ptr(), s), 2.0 * B * 1568 * H),
         "fc_dgrad": (lambda: call("ppo_linear_dgrad_mask", dh.data_ptr(), B, H, pk[3], 1568, a3.data_ptr(),
