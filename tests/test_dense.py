@@ -164,3 +164,24 @@ def test_fc_fwd_splitk_vs_float64(gpu, Z, B, H):
     assert (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
     assert (got - ref_ub.cpu().double()).abs().max().item() <= 2e-6 * ref.abs().max().item()
     assert torch.equal(short, ref_ub)   # too small a workspace: the unsplit kernel
+
+
+@pytest.mark.parametrize("Z,cols", [(7, 100), (39, 802816), (96, 9000), (512, 512), (512, 1), (300, 4096), (1, 33)])
+def test_colsum_vs_float64(gpu, Z, cols):
+    """ppo_colsum (the deterministic split-K / block-partial reduce behind every
+    weight gradient and the heads' partials) over the slab counts and widths the
+    engine uses: within fp32 summation noise of float64 and the same bits twice."""
+    H_ = _hip()
+    g = torch.Generator().manual_seed(Z + cols)
+    ld = cols + 3
+    src = torch.randn(Z, ld, generator=g).cuda()
+    outs = []
+    for _ in range(2):
+        out = torch.full((cols,), float("nan"), device=gpu)
+        H_.call("ppo_colsum", src.data_ptr(), ld, Z, cols, out.data_ptr(), 0.5, 0, _s())
+        outs.append(out)
+    torch.cuda.synchronize()
+    ref = 0.5 * src[:, :cols].double().sum(0)
+    err = (outs[0].double() - ref).abs().max().item()
+    assert err <= 1e-6 * Z * src.abs().max().item() + 1e-7
+    assert torch.equal(outs[0], outs[1])
