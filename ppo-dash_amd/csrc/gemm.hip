@@ -1884,7 +1884,8 @@ static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measure
 // small_b: forwards of at most this many samples (images / linear rows) take the
 // small-batch path of small.hip (an output element per thread or wave, fp32 FMA)
 static int g_small_b = 4;
-// order: fc tile order override for A/B (0: per-layer default, 1: m fastest, 2: n fastest; igemm_x9.h tile_of)
+// order: fc tile order override for A/B (0: per-layer default, 1: m fastest, 2: n fastest; igemm_x9.h tile_of;
+// 3: the default order with the fc weight gradient's scalar epilogue, for A/B)
 // fc_splitk: K slices of the rollout-sized fc forward with a workspace (ppo_fc_fwd_ws; <= 1: unsplit)
 static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0, 0, 2};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
@@ -2159,7 +2160,7 @@ PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float*
 #include "dense_x32.h"
 
 // tile order of an fc GEMM launch: the layer's measured default unless the "order" knob overrides it
-static int fc_order(int dflt) { return g_tune[TK_ORDER] ? g_tune[TK_ORDER] - 1 : dflt; }
+static int fc_order(int dflt) { return g_tune[TK_ORDER] == 1 || g_tune[TK_ORDER] == 2 ? g_tune[TK_ORDER] - 1 : dflt; }
 
 // CNNBase fc (model.py:181): out[m * ldo + n] = relu(x [M][1568] · W4p [H][1568]^T + b), W4p the packed
 // segment of ppo_pack_weights (its bf16 planes follow it)
@@ -2188,6 +2189,8 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
     p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1; \
     set_planes(p, w4p, (long long)H * K, H, K);                                                      \
     p.n_fast = fc_order(1);                                                                          \
+    p.vec = g_tune[TK_FC_FWD] != 1 && H % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)out & 15) == 0 &&   \
+            (b == nullptr || ((uintptr_t)b & 15) == 0);                                              \
     return launch_x9(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);                      \
   }
     if (v == 5) PPO_FC(XP128x64w8)
@@ -2209,6 +2212,7 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
 // and applies ReLU.
 template <class C_>
 struct DenseFwdSplitK : DenseReluFwd<C_> {
+  static constexpr bool VEC_STORE = false;   // partials go to the slab (store), never store4
   float* slab = nullptr;
   int chunk = 0;   // k per slice, a multiple of 32
   __device__ void k_range(int z, int& b, int& e) const {
@@ -2372,6 +2376,8 @@ PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt
     p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;        \
     set_planes(p, wt, (long long)N * K, N, K);                                      \
     p.n_fast = fc_order(0);                                                         \
+    p.vec = g_tune[TK_FC_DGRAD] != 1 && N % 4 == 0 && ((uintptr_t)dx & 15) == 0 &&  \
+            (act == nullptr || ((uintptr_t)act & 15) == 0);                         \
     return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K); \
   }
     if (g_tune[TK_FC_DGRAD] == 10) PPO_FCD(SP128)   // split-at-staging: 1.06 / 1.00 vs 0.74 ms (slower)
@@ -2609,6 +2615,7 @@ PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int 
     DenseWgrad<CFG> p;                                                              \
     set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);                                  \
     p.x = x; p.K = K; p.n_fast = fc_order(0);                                       \
+    p.vec = g_tune[TK_ORDER] < 3 && K % 4 == 0 && ((uintptr_t)slab & 15) == 0;      \
     return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K); \
   }
     // fc_wgrad tune: 0 / 10 split-at-staging 256 x 128 (default: 0.727 vs 0.775 ms at the c3

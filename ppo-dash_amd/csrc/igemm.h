@@ -343,6 +343,18 @@ struct DenseReluFwd : C_ {
       out[(size_t)m * (ldo ? ldo : N) + n] = relu == 1 ? fmaxf(y, 0.f) : (relu == 2 ? tanhf(y) : y);
     }
   }
+  // vector epilogue (see DenseDgradMask::store4); vec = 1 only with N, ldo and the
+  // pointers 16-B compatible
+  static constexpr bool VEC_STORE = true;
+  int vec = 0;
+  __device__ void store4(int m, int n, int, const f32x4& v) const {
+    if (m >= M || n >= N) return;
+    f32x4 y = v;
+    if (bias) y += *reinterpret_cast<const f32x4*>(bias + n);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = relu == 1 ? fmaxf(y[r], 0.f) : (relu == 2 ? tanhf(y[r]) : y[r]);
+    *reinterpret_cast<f32x4*>(out + (size_t)m * (ldo ? ldo : N) + n) = y;
+  }
 };
 
 // dx[m][n] = (act[m][n] > 0) * Σ_k dy[m][k] wt[n][k]
@@ -373,6 +385,20 @@ struct DenseDgradMask : C_ {
       }
     }
   }
+  // vector epilogue (igemm_x9_kernel, vec = 1 set by the launcher when N, the act row
+  // stride and both pointers allow 16-B accesses): columns n .. n + 3 of row m
+  static constexpr bool VEC_STORE = true;
+  int vec = 0;
+  __device__ void store4(int m, int n, int, const f32x4& v) const {
+    if (m >= M || n >= N) return;
+    f32x4 o = v;
+    if (act) {
+      const f32x4 y = *reinterpret_cast<const f32x4*>(act + (size_t)m * (ldact ? ldact : N) + n);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = mode == 2 ? v[r] * (1.0f - y[r] * y[r]) : (y[r] > 0.f ? v[r] : 0.f);
+    }
+    *reinterpret_cast<f32x4*>(dx + (size_t)m * N + n) = o;
+  }
 };
 
 template <class C_>
@@ -392,6 +418,11 @@ struct WgradBase : C_ {
   }
   __device__ void store(int m, int n, int z, float v) const {
     if (m < COUT && n < NW) slab[((size_t)z * COUT + m) * NW + n] = v;
+  }
+  static constexpr bool VEC_STORE = true;   // vec = 1: NW % 4 == 0, 16-B aligned slab
+  int vec = 0;
+  __device__ void store4(int m, int n, int z, const f32x4& v) const {
+    if (m < COUT && n < NW) *reinterpret_cast<f32x4*>(slab + ((size_t)z * COUT + m) * NW + n) = v;
   }
   __device__ void store_bias(int m, int z, float v) const {
     if (m < COUT) slab_bias[(size_t)z * COUT + m] = v;

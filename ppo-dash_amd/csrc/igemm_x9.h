@@ -117,7 +117,8 @@ template <int BM_, int BN_, int WM_, int WN_, bool AKC, bool BKC, bool BIASA = f
 struct CfgX {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NT = 64 * WM_ * WN_, BK = 32;
   static constexpr bool A_KC = AKC, B_KC = BKC, BIAS_FROM_A = BIASA, TILE_EPI = false, B_TILE = false;
-  static constexpr bool A_EXACT = AX_, B_EXACT = BX_, B_PLANES = BP_, SPLIT_STAGE = false;
+  static constexpr bool A_EXACT = AX_, B_EXACT = BX_, B_PLANES = BP_, SPLIT_STAGE = false, VEC_STORE = false;
+  int vec = 0;
   struct ACtx { const float* p; int a; int b; bool ok; };
   struct BCtx { const float* p; int a; bool ok; };
   // B_PLANES: plane p of B[n][k] at bpl[p * bps + n * bld + k] (bf16 bits), n < bnr, k < bld
@@ -174,6 +175,29 @@ __device__ __forceinline__ void tile_of(int n_fast, int BM, int BN, int& m0, int
   const int r = t - z * mn, mt = r / gy;
   m0 = mt * BM;
   n0 = (r - mt * gy) * BN;
+}
+
+// Vector epilogue of a wave's TM x TN 16x16 tiles: each tile goes through the
+// wave's own 16 x 17-float slice of the (free) LDS so that every lane stores four
+// consecutive columns of one row (one 16-B store, and 16-B operand loads in the
+// problem's store4) instead of one column of four rows (4-B accesses in 64-B runs):
+// fc forward 0.565 -> 0.542, fc dgrad 0.723 -> 0.680 ms at the c3 minibatch.
+template <class P, int TM, int TN>
+__device__ __forceinline__ void vec_epilogue(const P& p, float* smem, const f32x4 (&acc)[TM][TN], int wave, int lane,
+                                             int mb, int nb, int z) {
+  float* T = smem + wave * (16 * 17);
+  const int fr = lane & 15, fg = lane >> 4, tr = lane >> 2, tc = 4 * (lane & 3);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[(4 * fg + r) * 17 + fr] = acc[i][j][r];
+      __builtin_amdgcn_wave_barrier();
+      const f32x4 v = {T[tr * 17 + tc], T[tr * 17 + tc + 1], T[tr * 17 + tc + 2], T[tr * 17 + tc + 3]};
+      __builtin_amdgcn_wave_barrier();
+      p.store4(mb + i * 16 + tr, nb + j * 16 + tc, z, v);
+    }
 }
 
 template <class P, int NP>
@@ -374,15 +398,25 @@ __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
     __syncthreads();
   }
 
+  bool vec_done = false;
+  if constexpr (P::VEC_STORE) {
+    if (p.vec) {   // the main loop ended on a barrier: the LDS is free
+      vec_epilogue<P, TM, TN>(p, smem, acc, wave, lane, m0 + wm * TM * 16, n0 + wn * TN * 16, z);
+      vec_done = true;
+    }
+  }
+  if (!vec_done) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        p.store(m0 + (wm * TM + i) * 16 + 4 * fg + r, n0 + (wn * TN + j) * 16 + fr, z, acc[i][j][r]);
+        for (int r = 0; r < 4; ++r)
+          p.store(m0 + (wm * TM + i) * 16 + 4 * fg + r, n0 + (wn * TN + j) * 16 + fr, z, acc[i][j][r]);
+  }
   if constexpr (P::BIAS_FROM_A) {
     if (n0 == 0) {   // fixed-order combine of the G partials of each row
+      __syncthreads();   // the vector epilogue's LDS slices are read
       constexpr int G = NT / BM;
       smem[tid] = bias_acc;   // the main loop ended on a barrier
       __syncthreads();
@@ -600,16 +634,27 @@ __global__ __launch_bounds__(P::NT) void igemm_x9s_kernel(const P p) {
     __syncthreads();
   }
 
+  bool vec_done = false;
+  if constexpr (P::VEC_STORE) {
+    if (p.vec) {   // the main loop ended on a barrier: the LDS is free
+      vec_epilogue<P, TM, TN>(p, reinterpret_cast<float*>(smem), acc, wave, lane, m0 + wm * TM * 16, n0 + wn * TN * 16,
+                              z);
+      vec_done = true;
+    }
+  }
+  if (!vec_done) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        p.store(m0 + (wm * TM + i) * 16 + 4 * fg + r, n0 + (wn * TN + j) * 16 + fr, z, acc[i][j][r]);
+        for (int r = 0; r < 4; ++r)
+          p.store(m0 + (wm * TM + i) * 16 + 4 * fg + r, n0 + (wn * TN + j) * 16 + fr, z, acc[i][j][r]);
+  }
   if constexpr (P::BIAS_FROM_A) {
     if (bias_on) {   // row r: its four k-groups' partials, fixed order (k0 + k1) + (k2 + k3)
-      float* red = reinterpret_cast<float*>(smem);   // the main loop ended on a barrier
+      __syncthreads();   // the vector epilogue's LDS slices are read
+      float* red = reinterpret_cast<float*>(smem);
       if (aon[0])
 #pragma unroll
         for (int q = 0; q < 4; ++q) red[(ak[0] >> 3) * BM + arow[0] + q] = bias_acc[q];
