@@ -106,6 +106,9 @@ def main():
                                    hw.data_ptr() + 4 * (H + 1), hw.data_ptr() + 4 * (9 * H + 1), 8, None, 7, 0, 0,
                                    None, hv.data_ptr(), ha.data_ptr(), hv.data_ptr() + 4 * B, hv.data_ptr() + 8 * B,
                                    s), 0.0),
+        # the c5 GRU input gradient dh = (dgi [B][768] . W_ih[:, :256]) masked by the fc ReLU (ppo_linear_dgrad_ex)
+        "gru_dx": (lambda: call("ppo_linear_dgrad_ex", dz3.data_ptr(), B, 768, w4.data_ptr(), 256, a3.data_ptr(), 1568,
+                                1, dz2.data_ptr(), s), 2.0 * B * 768 * 256),
         "fc_fwd_generic": (lambda: call("ppo_linear_relu_fwd", a3.data_ptr(), B, 1568, pk[2], b4.data_ptr(), H,
                                         h.data_ptr(), s), 2.0 * B * 1568 * H),
         "fc_dgrad": (lambda: call("ppo_linear_dgrad_mask", dh.data_ptr(), B, H, pk[3], 1568, a3.data_ptr(),
