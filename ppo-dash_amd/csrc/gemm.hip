@@ -2311,6 +2311,8 @@ PPO_API int ppo_linear_fwd_ex(const float* x, const int64_t* idx, int M, int K, 
     DenseReluFwd<X128> p;
     p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = act;
     p.idx = idx;
+    p.vec = g_tune[TK_FC_FWD] != 1 && N % 4 == 0 && (ldo ? ldo : N) % 4 == 0 && ((uintptr_t)out & 15) == 0 &&
+            (b == nullptr || ((uintptr_t)b & 15) == 0);
     return launch_x9(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);
   }
   if (N % 128 == 0) {
@@ -2333,6 +2335,8 @@ PPO_API int ppo_linear_dgrad_ex(const float* dy, int M, int K, const float* wt, 
   if (use_x9()) {
     DenseDgradMask<X128> p;
     p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K; p.ldact = ldact; p.mode = mode;
+    p.vec = g_tune[TK_FC_DGRAD] != 1 && N % 4 == 0 && (ldact ? ldact : N) % 4 == 0 && ((uintptr_t)dx & 15) == 0 &&
+            (act == nullptr || ((uintptr_t)act & 15) == 0);
     return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_ex", 2.0 * M * N * K);
   }
   DenseDgradMask<CfgN128> p;
