@@ -405,13 +405,14 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(envs, T, E, M, hidden, threads):
+def cpu_baseline(envs, T, E, M, hidden, threads, reps=3):
     """The reference's CPU path (T/run.py:168-248: act -> env -> insert x T,
     get_value, compute_returns, PPO.update with torch.optim.Adam and
     clip_grad_norm_, after_update) restated in torch (oracle/torch_ref.py, pinned
     to the reference's recorded iteration), fp32 observations as the reference
-    stores them, timed for one iteration of `envs` lanes x T steps — at 1 thread
-    (the reference's torch.set_num_threads(1), T/run.py:55) and at `threads`."""
+    stores them, `envs` lanes x T steps per iteration — at 1 thread (the
+    reference's torch.set_num_threads(1), T/run.py:55) and at `threads`: a short
+    warm-up iteration, then the median of `reps` timed iterations."""
     from a2c_ppo_acktr.model import CNNBase, Policy
     from a2c_ppo_acktr.synthetic import Discrete
     from oracle import torch_ref as TR
@@ -428,21 +429,29 @@ def cpu_baseline(envs, T, E, M, hidden, threads):
             opt = torch.optim.Adam(p, lr=1e-4, eps=1e-5)
             gen = torch.Generator().manual_seed(123)
             frames = TR.env_frames(envs, gen=gen)
-            t0 = time.perf_counter()
-            TR.run_iteration(p, opt, envs, T, ppo_epoch=E, num_mini_batch=M, gen=gen, frames=frames)
-            dt = time.perf_counter() - t0
-            runs[th] = (envs * T / dt, dt)
+            # one short warm-up iteration (allocator, thread pool), then the median of
+            # `reps` whole iterations
+            TR.run_iteration(p, opt, envs, max(T // 8, 1), ppo_epoch=1, num_mini_batch=M, gen=gen, frames=frames)
+            times = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                TR.run_iteration(p, opt, envs, T, ppo_epoch=E, num_mini_batch=M, gen=gen, frames=frames)
+                times.append(time.perf_counter() - t0)
+            dt = sorted(times)[len(times) // 2]
+            runs[th] = (envs * T / dt, dt, times)
     finally:
         torch.set_num_threads(saved)
         torch.set_rng_state(rng_state)
     best = max(runs, key=lambda k: runs[k][0])
     return {"value": round(runs[best][0], 2), "unit": "env-steps/s", "cores": best, "kind": "port",
             "cpu_model": cpu_model(),
-            "by_threads": {str(k): {"value": round(v[0], 2), "seconds": round(v[1], 2)} for k, v in runs.items()},
+            "by_threads": {str(k): {"value": round(v[0], 2), "seconds": round(v[1], 2),
+                                    "runs_s": [round(x, 3) for x in v[2]]} for k, v in runs.items()},
             "sample": f"the reference CPU path (T/run.py:168-248) restated in torch on the host "
                       f"(oracle/torch_ref.py: F.conv2d/linear, autograd, torch.optim.Adam, clip_grad_norm_, "
                       f"fp32 obs storage), CNNBase H={hidden}, {envs} envs x {T} steps, {E} epochs x {M} "
-                      f"minibatches, one iteration per thread setting; value = the faster setting"}
+                      f"minibatches; per thread setting one warm-up iteration then the median of {reps} "
+                      f"iterations; value = the faster setting"}
 
 
 def free_port():

@@ -114,10 +114,38 @@ def _timed_all_reduce(t):
 
 
 _OVERLAP = {"on": True, "stream": {}}
-# started tail buckets: end address of the tail -> (event or None, element count);
-# allreduce_grads of a buffer ending there waits for it and reduces only the rest,
-# so no caller can sum a tail twice
+# started tail buckets of the CURRENT minibatch: end address of the tail -> (event or
+# None, element count); allreduce_grads of a buffer ending there waits for it and
+# reduces only the rest, so no caller can sum a tail twice.  begin_minibatch() drops
+# entries a failed minibatch left behind (after the current stream has waited for
+# their collectives), so a later buffer at the same address never matches a stale one.
 _PENDING = {}
+
+
+def begin_minibatch():
+    """Called by the engines before a minibatch's backward: joins and forgets any
+    tail bucket that no allreduce_grads consumed (an exception between
+    start_bucket and the optimizer step).  Its side-stream collective still writes
+    into the gradient buffer, so the current stream waits for it first."""
+    for done, _ in _PENDING.values():
+        if done is not None:
+            torch.cuda.current_stream().wait_event(done)
+    _PENDING.clear()
+
+
+def pending_buckets():
+    """number of started tail buckets not yet joined into the current stream"""
+    return len(_PENDING)
+
+
+def assert_no_pending(what):
+    """Persistent GRU launches need all their blocks co-resident: a collective
+    kernel running beside them on a side stream could hold CUs they wait for.
+    Every started bucket is joined (current stream waits for its event) in
+    allreduce_grads before clip + Adam, so none may be pending when such a
+    launch is queued on the current stream."""
+    if _PENDING:
+        raise RuntimeError(f"{what}: {len(_PENDING)} gradient bucket(s) still reducing on a side stream")
 
 
 def overlap_buckets(on=True):
@@ -172,6 +200,19 @@ def allreduce_grads(grad):
         else:
             _timed_all_reduce(grad)
     return 1.0 / G
+
+
+def global_guard(err, bad, out):
+    """The optimizer-step guard made global (G > 1): out (float64 [1], device) =
+    Σ over ranks of (err != 0) + bad, where err is this rank's persistent-GRU error
+    word (int32 view) and bad its count of out-of-range stored actions (float64
+    view).  The gradient the step consumes is already summed over ranks, so a
+    failure on ANY rank must skip the step on EVERY rank; clip + Adam read out
+    (> 0 skips).  Both terms are >= 0, so the sum is > 0 iff some rank failed."""
+    torch.add(bad, (err != 0).to(torch.float64), out=out)
+    if active():
+        dist.all_reduce(out)
+    return out
 
 
 def allreduce_losses(acc):

@@ -362,6 +362,7 @@ class CNNEngine:
         storage rows idx (int64 [B], device)."""
         self.ensure_bound()
         self.pack()
+        _dist.begin_minibatch()
         B = idx.numel()
         ws = self.ws["train"]
         h = self.trunk(storage.obs, idx, B, ws)
@@ -519,6 +520,7 @@ class RecurrentEngine(CNNEngine):
         the n envs `envs` (int64 device), BPTT over the full T, then one Adam step."""
         self.ensure_bound()
         self.pack()
+        _dist.begin_minibatch()
         dev, H, s = self.device, self.H, stream()
         T, N, n = storage.num_steps, storage.rewards.shape[1], envs.numel()
         R = T * n
@@ -534,7 +536,9 @@ class RecurrentEngine(CNNEngine):
         sv = {k: ws.get("s_" + k, R * H, device=dev) for k in ("r", "z", "n", "ghn", "hin")}
         masks = storage.masks
         cnt = ws.get("gru_cnt", call("ppo_gru_seq_counters", n), torch.int32, dev)
-        # error word status[0]: sticky for the update, gates every clip + Adam after a timeout
+        # error word status[0]: sticky for the update, gates every clip + Adam after a timeout;
+        # no gradient bucket may still be reducing on a side stream beside the persistent launch
+        _dist.assert_no_pending("train_minibatch_rec")
         call("ppo_gru_seq_fwd_ws", h0.data_ptr(), masks.data_ptr(), idx.data_ptr(), self.pv(self.GHH),
              self.pv(self.GBH), gi.data_ptr(), T, n, H, hout.data_ptr(), sv["r"].data_ptr(), sv["z"].data_ptr(),
              sv["n"].data_ptr(), sv["ghn"].data_ptr(), sv["hin"].data_ptr(), cnt.data_ptr(), self.status_ptr(0), s)
@@ -646,6 +650,7 @@ class MLPEngine(CNNEngine):
     def train_minibatch(self, storage, adv, idx, hp, loss_acc, optimizer):
         self.ensure_bound()
         self.pack()
+        _dist.begin_minibatch()
         dev, H, B = self.device, self.H, idx.numel()
         ws = self.ws["train"]
         x = self._x(storage.obs, storage.vector_obs if self.V else None, idx, B, ws)

@@ -37,9 +37,11 @@ class FlatAdam(object):
         self._partials = None
         self.last_grad_norm = None
         self._norm = None
-        # (int* error word, double* bad-action count, int* skipped-step count) device
-        # pointers set by PPO.update: a guarded step is skipped on the device
+        # (int32 [1] error word, float64 [1] bad-action count, int* skipped-step count)
+        # set by PPO.update: a guarded step is skipped on the device (on every rank
+        # when any rank's guard is set, _dist.global_guard)
         self.guard = None
+        self._gflag = None
 
     def zero_grad(self, set_to_none=False):
         for p in self.param_groups[0]["params"]:
@@ -70,7 +72,17 @@ class FlatAdam(object):
         s = stream()
         call("ppo_grad_sumsq", eng.grad.data_ptr(), n, scale, self._partials.data_ptr(), s)
         mn = self.max_grad_norm if self.max_grad_norm is not None else -1.0
-        gi, gd, sk = self.guard if self.guard is not None else (None, None, None)
+        gi = gd = sk = None
+        if self.guard is not None:
+            err, bad, sk = self.guard
+            if _dist.active():
+                # the gradient is already summed over ranks: any rank's failure skips the
+                # step on every rank (one 8-byte all-reduce), so all ranks stay identical
+                if self._gflag is None or self._gflag.device != eng.device:
+                    self._gflag = torch.zeros(1, dtype=torch.float64, device=eng.device)
+                gd = _dist.global_guard(err, bad, self._gflag).data_ptr()
+            else:
+                gi, gd = err.data_ptr(), bad.data_ptr()
         call("ppo_clip_adam_guarded", eng.flat.data_ptr(), eng.grad.data_ptr(), self.exp_avg.data_ptr(),
              self.exp_avg_sq.data_ptr(), n, self._partials.data_ptr(), scale, float(mn), float(g["lr"]),
              float(b1), float(b2), float(g["eps"]), self.step_count, self._norm.data_ptr(), gi, gd, sk, s)
@@ -127,7 +139,7 @@ class PPO():
         # (status[0]) or an out-of-range stored action (loss_acc[3]) turns the step
         # into a no-op on the device, counted in status[1]; _losses() raises
         eng.status[:2].zero_()
-        self.optimizer.guard = (eng.status_ptr(0), self._loss_acc.data_ptr() + 8 * 3, eng.status_ptr(1))
+        self.optimizer.guard = (eng.status[0:1], self._loss_acc[3:4], eng.status_ptr(1))
         hp = {"clip": float(self.clip_param), "value_coef": float(self.value_loss_coef),
               "entropy_coef": float(self.entropy_coef), "use_clipped_value_loss": bool(self.use_clipped_value_loss)}
         num_steps, num_processes = rollouts.rewards.size()[0:2]

@@ -54,6 +54,24 @@ def _worker(rank, world, port, out):
     assert _dist.start_bucket(gb[30:])
     assert _dist.allreduce_grads(gb) == scale   # reduces the head only
     assert torch.equal(gb, g)
+    # a started bucket no allreduce_grads consumed (a minibatch that raised in between)
+    # is forgotten by the next minibatch: the next gradient is reduced whole
+    assert _dist.start_bucket(g_local.clone()[30:]) and _dist.pending_buckets() == 1
+    _dist.begin_minibatch()
+    assert _dist.pending_buckets() == 0
+    gc = g_local.clone()
+    _dist.allreduce_grads(gc)
+    assert torch.equal(gc, g)
+    # the optimizer-step guard is global: only rank 1 flags, both ranks see it
+    flag = torch.zeros(1, dtype=torch.float64)
+    _dist.global_guard(torch.tensor([0], dtype=torch.int32),
+                       torch.tensor([1.0 if rank == 1 else 0.0], dtype=torch.float64), flag)
+    assert flag.item() == 1.0
+    _dist.global_guard(torch.tensor([7 if rank == 0 else 0], dtype=torch.int32),
+                       torch.tensor([0.0], dtype=torch.float64), flag)
+    assert flag.item() == 1.0
+    _dist.global_guard(torch.tensor([0], dtype=torch.int32), torch.tensor([0.0], dtype=torch.float64), flag)
+    assert flag.item() == 0.0
     p1, *_ = O.clip_adam(params.numpy().astype(np.float64), gmean, np.zeros(P), np.zeros(P), 1, 1e-3, 1e-5, 0.5)
     losses = torch.tensor([1.0 + rank, 2.0, 3.0], dtype=torch.float64)
     _dist.allreduce_losses(losses)
