@@ -198,6 +198,27 @@ int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, float* slab
 int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, float* slab, float* slab_bias, void* stream);
 int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int K, int Z, float* slab, float* slab_bias,
                      void* stream);
+/* conv1 -> conv2 with conv1's output pre-split (a1split.hip; replaces the a1 hand-off
+ * of model.py:177-178 inside ppo_conv1_fwd / ppo_conv2_fwd / ppo_conv2_wgrad): conv1
+ * on u8 observations (C = 4) writes a1 = relu(conv1) as three exact bf16 planes
+ * a1s [B][4800 units of 16 B] (unit (p, c, rho) = channels 8c..8c+7 of pixel (y, x)
+ * in plane p, rho = 100 (2 (y & 1) + (x & 1)) + 10 (y >> 1) + (x >> 1)); conv2's
+ * forward stages it by LDS-DMA and its weight gradient without the split.  Results
+ * are bit-identical to the fp32-a1 kernels.  fp32 arithmetic only (products 6 / 9):
+ * ppo_a1split_enabled() says whether the engine takes this path (tune "a1split"). */
+/* CU-contention probe (probe.hip; diagnostics, not on the training path): `blocks`
+ * workgroups that each spin for `ticks` of the 100 MHz s_memrealtime counter and record
+ * (start, end) into stamps [blocks][2]; ppo_probe_now writes the counter's current value */
+int ppo_probe_side_kernel(int blocks, int threads, long long ticks, long long* stamps, void* stream);
+int ppo_probe_now(long long* out, void* stream);
+long long ppo_a1s_bytes(int B);
+int ppo_a1split_enabled(void);
+int ppo_conv1_fwd_split(const uint8_t* obs, const int64_t* idx, long long row0, int B, const float* w1,
+                        const float* b1, uint16_t* a1s, uint32_t* mbits, void* stream);
+int ppo_conv2_fwd_split(const uint16_t* a1s, int B, const float* w2p, const float* b2, float* out, uint64_t* mbits,
+                        void* stream);
+int ppo_conv2_wgrad_split(const float* dz2, const uint16_t* a1s, int B, int Z, float* slab, float* slab_bias,
+                          void* stream);
 /* scale multiplies the weight sums only (conv1 with u8 observations stages the
  * bytes as integers: pass 1/255); bias sums are unscaled */
 int ppo_wgrad_reduce(const float* slab, const float* slab_bias, int Z, int M, int NW, int kind, int a, int b,

@@ -1873,10 +1873,10 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
 // ---------------------------------------------------------------------------
 enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_X9,
-       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_FC_DGRAD, TK_FC_WGRAD, TK_ORDER, TK_FC_SPLITK, TK_N };
+       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_FC_DGRAD, TK_FC_WGRAD, TK_ORDER, TK_FC_SPLITK, TK_A1SPLIT, TK_N };
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
                                          "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad", "fc_dgrad", "fc_wgrad",
-                                         "order", "fc_splitk"};
+                                         "order", "fc_splitk", "a1split"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
@@ -1887,7 +1887,8 @@ static int g_small_b = 4;
 // order: fc tile order override for A/B (0: per-layer default, 1: m fastest, 2: n fastest; igemm_x9.h tile_of;
 // 3: the default order with the fc weight gradient's scalar epilogue, for A/B)
 // fc_splitk: K slices of the rollout-sized fc forward with a workspace (ppo_fc_fwd_ws; <= 1: unsplit)
-static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0, 0, 2};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
+// a1split: conv1 writes its output pre-split for conv2 (a1split.hip; 1 on, 0 the fp32 a1 hand-off)
+static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0, 0, 2, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 int heads_lds_knob(int set, int value);   // heads.hip (the LDS-weight heads_train kernel, default on)
 
@@ -1980,6 +1981,11 @@ static int device_cus() {
   return n_cu;
 }
 
+// accessors for the kernels in other translation units (a1split.hip)
+int gemm_products() { return g_products; }
+int gemm_device_cus() { return device_cus(); }
+PPO_API int ppo_a1split_enabled() { return g_tune[TK_A1SPLIT] != 0 && g_products != 1 ? 1 : 0; }
+
 static inline bool use_x9() { return g_tune[TK_X9] != 0; }
 static inline bool use_x9_all() { return g_tune[TK_X9] == 2; }
 template <class P>
@@ -2000,6 +2006,8 @@ static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, lo
                           const float* w1, const float* b1, float* out, uint16_t* mbits, void* stream);
 int conv1_wgrad_u8_tr(const float* dz1, const uint8_t* obs, const int64_t* idx, long long row0, int B, int Z,
                       float* slab, float* slab_bias, void* stream);   // conv1f.hip
+int conv1_wgrad_kw(const float* dz1, const uint8_t* obs, const int64_t* idx, long long row0, int B, int Z,
+                   float* slab, float* slab_bias, int variant, void* stream);   // conv1w.hip
 
 // conv1 forward: out [B][20][20][32] = relu(conv(obs rows, W1 torch layout) + b1)
 PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
@@ -2533,6 +2541,9 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
     PPO_LAUNCH_CHECK("conv1_wgrad_parts_kernel");
     return 0;
   }
+  if (obs_is_u8 && C == 4 && (g_tune[TK_CONV1_WGRAD] == 7 || g_tune[TK_CONV1_WGRAD] == 8) && g_products != 1)
+    return conv1_wgrad_kw(dz1, (const uint8_t*)obs, idx, row0, B, Z, slab, slab_bias, g_tune[TK_CONV1_WGRAD],
+                          stream);   // conv1w.hip, k-split over waves (8: u8 image by LDS-DMA)
   if (!obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] != 9 && ((uintptr_t)obs & 15) == 0)   // conv1f.hip
     return ppo_conv1_wgrad_f32(dz1, (const float*)obs, idx, row0, B, Z, slab, slab_bias, stream);
   if (obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] == 6)   // conv1f.hip, tr_b16 im2col (A/B)

@@ -9,7 +9,7 @@ device tensors, each rank with its own env lanes.  Modes (argv[4]):
           the reduced gradient equals (g_0 + g_1) / 2 bit for bit
   guard   (tests/test_dist_gpu.py) rank 1 alone stores an out-of-range action:
           every rank must skip every step (parameters, Adam moments, step count
-          unchanged) and raise""")
+          unchanged) and raise"""
 import json
 import os
 import sys

@@ -60,3 +60,20 @@ def test_guard_skips_on_every_rank():
     for o in outs:
         assert o["raised"], o
         assert o["params_kept"] and o["moments_zero"] and o["step_count"] == 0, o
+
+
+def test_gru_launch_after_bucket_join():
+    """Persistent GRU launches need their blocks co-resident; a collective kernel on
+    the side stream could hold CUs they wait for.  A started gradient bucket is
+    pending until allreduce_grads joins it (the current stream waits for it) and
+    _dist.assert_no_pending refuses a persistent launch meanwhile; a recurrent
+    update with the collectives forced on (one-rank gloo group on the device) runs
+    every minibatch's GRU launches with no bucket pending, and trains."""
+    import subprocess
+    worker = os.path.join(os.path.dirname(__file__), "helpers", "rank1_gru_worker.py")
+    r = subprocess.run([sys.executable, worker], capture_output=True, text=True, timeout=150)
+    assert r.returncode == 0, r.stderr[-3000:]
+    o = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert o["bucket_started"] and o["pending_after_start"] == 1 and o["refused"]
+    assert o["pending_after_join"] == 0 and o["pending_at_end"] == 0
+    assert o["losses_finite"] and o["moved"] > 0

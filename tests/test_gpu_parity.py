@@ -1388,11 +1388,13 @@ def test_gru_persistent_bptt_timeout_sets_error(gpu):
     assert err.item() == 0 and torch.isfinite(dgi).all() and (dgi[: n] != 0).any()
 
 
-@pytest.mark.parametrize("variant", [3, 4, 5, 6, 9])
+@pytest.mark.parametrize("variant", [3, 4, 5, 6, 7, 8, 9])
 def test_conv1_wgrad_variants_vs_torch(gpu, variant):
     """conv1 weight + bias gradient from u8 observations gathered by index (the
     minibatch path): the part-pipelined bf16x3 kernel with 8 (3) and 16
-    waves (4; 5 two tiles per wave) and the fp32 tile GEMM (9) vs torch float64
+    waves (4; 5 two tiles per wave), the k-split kernel of conv1w.hip (7: B = 300
+    and Z = 256 leave blocks with one and two images) and the fp32 tile GEMM (9)
+    vs torch float64
     on (u8 / 255):
     max |err| <= 1e-5 * max |ref|.
     B = 300 images, rows gathered out of order."""
