@@ -1888,7 +1888,7 @@ static int g_small_b = 4;
 // 3: the default order with the fc weight gradient's scalar epilogue, for A/B)
 // fc_splitk: K slices of the rollout-sized fc forward with a workspace (ppo_fc_fwd_ws; <= 1: unsplit)
 // a1split: conv1 writes its output pre-split for conv2 (a1split.hip; 1 on, 0 the fp32 a1 hand-off)
-static int g_tune[TK_N] = {0, 8, 8, 8, 5, 0, 12, 1, 8, 8, 0, 0, 0, 2, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 8, 8, 8, 8, 0, 12, 1, 8, 8, 0, 0, 0, 2, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 int heads_lds_knob(int set, int value);   // heads.hip (the LDS-weight heads_train kernel, default on)
 
@@ -2517,12 +2517,15 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
   const long long R = (long long)B * 400;
   PPO_REQUIRE(R < 0x7fffffffLL, "ppo_conv1_wgrad: B too large");
   const double fl = 2.0 * R * 32 * C * 64;
-  if (obs_is_u8 && C == 4 && (g_tune[TK_CONV1_WGRAD] >= 3 && g_tune[TK_CONV1_WGRAD] <= 5)) {   // part-pipelined
+  const int c1w = g_tune[TK_CONV1_WGRAD];
+  // part-pipelined (3-5; also the half-precision mode under the k-split tunes 7 / 8, which
+  // exist for fp32 dz only: the bf16-dz part kernel, tune 5's, runs there)
+  if (obs_is_u8 && C == 4 && ((c1w >= 3 && c1w <= 5) || ((c1w == 7 || c1w == 8) && g_products == 1))) {
     if (B <= 0 || Z <= 0) return 0;
     PPO_REQUIRE((B + Z - 1) / Z <= 512, "ppo_conv1_wgrad: %d images over %d blocks (at most 512 per block)", B, Z);
     int slot;
     const bool prof = ppo_prof_begin("conv1_wgrad_u8", as_stream(stream), &slot);
-    if (g_products == 1 && g_tune[TK_CONV1_WGRAD] == 5)   // half-precision mode: bf16 dz
+    if (g_products == 1 && c1w != 3 && c1w != 4)   // half-precision mode: bf16 dz
       conv1_wgrad_parts_kernel<1, 16, 2><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
                                                                             slab, slab_bias, 0);
     else if (g_products == 1)
