@@ -70,6 +70,7 @@ SIGNATURES = {
     # probe.hip (CU-contention diagnostics)
     "ppo_probe_side_kernel": [c_int, c_int, c_ll, c_p, c_p],
     "ppo_probe_now": [c_p, c_p],
+    "ppo_probe_conv2_wgrad_anatomy": [c_int, c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     # a1split.hip (conv1 output pre-split for conv2)
     "ppo_a1s_bytes": [c_int],
     "ppo_a1split_enabled": [],

@@ -897,7 +897,9 @@ __device__ __forceinline__ int c2w_pix(int r) {
   return r < 72 ? (r >> 3) * 9 + (r & 7) : (r - 72) * 9 + 8;
 }
 
-template <int NP>
+// DBG (timing anatomy only, ppo_probe_conv2_wgrad_anatomy; wrong results): 1 skips
+// the MFMAs, 2 the LDS staging (split + ds_write), 4 the global loads
+template <int NP, int DBG = 0>
 __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __restrict__ dz2,
                                                             const float* __restrict__ a1, int B,
                                                             float* __restrict__ slab,
@@ -933,6 +935,7 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
   float ds[DPER][8];
   float bsum = 0.f;   // bias partial of co = tid & 63 (fixed for this thread's D units)
   auto fetch = [&](int b) {
+    if constexpr ((DBG & 4) != 0) return;
     const f32x4* src = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
 #pragma unroll
     for (int j = 0; j < XPER; ++j)
@@ -951,6 +954,7 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
     }
   };
   auto put = [&]() {
+    if constexpr ((DBG & 2) != 0) return;
 #pragma unroll
     for (int j = 0; j < XPER; ++j)
       if (tid + 512 * j < XU) {
@@ -1021,14 +1025,19 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
         bf.l = __builtin_bit_cast(bf16x8, __builtin_shufflevector(t[2][0], t[2][1], 0, 1, 2, 3, 4, 5, 6, 7));
 #define PPO_PART(XX, YY) \
   _Pragma("unroll") for (int mt = 0; mt < 4; ++mt) acc[j][mt] = mma(a[mt].XX, bf.YY, acc[j][mt]);
-        PPO_PRODUCTS(NP, PPO_PART)
+        if constexpr ((DBG & 1) == 0) {
+          PPO_PRODUCTS(NP, PPO_PART)
+        } else {   // keep the fragment reads live
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) acc[j][mt][0] += (float)a[mt].h[0] + (float)bf.h[0] + (float)bf.l[1];
+        }
 #undef PPO_PART
       }
     }
-    __syncthreads();   // the image is consumed
+    lds_barrier();   // the image is consumed (LDS-only: the prefetch stays in flight)
     if (b + Z < B) put();
     if (b + 2 * Z < B) fetch(b + 2 * Z);
-    __syncthreads();   // the next image is in LDS
+    lds_barrier();   // the next image is in LDS (the image after next still loading)
   }
   // this block's partial: C row 4g + r of co tile mt, column i16 of n tile j
   float* o = slab + (size_t)blockIdx.x * (64 * 512) + 64 * wave + i16;
@@ -2590,6 +2599,26 @@ PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, flo
   set_wgrad(p, dz2, 64, (long long)B * 81, Z, slab, slab_bias, 512);
   p.in = a1;
   return launch(p, 64, 512, Z, as_stream(stream), "conv2_wgrad", 2.0 * B * 81 * 64 * 512);
+}
+
+// timing anatomy of the conv2 weight gradient (diagnostics, wrong results by design): dbg bits as
+// conv2_wgrad_x9_kernel's DBG (1 no MFMAs, 2 no LDS staging, 4 no global loads)
+PPO_API int ppo_probe_conv2_wgrad_anatomy(int dbg, const float* dz2, const float* a1, int B, int Z, float* slab,
+                                          float* slab_bias, void* stream) {
+  PPO_REQUIRE(B > 0 && Z > 0 && dbg >= 0 && dbg < 8, "ppo_probe_conv2_wgrad_anatomy: B=%d Z=%d dbg=%d", B, Z, dbg);
+  hipStream_t st = as_stream(stream);
+  switch (dbg) {
+    case 0: conv2_wgrad_x9_kernel<6, 0><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    case 1: conv2_wgrad_x9_kernel<6, 1><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    case 2: conv2_wgrad_x9_kernel<6, 2><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    case 3: conv2_wgrad_x9_kernel<6, 3><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    case 4: conv2_wgrad_x9_kernel<6, 4><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    case 5: conv2_wgrad_x9_kernel<6, 5><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    case 6: conv2_wgrad_x9_kernel<6, 6><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    default: conv2_wgrad_x9_kernel<6, 7><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+  }
+  PPO_LAUNCH_CHECK("conv2_wgrad_x9_kernel (anatomy)");
+  return 0;
 }
 
 PPO_API int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, float* slab, float* slab_bias,

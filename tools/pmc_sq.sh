@@ -10,7 +10,7 @@ SETS=("SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_AC
 i=0
 for s in "${SETS[@]}"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $s --output-format csv -d gpurun_out/pmc1 -o p$i -- python3 tools/kbench.py --reps 2 --only $ONLY --tune "${TUNE:-stagger=0}" > gpurun_out/pmc1/log$i.txt 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $s --output-format csv -d gpurun_out/pmc1 -o p$i -- python3 tools/kbench.py --reps 2 --only $ONLY --tune "${TUNE:-stagger=0}" ${KBARGS:-} > gpurun_out/pmc1/log$i.txt 2>&1
   rc=$?; echo "set $i: rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/pmc1/log$i.txt; exit $rc; }
 done
 for k in ${ONLY//,/ }; do echo "== $k"; done
