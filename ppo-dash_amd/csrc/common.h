@@ -103,10 +103,11 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
-// workgroup barrier that publishes LDS writes (lgkmcnt(0)) but leaves global loads
-// in flight: __syncthreads' fence would wait for every outstanding load (vmcnt(0)),
-// i.e. for the register prefetch of the next items; the compiler still waits for
-// those loads where their registers are used
+// workgroup barrier publishing LDS writes (lgkmcnt(0)) as one asm statement, for
+// the kernels that stage LDS by DMA (global_load_lds, asm) and wait for it with
+// their own vmcnt counts.  On gfx950 __syncthreads emits the same two instructions
+// (its workgroup fence adds no vmcnt wait: loads in flight stay in flight), so
+// elsewhere the two are interchangeable.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Range-checked buffer stores: a store whose byte offset is out of the

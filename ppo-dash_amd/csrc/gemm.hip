@@ -711,7 +711,7 @@ struct Conv2Dgrad : C_ {
 //     stage's planes 0-1 during k-steps 0-3, its lo parts held in registers
 //     until a mid-image barrier (after k-step 5) has retired the partial reads,
 //     then written during k-steps 6-7.  The image after next is fetched into
-//     registers from k-step 4 on.
+//     registers one unit per k-step (1-4), each once its register has been staged.
 //   * Epilogue in the swapped MFMA orientation (weights as A): one 16-B store of
 //     four consecutive channels per tile, dummy rows dropped by buffer range.
 template <int NP, bool MASK = false>
@@ -763,13 +763,14 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
   const bool has_last = tid + 512 * (UPER - 1) < UNITS;
   f32x4 stg[UPER][2];
   bf16x8 lo[UPER];
-  auto fetch = [&](int b) {   // unconditional loads (the 4th unit of waves 1-7 reloads unit 1599)
+  auto fetch_unit = [&](int b, int j) {   // unconditional (the 4th unit of waves 1-7 reloads unit 1599)
     const f32x4* src = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
+    stg[j][0] = src[usrc[j]];
+    stg[j][1] = src[usrc[j] + 1];
+  };
+  auto fetch = [&](int b) {
 #pragma unroll
-    for (int j = 0; j < UPER; ++j) {
-      stg[j][0] = src[usrc[j]];
-      stg[j][1] = src[usrc[j] + 1];
-    }
+    for (int j = 0; j < UPER; ++j) fetch_unit(b, j);
   };
   auto put_hm = [&](int j, int st) {   // hi / mid parts now, lo part held
     Frag3 f;
@@ -801,11 +802,14 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
       put_hm(j, 0);
       put_l(j, 0);
     }
-    if (b + G < B) fetch(b + G);
+    fetch(b + G < B ? b + G : b);
   }
   __syncthreads();
   for (; b < B; b += G) {
-    const bool nxt = b + G < B, nn = b + 2 * G < B;
+    // no branches in the k loop (a conditional load or stage write made the wait
+    // counts unknown at the merge: vmcnt(0) at every staging step): past the
+    // block's last image the staging re-reads / re-stages an image nothing uses
+    const int bnn = b + 2 * G < B ? b + 2 * G : b;
     const bf16x8* Sc = S + cur * STG;
     f32x4 acc[MT];
 #pragma unroll
@@ -832,10 +836,12 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
         PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
       }
-      if (s < UPER && nxt) put_hm(s, cur ^ 1);
-      if (s == UPER && nn) fetch(b + 2 * G);
+      if (s < UPER) put_hm(s, cur ^ 1);
+      // the image after next, one unit per k-step as its registers free up (all
+      // four at one k-step stalled every wave of the chip at the same time)
+      if (s >= 1 && s <= UPER) fetch_unit(bnn, s - 1);
       if (s == 5) lds_barrier();   // mid-image: the previous image's partials (lo plane of stage cur ^ 1) are read
-      if (s >= 6 && nxt) {
+      if (s >= 6) {
 #pragma unroll
         for (int j = 0; j < UPER; ++j)
           if ((j & 1) == s - 6) put_l(j, cur ^ 1);
@@ -898,7 +904,9 @@ __device__ __forceinline__ int c2w_pix(int r) {
 }
 
 // DBG (timing anatomy only, ppo_probe_conv2_wgrad_anatomy; wrong results): 1 skips
-// the MFMAs, 2 the LDS staging (split + ds_write), 4 the global loads
+// the MFMAs, 2 the LDS staging (split + ds_write), 4 the global loads; schedule
+// experiments (right results): 8 spreads the 8 load parts over all 12 slots, 16
+// starts the odd blocks half an image late (s_sleep)
 template <int NP, int DBG = 0>
 __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __restrict__ dz2,
                                                             const float* __restrict__ a1, int B,
@@ -934,26 +942,36 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
   f32x4 xs[XPER][2];
   float ds[DPER][8];
   float bsum = 0.f;   // bias partial of co = tid & 63 (fixed for this thread's D units)
-  auto fetch = [&](int b) {
+  // the next image's loads in 8 parts (a1 units j = 0..3, then dz2 units j = 0, 1
+  // in halves), issued one per (k-step, n tile) slot of the first two k-steps of
+  // the current image's MFMAs: issued between the barriers, with every CU at the
+  // same point, the 72 KB per image stalled the waves at issue for the whole
+  // chip's transfer time (tools/kbench.py conv2_wgrad_anat*: 0.66 of 1.78 ms)
+  auto fetch_part = [&](int b, int k) {
     if constexpr ((DBG & 4) != 0) return;
-    const f32x4* src = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
+    // per-image buffer resources: 32-bit offsets, and a load past the range (the
+    // a1 units >= XU, the dz2 slots >= 81) returns 0 without a branch
+    if (k < 4) {
+      const auto ra = make_rsrc(a1 + (size_t)b * 12800, 12800 * 4);
+      const int off = tid + 512 * k < XU ? xsrc[k] * 4 : 0x7ffffff0;
+      xs[k][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+      xs[k][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
+    } else {
+      const auto rd = make_rsrc(dz2 + (size_t)b * (81 * 64), 81 * 64 * 4);
+      const int j = (k - 4) >> 1, e0 = 4 * ((k - 4) & 1), v = tid + 512 * j;
 #pragma unroll
-    for (int j = 0; j < XPER; ++j)
-      if (tid + 512 * j < XU) { xs[j][0] = src[xsrc[j] / 4]; xs[j][1] = src[xsrc[j] / 4 + 1]; }
-    const float* dsrc = dz2 + (size_t)b * (81 * 64);
-#pragma unroll
-    for (int j = 0; j < DPER; ++j) {
-      const int v = tid + 512 * j;
-      if (v < DU) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int r = 8 * (v >> 6) + e;
-          ds[j][e] = r < 81 ? dsrc[c2w_pix(r) * 64 + (v & 63)] : 0.f;
-        }
+      for (int e = e0; e < e0 + 4; ++e) {
+        const int r = 8 * (v >> 6) + e;
+        const int off = v < DU && r < 81 ? (c2w_pix(r) * 64 + (v & 63)) * 4 : 0x7ffffff0;
+        ds[j][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, off, 0, 0));
       }
     }
   };
-  auto put = [&]() {
+  auto fetch = [&](int b) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) fetch_part(b, k);
+  };
+  auto put = [&](bool count) {   // count: add the dz2 to the bias partial
     if constexpr ((DBG & 2) != 0) return;
 #pragma unroll
     for (int j = 0; j < XPER; ++j)
@@ -972,7 +990,7 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
         split8(f32x4{ds[j][0], ds[j][1], ds[j][2], ds[j][3]}, f32x4{ds[j][4], ds[j][5], ds[j][6], ds[j][7]}, f,
                false);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) bsum += ds[j][e];
+        for (int e = 0; e < 8; ++e) bsum += count ? ds[j][e] : 0.f;
         const int off = (v & 63) * DR + 8 * (v >> 6);
         *reinterpret_cast<bf16x8*>(&D[off]) = f.h;
         *reinterpret_cast<bf16x8*>(&D[DPL + off]) = f.m;
@@ -987,14 +1005,17 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
     for (int mt = 0; mt < 4; ++mt) acc[j][mt] = zero4();
   const int Z = gridDim.x;
   int b = blockIdx.x;
+  if constexpr ((DBG & 16) != 0)
+    if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(100);
   if (b < B) {
     fetch(b);
-    put();
-    if (b + Z < B) fetch(b + Z);
+    put(true);
   }
   __syncthreads();
   typedef short s16x4 __attribute__((ext_vector_type(4)));
   for (; b < B; b += Z) {
+    const bool pf = b + Z < B;
+    const int bn = pf ? b + Z : b;   // the last image re-reads itself (no branch in the MFMA stream)
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
       Frag3 a[4];
@@ -1007,6 +1028,17 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        if constexpr ((DBG & 8) != 0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if ((3 * k) >> 1 == 4 * s + j) {
+              fetch_part(bn, k);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+        } else if (4 * s + j < 8) {
+          fetch_part(bn, 4 * s + j);
+          __builtin_amdgcn_sched_barrier(0);   // the loads stay in their slot
+        }
         const int tap = 2 * wave + (j >> 1), ky = tap >> 2, kx = tap & 3, cb = j & 1;
         const int toff = 20 * ky + 10 * (kx & 1) + (kx >> 1);
         s16x4 t[3][2];
@@ -1034,10 +1066,9 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
 #undef PPO_PART
       }
     }
-    lds_barrier();   // the image is consumed (LDS-only: the prefetch stays in flight)
-    if (b + Z < B) put();
-    if (b + 2 * Z < B) fetch(b + 2 * Z);
-    lds_barrier();   // the next image is in LDS (the image after next still loading)
+    __syncthreads();   // the image is consumed
+    put(pf);   // unconditional: every load is waited for inside the iteration
+    __syncthreads();   // the next image is in LDS
   }
   // this block's partial: C row 4g + r of co tile mt, column i16 of n tile j
   float* o = slab + (size_t)blockIdx.x * (64 * 512) + 64 * wave + i16;
@@ -2605,7 +2636,8 @@ PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, flo
 // conv2_wgrad_x9_kernel's DBG (1 no MFMAs, 2 no LDS staging, 4 no global loads)
 PPO_API int ppo_probe_conv2_wgrad_anatomy(int dbg, const float* dz2, const float* a1, int B, int Z, float* slab,
                                           float* slab_bias, void* stream) {
-  PPO_REQUIRE(B > 0 && Z > 0 && dbg >= 0 && dbg < 8, "ppo_probe_conv2_wgrad_anatomy: B=%d Z=%d dbg=%d", B, Z, dbg);
+  PPO_REQUIRE(B > 0 && Z > 0 && ((dbg >= 0 && dbg < 8) || dbg == 8 || dbg == 16 || dbg == 24),
+              "ppo_probe_conv2_wgrad_anatomy: B=%d Z=%d dbg=%d", B, Z, dbg);
   hipStream_t st = as_stream(stream);
   switch (dbg) {
     case 0: conv2_wgrad_x9_kernel<6, 0><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
@@ -2615,7 +2647,10 @@ PPO_API int ppo_probe_conv2_wgrad_anatomy(int dbg, const float* dz2, const float
     case 4: conv2_wgrad_x9_kernel<6, 4><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
     case 5: conv2_wgrad_x9_kernel<6, 5><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
     case 6: conv2_wgrad_x9_kernel<6, 6><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    default: conv2_wgrad_x9_kernel<6, 7><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    case 7: conv2_wgrad_x9_kernel<6, 7><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    case 8: conv2_wgrad_x9_kernel<6, 8><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    case 16: conv2_wgrad_x9_kernel<6, 16><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
+    default: conv2_wgrad_x9_kernel<6, 24><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
   }
   PPO_LAUNCH_CHECK("conv2_wgrad_x9_kernel (anatomy)");
   return 0;

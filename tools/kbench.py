@@ -163,7 +163,7 @@ def main():
         # timing anatomy of the conv2 weight gradient (wrong results): no MFMA / no staging / no loads
         **{f"conv2_wgrad_anat{d}": ((lambda d=d: call("ppo_probe_conv2_wgrad_anatomy", d, dz2.data_ptr(),
                                                          a1.data_ptr(), B, z2c, slab.data_ptr(), slab_b.data_ptr(),
-                                                         s)), 2.0 * B * 81 * 64 * 512) for d in range(8)},
+                                                         s)), 2.0 * B * 81 * 64 * 512) for d in (*range(8), 8, 16, 24)},
         "conv1_wreduce": (lambda: call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), z1, 32, 256, 0, 0, 0,
                                        gw.data_ptr(), gb.data_ptr(), 1.0 / 255, 0, s), 0.0),
     }
