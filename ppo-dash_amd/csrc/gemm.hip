@@ -1561,7 +1561,7 @@ __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __rest
 // BITS: the ReLU mask comes as bits (a1 points at u32 words [B][400] from
 // ppo_conv1_fwd_mask, 1.6 KB per image) instead of the fp32 activations
 // (51.2 KB per image): 40 % less HBM traffic, 12 % less time.
-template <int NP, bool BITS = false>
+template <int NP, bool BITS = false, bool ANAT = false>
 __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __restrict__ dz2, int B,
                                                             const uint16_t* __restrict__ wpl,
                                                             const float* __restrict__ a1,
@@ -1601,18 +1601,34 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
   f32x4 stg[PER][2];
   f32x4 mst[BITS ? 1 : MPER];
   uint4 mbv;
-  auto fetch = [&](int b) {
+  // part j of an image's loads: dz2 unit j (+ the mask bits with the last one)
+  auto fetch_part = [&](int b, int j) {
     const f32x4* src = reinterpret_cast<const f32x4*>(dz2 + (size_t)b * (HO * HO * CO));
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int c = tid + 512 * j;
-      const int cc = c < CH ? c : 0;   // unconditional loads: no exec branch around them
-      stg[j][0] = src[2 * cc];
-      stg[j][1] = src[2 * cc + 1];
-    }
+    const int c = tid + 512 * j;
+    const int cc = c < CH ? c : 0;   // unconditional loads: no exec branch around them
+    stg[j][0] = src[2 * cc];
+    stg[j][1] = src[2 * cc + 1];
     if constexpr (BITS) {
-      if (tid < 100) mbv = reinterpret_cast<const uint4*>(a1)[(size_t)b * 100 + tid];   // 400 words
+      if (j == PER - 1) {   // 400 words; lanes past them read out of range (0), no branch
+        const auto rm = make_rsrc(reinterpret_cast<const uint32_t*>(a1) + (size_t)b * 400, 1600);
+        mbv = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rm, tid < 100 ? 16 * tid : 0x7ffffff0,
+                                                                              0, 0));
+      }
+    }
+  };
+  auto fetch = [&](int b) {
+    if constexpr (BITS) {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) fetch_part(b, j);
     } else {
+      const f32x4* src = reinterpret_cast<const f32x4*>(dz2 + (size_t)b * (HO * HO * CO));
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int c = tid + 512 * j;
+        const int cc = c < CH ? c : 0;
+        stg[j][0] = src[2 * cc];
+        stg[j][1] = src[2 * cc + 1];
+      }
       const f32x4* ms = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
 #pragma unroll
       for (int j = 0; j < MPER; ++j) {
@@ -1655,20 +1671,34 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
     if (b + G < B) fetch(b + G);
   }
   __syncthreads();
-  const bool late = (stagger & 1) && wave >= 4;   // waves 4-7 stage after their compute (see conv3 dgrad)
+  const bool late = (stagger & 1) && wave >= 4;   // waves 4-7 stage after their compute (see conv3 dgrad; !BITS)
   // timing anatomy only (tools/kbench.py --tune stagger=...; wrong results):
-  // 16 skips the MFMAs, 32 the epilogue stores, 64 the staging of the next image
-  const bool no_mma = stagger & 16, no_epi = stagger & 32, no_stage = stagger & 64;
+  // 16 skips the MFMAs, 32 the epilogue stores, 64 the staging of the next image (!BITS)
+  // (compiled in only for ANAT: a runtime branch around the k loop costs the
+  // default kernel exact wait counts at its merge)
+  const bool no_mma = ANAT && (stagger & 16), no_epi = ANAT && (stagger & 32), no_stage = ANAT && (stagger & 64);
   f32x4 eacc[MT];
   int bprev = -1;
   const int cbs = (ph >> 1) * 640 + (ph & 1) * 32 + 16 * (wave & 1) + 4 * g;
+  // (bp < 0: before the first image, or no_epi: an empty range drops the store)
   auto store_tile = [&](int t, const f32x4& v, int bp) {
     const int eo = etab[16 * t + i16];
-    const auto rs = make_rsrc(dz1 + (size_t)bp * 12800, 12800 * 4);
+    const auto rs = make_rsrc(dz1 + (size_t)max(bp, 0) * 12800, bp >= 0 && !no_epi ? 12800 * 4 : 0);
     bstore_f32x4(v, rs, eo >= 0 ? 4 * (eo + cbs) : -1);
   };
   for (; b < B; b += G) {
-    if (!late && !no_stage) {
+    // BITS: branch-free staging (a conditional load made the wait counts unknown
+    // at the merge): the next image's stage is written unconditionally and the
+    // image after next (the block's last image re-read past the end) is loaded in
+    // two parts during k-steps 1 and 3, not all at once before the k loop
+    const int bnn = b + 2 * G < B ? b + 2 * G : b;
+    if constexpr (BITS) {
+      // every load in flight is this stage's (issued a k-step or more ago): wait
+      // for all of them here, or the partial unit's exec branch in put leaves them
+      // pending on one path and the fragment reads below wait one by one
+      __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0) (expcnt / lgkmcnt unconstrained)
+      put(cur ^ 1);
+    } else if (!late && !no_stage) {
       if (b + G < B) put(cur ^ 1);
       if (b + 2 * G < B) fetch(b + 2 * G);
     }
@@ -1677,9 +1707,9 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = zero4();
     if (no_mma) {   // anatomy only
-      if (bprev >= 0 && !no_epi)
 #pragma unroll
-        for (int t = 0; t < MT; ++t) store_tile(t, eacc[t], bprev);
+      for (int t = 0; t < MT; ++t) store_tile(t, eacc[t], bprev);
+      if constexpr (BITS) fetch(bnn);
     } else {
       // software pipeline over half k-steps: group 0 = {border tile of the tap
       // row, tiles 1, 2}, group 1 = tiles 3-5; the fragments of the next group
@@ -1726,8 +1756,13 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
           ld(s, 1);
           mm(s, 1);
         }
-        if (s < MT && bprev >= 0 && !no_epi) store_tile(s, eacc[s], bprev);
-        if constexpr (BITS) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (BITS) {
+          if (s < MT) store_tile(s, eacc[s], bprev);
+          if (s == 1 || s == 3) fetch_part(bnn, s >> 1);
+          __builtin_amdgcn_sched_barrier(0);
+        } else if (s < MT && bprev >= 0 && !no_epi) {
+          store_tile(s, eacc[s], bprev);
+        }
       }
     }
     // masked results of this image, stored during the next one's k-steps:
@@ -1744,7 +1779,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
       }
     }
     bprev = b;
-    if (late && !no_stage) {
+    if (!BITS && late && !no_stage) {
       if (b + G < B) put(cur ^ 1);
       if (b + 2 * G < B) fetch(b + 2 * G);
     }
@@ -2493,6 +2528,7 @@ static int conv2_dgrad_img(const float* dz2, int B, const float* w2d, const floa
   const int sg = g_stagger & ~2;
   if (g_products == 9) conv2_dgrad_x9_kernel<9, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
   else if (g_products == 1) conv2_dgrad_x9_kernel<1, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
+  else if (sg & 0x70) conv2_dgrad_x9_kernel<6, BITS, true><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
   else conv2_dgrad_x9_kernel<6, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
   if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
   PPO_LAUNCH_CHECK("conv2_dgrad_x9_kernel");

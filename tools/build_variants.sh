@@ -1,10 +1,12 @@
 #!/bin/bash
 # Build A/B variants of libppo_hip.so with extra -D flags (container-side):
 #   tools/build_variants.sh NAME "-DFOO=1 -DBAR=0" [NAME2 "FLAGS2" ...]
-# -> ppo-dash_amd/lib/libppo_hip_NAME.so (gemm.hip recompiled; other objects reused)
+# -> ppo-dash_amd/lib/libppo_hip_NAME.so (gemm.hip recompiled with the flags; the
+# other objects of the Makefile's build reused)
 set -e
 cd "$(dirname "$0")/../ppo-dash_amd"
-make -s build/storage.o build/gae.o build/gru.o build/heads.o build/optim.o build/obs.o
+make -s
+OTHERS=$(ls build/*.o | grep -v -e '^build/gemm.o$' -e '^build/gemm_')
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -fvisibility=hidden $flags -c csrc/gemm.hip -o build/gemm_$name.o &
@@ -12,7 +14,7 @@ done
 wait
 for o in build/gemm_*.o; do
   name=${o#build/gemm_}; name=${name%.o}
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o lib/libppo_hip_$name.so build/storage.o build/gae.o build/gru.o build/heads.o build/optim.o build/obs.o $o
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC -o lib/libppo_hip_$name.so $OTHERS $o
   rm -f $o
 done
 ls lib/
