@@ -211,8 +211,13 @@ int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int K, int Z
  * (start, end) into stamps [blocks][2]; ppo_probe_now writes the counter's current value */
 int ppo_probe_side_kernel(int blocks, int threads, long long ticks, long long* stamps, void* stream);
 int ppo_probe_now(long long* out, void* stream);
+/* timing anatomy of ppo_conv2_fwd_mask's image-resident kernel (wrong results by design): dbg bit 1
+ * skips the MFMAs, 2 the staging, 4 the global loads, 8 the epilogue stores */
+int ppo_probe_conv2_fwd_anatomy(int dbg, const float* a1, int B, const float* w2p, const float* b2, float* out,
+                                uint16_t* mbits, void* stream);
 /* timing anatomy of ppo_conv2_wgrad's image-resident kernel (wrong results by design): dbg bit 1 skips
- * the MFMAs, 2 the LDS staging, 4 the global loads */
+ * the MFMAs, 2 the LDS staging, 4 the global loads; 8 / 16 / 24 schedule experiments (right results:
+ * loads over all 12 slots / odd blocks started half an image late / both) */
 int ppo_probe_conv2_wgrad_anatomy(int dbg, const float* dz2, const float* a1, int B, int Z, float* slab,
                                   float* slab_bias, void* stream);
 long long ppo_a1s_bytes(int B);

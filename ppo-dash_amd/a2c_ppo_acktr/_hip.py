@@ -70,6 +70,7 @@ SIGNATURES = {
     # probe.hip (CU-contention diagnostics)
     "ppo_probe_side_kernel": [c_int, c_int, c_ll, c_p, c_p],
     "ppo_probe_now": [c_p, c_p],
+    "ppo_probe_conv2_fwd_anatomy": [c_int, c_p, c_int, c_p, c_p, c_p, c_p, c_p],
     "ppo_probe_conv2_wgrad_anatomy": [c_int, c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     # a1split.hip (conv1 output pre-split for conv2)
     "ppo_a1s_bytes": [c_int],
@@ -144,6 +145,8 @@ def lib():
                                "(or __graft_entry__.build()); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
         for name, args in SIGNATURES.items():
+            if name.startswith("ppo_probe_") and not hasattr(L, name):
+                continue   # diagnostics only: an older library (same-box A/B builds) may lack a probe
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPES.get(name, c_int)

@@ -714,7 +714,9 @@ struct Conv2Dgrad : C_ {
 //     registers one unit per k-step (1-4), each once its register has been staged.
 //   * Epilogue in the swapped MFMA orientation (weights as A): one 16-B store of
 //     four consecutive channels per tile, dummy rows dropped by buffer range.
-template <int NP, bool MASK = false>
+// DBG (timing anatomy only, ppo_probe_conv2_fwd_anatomy; wrong results): 1 skips
+// the MFMAs, 2 the staging (split + ds_write), 4 the global loads, 8 the epilogue stores
+template <int NP, bool MASK = false, int DBG = 0>
 __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restrict__ a1, int B,
                                                            const uint16_t* __restrict__ wpl,
                                                            const float* __restrict__ bias,
@@ -764,6 +766,10 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
   f32x4 stg[UPER][2];
   bf16x8 lo[UPER];
   auto fetch_unit = [&](int b, int j) {   // unconditional (the 4th unit of waves 1-7 reloads unit 1599)
+    if constexpr ((DBG & 4) != 0) {   // no load; the registers stay opaque to the compiler
+      asm volatile("" : "+v"(stg[j][0]), "+v"(stg[j][1]));
+      return;
+    }
     const f32x4* src = reinterpret_cast<const f32x4*>(a1 + (size_t)b * 12800);
     stg[j][0] = src[usrc[j]];
     stg[j][1] = src[usrc[j] + 1];
@@ -773,6 +779,10 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
     for (int j = 0; j < UPER; ++j) fetch_unit(b, j);
   };
   auto put_hm = [&](int j, int st) {   // hi / mid parts now, lo part held
+    if constexpr ((DBG & 2) != 0) {   // no staging; the loaded registers stay live
+      asm volatile("" ::"v"(stg[j][0]), "v"(stg[j][1]));
+      return;
+    }
     Frag3 f;
     split8(stg[j][0], stg[j][1], f, NP == 1);
     lo[j] = f.l;
@@ -783,6 +793,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
     }
   };
   auto put_l = [&](int j, int st) {
+    if constexpr ((DBG & 2) != 0) return;
     if constexpr (NP > 1)
       if (j < UPER - 1 || has_last) S[st * STG + 2 * PLN + udst[j]] = lo[j];
   };
@@ -833,7 +844,12 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
         }
 #define PPO_PART(X, Y) \
   _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(w.Y, a[u].X, acc[t0 + u]);
-        PPO_PRODUCTS(NP, PPO_PART)
+        if constexpr ((DBG & 1) == 0) {
+          PPO_PRODUCTS(NP, PPO_PART)
+        } else {   // keep the fragment reads live
+#pragma unroll
+          for (int u = 0; u < 3; ++u) asm volatile("" ::"v"(a[u].h), "v"(a[u].m), "v"(a[u].l));
+        }
 #undef PPO_PART
       }
       if (s < UPER) put_hm(s, cur ^ 1);
@@ -863,8 +879,8 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
         f32x4 y;
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
-        bstore_f32x4(y, rs, m >= 0 ? 4 * (m * 64 + 16 * nt + 4 * g) : -1);
-        if constexpr (MASK) {   // ReLU mask bits of pixel m, channels 16 nt .. +15: 4 lanes' nibbles
+        if constexpr ((DBG & 8) == 0) bstore_f32x4(y, rs, m >= 0 ? 4 * (m * 64 + 16 * nt + 4 * g) : -1);
+        if constexpr (MASK && (DBG & 8) == 0) {   // ReLU mask bits of pixel m, channels 16 nt .. +15: 4 lanes' nibbles
           int nib = 0;
 #pragma unroll
           for (int r = 0; r < 4; ++r) nib |= (y[r] > 0.f ? 1 : 0) << r;
@@ -2666,6 +2682,27 @@ PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, flo
   set_wgrad(p, dz2, 64, (long long)B * 81, Z, slab, slab_bias, 512);
   p.in = a1;
   return launch(p, 64, 512, Z, as_stream(stream), "conv2_wgrad", 2.0 * B * 81 * 64 * 512);
+}
+
+// timing anatomy of the conv2 forward (diagnostics, wrong results by design): dbg bits as
+// conv2_fwd_x9c_kernel's DBG (1 no MFMAs, 2 no staging, 4 no global loads, 8 no epilogue stores),
+// the mask-writing instantiation the training forward runs
+PPO_API int ppo_probe_conv2_fwd_anatomy(int dbg, const float* a1, int B, const float* w2p, const float* b2,
+                                        float* out, uint16_t* mbits, void* stream) {
+  PPO_REQUIRE(B > 0 && dbg >= 0 && dbg < 16, "ppo_probe_conv2_fwd_anatomy: B=%d dbg=%d", B, dbg);
+  const int n_cu = device_cus();
+  const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+  const uint16_t* wpl = planes_of(w2p, 64 * 512);
+  hipStream_t st = as_stream(stream);
+  switch (dbg) {
+#define PPO_C2FA(D) \
+  case D: conv2_fwd_x9c_kernel<6, true, D><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits); break;
+    PPO_C2FA(0) PPO_C2FA(1) PPO_C2FA(2) PPO_C2FA(3) PPO_C2FA(4) PPO_C2FA(5) PPO_C2FA(6) PPO_C2FA(7)
+    PPO_C2FA(8) PPO_C2FA(9) PPO_C2FA(10) PPO_C2FA(11) PPO_C2FA(12) PPO_C2FA(13) PPO_C2FA(14) PPO_C2FA(15)
+#undef PPO_C2FA
+  }
+  PPO_LAUNCH_CHECK("conv2_fwd_x9c_kernel (anatomy)");
+  return 0;
 }
 
 // timing anatomy of the conv2 weight gradient (diagnostics, wrong results by design): dbg bits as

@@ -160,6 +160,10 @@ def main():
                                             a2.data_ptr(), None, s), 2.0 * B * 81 * 64 * 512),
         "conv2_wgrad_split": (lambda: call("ppo_conv2_wgrad_split", dz2.data_ptr(), a1s.data_ptr(), B, z2c,
                                            slab.data_ptr(), slab_b.data_ptr(), s), 2.0 * B * 81 * 64 * 512),
+        # timing anatomy of the conv2 forward (wrong results): no MFMA / staging / loads / stores
+        **{f"conv2_fwd_anat{d}": ((lambda d=d: call("ppo_probe_conv2_fwd_anatomy", d, a1.data_ptr(), B, pk[0],
+                                                       b2.data_ptr(), a2.data_ptr(), m2.data_ptr(), s)),
+                                  2.0 * B * 81 * 64 * 512) for d in range(16)},
         # timing anatomy of the conv2 weight gradient (wrong results): no MFMA / no staging / no loads
         **{f"conv2_wgrad_anat{d}": ((lambda d=d: call("ppo_probe_conv2_wgrad_anatomy", d, dz2.data_ptr(),
                                                          a1.data_ptr(), B, z2c, slab.data_ptr(), slab_b.data_ptr(),
