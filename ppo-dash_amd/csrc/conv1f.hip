@@ -912,6 +912,9 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
 // holds (idx gather as ppo_conv1_fwd) — and on raw u8 RGB frames with the
 // NormalizeWrapper / FrameStackMono(2) decode fused (SRC_RGB); mbits (nullable):
 // the ReLU mask bits of the output as ppo_conv1_fwd_mask writes them
+int conv1_fwd_rgb_affine(const uint8_t* frames, const int64_t* idx, long long row0, int B, const float* mean,
+                         double stdv, const float* w1, const float* b1, float* out, uint32_t* mbits, void* stream);
+
 static int conv1_fwd_x6_launch(int src, const void* obs, const int64_t* idx, long long row0, int B, const float* mean,
                                double stdv, const float* w1, const float* b1, float* out, uint32_t* mbits,
                                void* stream) {
@@ -969,6 +972,9 @@ PPO_API int ppo_conv1_fwd_rgb(const uint8_t* frames, const int64_t* idx, long lo
   PPO_REQUIRE(B >= 0 && frames != nullptr && stdv != 0.0, "ppo_conv1_fwd_rgb: B=%d std=%g", B, stdv);
   PPO_REQUIRE(((uintptr_t)frames & 15) == 0 && (mean == nullptr || ((uintptr_t)mean & 15) == 0),
               "ppo_conv1_fwd_rgb: frames and mean must be 16-B aligned");
+  // the affine fold (rgbaff.hip) unless tuned off or the raw mode's truncated grey plane
+  if (ppo_tune_get("rgb_aff") != 0 && !(mean == nullptr && stdv == 1.0))
+    return conv1_fwd_rgb_affine(frames, idx, row0, B, mean, stdv, w1, b1, out, mbits, stream);
   return conv1_fwd_x6_launch(SRC_RGB, frames, idx, row0, B, mean, stdv, w1, b1, out, mbits, stream);
 }
 

@@ -26,6 +26,17 @@
 #include "igemm_x9.h"
 #include "small.h"
 
+// experiment (build_variants -DPPO_STAGGER=N): odd blocks of the persistent image
+// kernels start N x 64 clocks late, so the chip's per-image load bursts spread out
+#ifndef PPO_STAGGER
+#define PPO_STAGGER 0
+#endif
+#define PPO_START_STAGGER()                                                 \
+  do {                                                                      \
+    if constexpr (PPO_STAGGER > 0)                                          \
+      if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(PPO_STAGGER);            \
+  } while (0)
+
 namespace {
 // ---------------------------------------------------------------------------
 // Forward problems
@@ -219,6 +230,7 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
       }
     }
   };
+  PPO_START_STAGGER();
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
   if (b < B) {
@@ -804,6 +816,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
   int vrow[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) vrow[t] = vtab[t][i16] + g * U;
+  PPO_START_STAGGER();
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
   if (b < B) {
@@ -922,7 +935,7 @@ __device__ __forceinline__ int c2w_pix(int r) {
 // DBG (timing anatomy only, ppo_probe_conv2_wgrad_anatomy; wrong results): 1 skips
 // the MFMAs, 2 the LDS staging (split + ds_write), 4 the global loads; schedule
 // experiments (right results): 8 spreads the 8 load parts over all 12 slots, 16
-// starts the odd blocks half an image late (s_sleep)
+// starts every block at once (no s_sleep stagger of the odd blocks)
 template <int NP, int DBG = 0>
 __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __restrict__ dz2,
                                                             const float* __restrict__ a1, int B,
@@ -1021,8 +1034,10 @@ __global__ __launch_bounds__(512) void conv2_wgrad_x9_kernel(const float* __rest
     for (int mt = 0; mt < 4; ++mt) acc[j][mt] = zero4();
   const int Z = gridDim.x;
   int b = blockIdx.x;
-  if constexpr ((DBG & 16) != 0)
-    if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(100);
+  // the odd blocks start ~half an image late (s_sleep 100 = 6,400 clocks): every
+  // block issues its next image's loads at the same k-steps, and in lock step the
+  // whole chip's loads arrive as one burst per image (1.69 -> 1.61-1.63 ms, kbench)
+  if ((DBG & 16) == 0 && (blockIdx.x & 1)) __builtin_amdgcn_s_sleep(100);
   if (b < B) {
     fetch(b);
     put(true);
@@ -1193,6 +1208,7 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
     }
   };
   __syncthreads();   // the zeroed pads
+  PPO_START_STAGGER();
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
   if (b < B) {
@@ -1329,6 +1345,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
     }
   };
   __syncthreads();   // the zeroed pad rows
+  PPO_START_STAGGER();
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
   if (b < B) {
@@ -1679,6 +1696,7 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
       }
     }
   };
+  PPO_START_STAGGER();
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
   if (b < B) {
@@ -1964,10 +1982,10 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
 // ---------------------------------------------------------------------------
 enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_X9,
-       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_FC_DGRAD, TK_FC_WGRAD, TK_ORDER, TK_FC_SPLITK, TK_A1SPLIT, TK_N };
+       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_FC_DGRAD, TK_FC_WGRAD, TK_ORDER, TK_FC_SPLITK, TK_A1SPLIT, TK_RGB_AFF, TK_N };
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
                                          "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad", "fc_dgrad", "fc_wgrad",
-                                         "order", "fc_splitk", "a1split"};
+                                         "order", "fc_splitk", "a1split", "rgb_aff"};
 // x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
@@ -1979,7 +1997,7 @@ static int g_small_b = 4;
 // 3: the default order with the fc weight gradient's scalar epilogue, for A/B)
 // fc_splitk: K slices of the rollout-sized fc forward with a workspace (ppo_fc_fwd_ws; <= 1: unsplit)
 // a1split: conv1 writes its output pre-split for conv2 (a1split.hip; 1 on, 0 the fp32 a1 hand-off)
-static int g_tune[TK_N] = {0, 8, 8, 8, 8, 0, 12, 1, 8, 8, 0, 0, 0, 2, 0};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
+static int g_tune[TK_N] = {0, 8, 8, 8, 8, 0, 12, 1, 8, 8, 0, 0, 0, 2, 0, 1};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
 
 int heads_lds_knob(int set, int value);   // heads.hip (the LDS-weight heads_train kernel, default on)
 

@@ -67,7 +67,19 @@ def test_fused_decode_bit_exact(gpu, mode, src):
     conv1's output relu(±x) of single input elements; with exact unit weights the
     six split products sum back to x itself, so the decoded inputs are read back
     exactly: every element of the 80x80 tap window of all four channels (colour
-    planes and the transposed grey plane) equals the reference chain's bit for bit."""
+    planes and the transposed grey plane) equals the reference chain's bit for bit.
+    (The fused-decode kernel, rgb_aff 0; the affine fold, test_rgb_affine_*, forms
+    no per-element fl32 of the decode and is checked against float64 instead.)"""
+    H = _hip()
+    old_aff = H.call("ppo_tune_get", b"rgb_aff")
+    H.call("ppo_tune_set", b"rgb_aff", 0)
+    try:
+        _decode_readback(gpu, mode, src)
+    finally:
+        H.call("ppo_tune_set", b"rgb_aff", old_aff)
+
+
+def _decode_readback(gpu, mode, src):
     g = torch.Generator().manual_seed(11)
     N = 6
     frames = torch.randint(0, 256, (N, 84, 84, 3), dtype=torch.uint8, generator=g)
@@ -103,12 +115,64 @@ def test_fused_decode_bit_exact(gpu, mode, src):
     np.testing.assert_array_equal(got, ref[:, :, :80, :80])
 
 
-@pytest.mark.parametrize("src", ["f32", "rgb"])
+def test_rgb_affine_raw_mode_keeps_decode(gpu):
+    """The raw mode (no normaliser, s = 1) stores FrameStackMono's grey plane as
+    truncated u8 — not affine in the bytes — so with the affine fold on it must
+    still take the fused decode: the bit-exact read-back holds."""
+    H = _hip()
+    old_aff = H.call("ppo_tune_get", b"rgb_aff")
+    H.call("ppo_tune_set", b"rgb_aff", 1)
+    try:
+        _decode_readback(gpu, "raw", "rgb")
+    finally:
+        H.call("ppo_tune_set", b"rgb_aff", old_aff)
+
+
+@pytest.mark.parametrize("mode", ["norm", "div255"])
+def test_rgb_affine_vs_float64(gpu, mode):
+    """The affine fold (rgbaff.hip) in both affine modes, whole frames (idx None),
+    B = 5 < the grid, extreme frames (all 0, all 255) included: forward + ReLU vs
+    torch float64 of the reference chain's decoded input at 1e-5 of max|ref|."""
+    H = _hip()
+    g = torch.Generator().manual_seed(23)
+    B = 5
+    frames = torch.randint(0, 256, (B, 84, 84, 3), dtype=torch.uint8, generator=g)
+    frames[0] = 0
+    frames[1] = 255
+    dec, mean, std = _decoded(frames.numpy(), mode)
+    w = torch.randn(32, 4, 8, 8, generator=g) * 0.05
+    b = torch.randn(32, generator=g) * 0.1
+    mean_d = None if mean is None else torch.from_numpy(mean.astype(np.float32)).cuda()
+    old_aff = H.call("ppo_tune_get", b"rgb_aff")
+    H.call("ppo_tune_set", b"rgb_aff", 1)
+    try:
+        out = _fwd("rgb", frames.cuda(), None, B, w.cuda(), b.cuda(), None, mean_d, std)
+        torch.cuda.synchronize()
+    finally:
+        H.call("ppo_tune_set", b"rgb_aff", old_aff)
+    ref = torch.relu(torch.nn.functional.conv2d(torch.from_numpy(dec).double(), w.double(), b.double(),
+                                                stride=4)).permute(0, 2, 3, 1)
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("src", ["f32", "rgb", "rgb_decode"])
 @pytest.mark.parametrize("products", [6, 9, 1])
 def test_conv1_fwd_vs_float64(gpu, src, products):
     """forward + bias + ReLU and the ReLU mask bits, rows gathered out of order,
     B = 300 > the persistent grid (blocks walk several images): 1e-5 of max|ref|
-    (products 6 / 9: fp32 accuracy), bf16 operand rounding (1: half-precision mode)."""
+    (products 6 / 9: fp32 accuracy), bf16 operand rounding (1: half-precision mode).
+    rgb: the affine fold (rgbaff.hip, default); rgb_decode: the fused decode."""
+    H = _hip()
+    old_aff = H.call("ppo_tune_get", b"rgb_aff")
+    H.call("ppo_tune_set", b"rgb_aff", 0 if src == "rgb_decode" else 1)
+    try:
+        _fwd_vs_float64(gpu, "rgb" if src == "rgb_decode" else src, products)
+    finally:
+        H.call("ppo_tune_set", b"rgb_aff", old_aff)
+
+
+def _fwd_vs_float64(gpu, src, products):
     H = _hip()
     g = torch.Generator().manual_seed(5 + products)
     B, rows = 300, 420
