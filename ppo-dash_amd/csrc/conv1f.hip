@@ -915,6 +915,9 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
 int conv1_fwd_rgb_affine(const uint8_t* frames, const int64_t* idx, long long row0, int B, const float* mean,
                          double stdv, const float* w1, const float* b1, float* out, uint32_t* mbits, void* stream);
 
+int conv1_wgrad_rgb_affine(const float* dz1, const uint8_t* frames, const int64_t* idx, long long row0, int B,
+                           const float* mean, double stdv, int Z, float* slab, float* slab_bias, void* stream);
+
 static int conv1_fwd_x6_launch(int src, const void* obs, const int64_t* idx, long long row0, int B, const float* mean,
                                double stdv, const float* w1, const float* b1, float* out, uint32_t* mbits,
                                void* stream) {
@@ -1024,6 +1027,8 @@ PPO_API int ppo_conv1_wgrad_rgb(const float* dz1, const uint8_t* frames, const i
   PPO_REQUIRE(B >= 0 && frames != nullptr && stdv != 0.0, "ppo_conv1_wgrad_rgb: B=%d std=%g", B, stdv);
   PPO_REQUIRE(((uintptr_t)frames & 15) == 0 && (mean == nullptr || ((uintptr_t)mean & 15) == 0),
               "ppo_conv1_wgrad_rgb: frames and mean must be 16-B aligned");
+  if (ppo_tune_get("rgb_aff") != 0 && !(mean == nullptr && stdv == 1.0))
+    return conv1_wgrad_rgb_affine(dz1, frames, idx, row0, B, mean, stdv, Z, slab, slab_bias, stream);
   return conv1_wgrad_x6_launch(SRC_RGB, dz1, frames, idx, row0, B, mean, stdv, Z, slab, slab_bias, stream);
 }
 

@@ -36,7 +36,7 @@
 // 8-B LDS reads), as in the u8 kernel.
 #include <mutex>
 
-#include "igemm.h"
+#include "igemm_x9.h"
 
 namespace {
 
@@ -211,12 +211,292 @@ __global__ __launch_bounds__(512) void conv1_fwd_rgbaff_kernel(const uint8_t* __
   }
 }
 
+// ---------------------------------------------------------------------------
+// Weight gradient by the same fold.  With X_c = rs (u_c - m_c):
+//   dW[co][c][ky][kx] = rs (G[co][c][ky][kx] - Gm[...])                 c < 3
+//   dW[co][3][ky][kx] = rs Σ_c k_c (GT[co][c][kx][ky] - GmT[...])
+//   G  = Σ_(b,p) dz[b][p][co] u_c[4oy+ky][4ox+kx],  GT the same at the transposed
+//   origin (4ox + r, 4oy + q);  Gm / GmT the same sums over the means with
+//   D[co][p] = Σ_b dz[b][p][co] in place of dz (the means do not depend on b).
+// G and GT are two passes of the u8 k-split kernel (conv1w.hip kw2: the raw frame
+// by LDS-DMA, phase rows converted once per image, two E stages, dz straight from
+// HBM and split in registers) over the three colour planes of the frame (TRANS:
+// of its transpose, u^T[y][x] = u[x][y]) — 6 column tiles of 32 instead of 8;
+// the direct pass also sums D per block (its dz values are in registers anyway)
+// into a [Z][32][400] scratch.  Each pass writes its columns of the block's slab
+// already scaled by rs (direct: n < 192; TRANS: the grey channel's 64 columns,
+// summed over c with k_c and transposed) and the direct pass the bias partials;
+// rgbaff_wfinal subtracts the means' share from slab 0.  Slab format and bias as
+// every conv1 wgrad (the engine's ppo_wgrad_reduce sums the Z slabs, scale 1).
+__device__ __forceinline__ void glds16_ra(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+template <bool TRANS>
+__global__ __launch_bounds__(512) void conv1_wgrad_rgbaff_kernel(const float* __restrict__ dz1,
+                                                                 const uint8_t* __restrict__ frames,
+                                                                 const int64_t* __restrict__ idx, long long row0,
+                                                                 int B, float rs, float* __restrict__ slab,
+                                                                 float* __restrict__ slab_bias,
+                                                                 float* __restrict__ dsum) {
+  constexpr int NW = 8, C = 3, IMG = RA_IMG, NTL = 2 * C;   // 6 column tiles of 32
+  constexpr int XW = 24, ROWE = 4 * XW, EST = C * IMG * ROWE;  // 24,192 elements per stage
+  constexpr int NITEM = IMG * 6, NPC = 21, RAWB = NPC * 1024;  // items (y, 16-x group); raw pieces
+  __shared__ __attribute__((aligned(16))) uint16_t E[2 * EST + RAWB / 2];   // 118,272 B
+  uint8_t* const RAW = reinterpret_cast<uint8_t*>(E + 2 * EST);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int G = gridDim.x;
+  const int kx = l32 & 7, dxl = kx & 3, sh = 2 * (kx >> 2);
+  const int lbase = ((l32 >> 3) * 4 + dxl) * XW;
+  const uint32_t raw_lds = (uint32_t)reinterpret_cast<uintptr_t>(RAW);
+  auto dma_raw = [&](int b) {   // pieces wave + 8 i (i < 3), clamped: harmless duplicates / tail
+    const uint8_t* img = frames + obs_row(idx, row0, b) * (long long)RA_FB;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int pc = min(wave + 8 * i, NPC - 1);
+      const int off = min(pc * 1024 + lane * 16, RA_FB - 16);
+      glds16_ra(img + off, __builtin_amdgcn_readfirstlane(raw_lds + pc * 1024));
+    }
+  };
+  // RAW (HWC bytes) -> E[st][c][y][dx][X] = plane value at (y, 4X + dx), bf16 (exact);
+  // the plane is u_c (direct) or u_c^T (TRANS); x >= 84 (never read) clamped
+  auto put = [&](int st) {
+    uint16_t* S = E + st * EST;
+    if (tid >= NITEM) return;
+    const int y = tid / 6, g6 = tid - 6 * y;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      float f[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int x = min(16 * g6 + j, IMG - 1);
+        const int byte = TRANS ? (x * IMG + y) * 3 + c : (y * IMG + x) * 3 + c;
+        f[j] = (float)RAW[byte];
+      }
+      uint16_t* dp = S + (c * IMG + y) * ROWE + 4 * g6;
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) {   // X = 4 g6 + jj: x = 16 g6 + 4 jj + dx
+        const uint2 q = {__builtin_amdgcn_perm(__float_as_uint(f[4 + dx]), __float_as_uint(f[dx]), 0x07060302u),
+                         __builtin_amdgcn_perm(__float_as_uint(f[12 + dx]), __float_as_uint(f[8 + dx]), 0x07060302u)};
+        *reinterpret_cast<uint2*>(dp + dx * XW) = q;
+      }
+    }
+  };
+  f32x16 acc[NTL];
+#pragma unroll
+  for (int t = 0; t < NTL; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bacc = 0.f;
+  float dacc[4][8];   // !TRANS: D sums of this lane's pixels per k-step slot (A, B, C, D)
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dacc[q][j] = 0.f;
+  auto dz_load = [&](int b, int s, float (&d)[8]) {
+    const auto rsc = make_rsrc(dz1 + (size_t)b * 12800, 12800 * 4);
+    const int o = ((16 * s + 8 * h) * 32 + l32) * 4;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsc, o + 128 * j, 0, 0));
+  };
+  auto bfrag = [&](const uint16_t* S, int tt, int q0off, int q1off) {
+    const int toff = ((tt >> 1) * IMG + 4 * (tt & 1)) * ROWE + lbase;
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint16_t* p = S + toff + (k ? q1off : q0off);
+      const uint2 d01 = *reinterpret_cast<const uint2*>(p);
+      const uint32_t d2 = *reinterpret_cast<const uint32_t*>(p + 4);
+      o[2 * k] = __builtin_amdgcn_alignbyte(d01.y, d01.x, sh);
+      o[2 * k + 1] = __builtin_amdgcn_alignbyte(d2, d01.y, sh);
+    }
+    return __builtin_bit_cast(bf16x8, uint4{o[0], o[1], o[2], o[3]});
+  };
+  auto qoff = [&](int q) { const int oy = q / 5; return 4 * oy * ROWE + 4 * (q - 5 * oy); };
+  auto kstep = [&](const uint16_t* S, int s, const float (&d)[8], int t0, int t1) {
+    Frag3 a;
+    split8(f32x4{d[0], d[1], d[2], d[3]}, f32x4{d[4], d[5], d[6], d[7]}, a, false);
+    const int q0 = 4 * s + 2 * h, o0 = qoff(q0), o1 = qoff(q0 + 1);
+#pragma unroll
+    for (int tt = 0; tt < NTL; ++tt) {
+      if (tt < t0 || tt >= t1) continue;
+      const bf16x8 bq = bfrag(S, tt, o0, o1);
+      acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, bq, acc[tt], 0, 0, 0);
+      acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, bq, acc[tt], 0, 0, 0);
+      acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, bq, acc[tt], 0, 0, 0);
+    }
+  };
+  auto add8 = [&](const float (&d)[8], int slot) {
+    if constexpr (!TRANS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bacc += d[j];
+        dacc[slot][j] += d[j];
+      }
+    }
+  };
+  int b = blockIdx.x, cur = 0;
+  float dA[8], dB[8], dC[8], dD[8];
+  if (b < B) {
+    dma_raw(b);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    put(0);
+    __syncthreads();   // raw consumed, E[0] complete
+    dz_load(b, wave, dA);
+    dz_load(b, wave + 8, dB);
+    if (b + G < B) dma_raw(b + G);
+  }
+  for (; b < B; b += G) {
+    const uint16_t* S = E + cur * EST;
+    const bool nxt = b + G < B;
+    dz_load(b, wave + 16, dC);
+    kstep(S, wave, dA, 0, NTL);
+    add8(dA, 0);
+    dz_load(b, 24, dD);
+    kstep(S, wave + 8, dB, 0, NTL);
+    add8(dB, 1);
+    if (nxt) {
+      // raw(b + G) is older than dB's loads, which k-step B waited for; the explicit wait
+      // (dC, dD may stay in flight) makes the order independent of the compiler's waits
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      lds_barrier();   // Y: every wave's pieces of raw(b + G) are in LDS
+      put(cur ^ 1);
+      lds_barrier();   // Z: raw consumed, E[cur ^ 1] complete
+      dz_load(b + G, wave, dA);
+      dz_load(b + G, wave + 8, dB);
+      if (b + 2 * G < B) dma_raw(b + 2 * G);
+    }
+    kstep(S, wave + 16, dC, 0, NTL);
+    add8(dC, 2);
+    kstep(S, 24, dD, wave, wave + 1);     // k-step 24: tile `wave` (waves 6, 7: none; D and bias: wave 0)
+    if (wave == 0) add8(dD, 3);
+    cur ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // D partial: lane (l32, h) of wave w, slot q: pixels 16 s_q + 8 h + j of channel l32
+  if constexpr (!TRANS) {
+    float* dp = dsum + (size_t)blockIdx.x * (32 * 400) + l32 * 400;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q == 3 && wave != 0) continue;
+      const int s = q == 0 ? wave : q == 1 ? wave + 8 : q == 2 ? wave + 16 : 24;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dp[16 * s + 8 * h + j] = dacc[q][j];
+    }
+  }
+  // fixed-order sum of the eight waves' partials (as kw2), three tiles at a time
+  float* X = reinterpret_cast<float*>(E);
+#pragma unroll
+  for (int half = 4; half >= 1; half >>= 1)
+#pragma unroll
+    for (int t0 = 0; t0 < NTL; t0 += 3) {
+      if (wave >= half && wave < 2 * half) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) X[(((wave - half) * 3 + t) * 16 + r) * 64 + lane] = acc[t0 + t][r];
+      }
+      __syncthreads();
+      if (wave < half) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[t0 + t][r] += X[((wave * 3 + t) * 16 + r) * 64 + lane];
+      }
+      __syncthreads();
+    }
+  float* out = slab + (size_t)blockIdx.x * 32 * 256;
+  if (wave == 0) {
+    if constexpr (!TRANS) {   // columns n = 32 t + l32 = 64 c + 8 ky + kx, c < 3
+#pragma unroll
+      for (int t = 0; t < NTL; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+          out[co * 256 + 32 * t + l32] = rs * acc[t][r];
+        }
+    } else {   // the grey channel: column (ky', kx') of tile 2c + hh reads u_c[4ox + kx'][4oy + ky'],
+      // the patch of W_3[ky'][kx'] (r = kx', q = ky'): dW3 column 192 + 8 ky' + kx' = 192 + 32 hh + l32
+      const float kg[3] = {0.299f, 0.587f, 0.114f};
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float v = kg[0] * acc[hh][r] + kg[1] * acc[2 + hh][r] + kg[2] * acc[4 + hh][r];
+          out[co * 256 + 192 + 32 * hh + l32] = rs * v;
+        }
+    }
+  }
+  if constexpr (!TRANS) {
+    X[tid] = bacc;
+    __syncthreads();
+    if (tid < 32) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += X[w * 64 + tid] + X[w * 64 + 32 + tid];
+      slab_bias[(size_t)blockIdx.x * 32 + tid] = t;
+    }
+  }
+}
+
+// slab 0 -= rs (Gm, Σ_c k_c GmT transposed): the means' share, D = Σ_z dsum[z]
+__global__ __launch_bounds__(512) void rgbaff_wfinal_kernel(const float* __restrict__ dsum, int Z,
+                                                            const float* __restrict__ mean, double rs,
+                                                            float* __restrict__ slab) {
+  const int co = blockIdx.x, tid = threadIdx.x;
+  __shared__ float Dl[400];
+  __shared__ double Gm[RA_K];
+  if (tid < 400) {
+    float t = 0.f;
+    for (int z = 0; z < Z; ++z) t += dsum[((size_t)z * 32 + co) * 400 + tid];
+    Dl[tid] = t;
+  }
+  __syncthreads();
+  if (tid < RA_K) {
+    double acc = 0.0;
+    for (int p = 0; p < 400; ++p) {
+      const int oy = p / 20, ox = p - 20 * oy;
+      int y, x, c;
+      if (tid < 192) {
+        c = tid >> 6;
+        y = 4 * oy + ((tid >> 3) & 7);
+        x = 4 * ox + (tid & 7);
+      } else {
+        const int kk = tid - 192;
+        c = kk >> 6;
+        y = 4 * ox + ((kk >> 3) & 7);
+        x = 4 * oy + (kk & 7);
+      }
+      acc += (double)Dl[p] * (double)mean[(y * RA_IMG + x) * 3 + c];
+    }
+    Gm[tid] = acc;
+  }
+  __syncthreads();
+  float* out = slab + co * 256;
+  if (tid < 192) {
+    out[tid] -= (float)(rs * Gm[tid]);
+  } else if (tid < 256) {   // column 192 + 8 ky + kx <- GmT[c][r = kx][q = ky]
+    const int n = tid - 192, ky = n >> 3, kx = n & 7;
+    const double v = 0.299f * Gm[192 + 8 * kx + ky] + 0.587f * Gm[256 + 8 * kx + ky] + 0.114f * Gm[320 + 8 * kx + ky];
+    out[tid] -= (float)(rs * v);
+  }
+}
+
 // Weff / Mb workspace per (device, stream): launches in flight on different
 // streams never share it.  Grow-only list; the buffers live for the process.
 struct AffWs {
   int dev;
   hipStream_t stream;
   float* buf;
+  float* dsum;   // [zcap][32][400] (the weight gradient's per-block D sums)
+  int zcap;
 };
 static std::mutex g_aff_mu;
 static AffWs g_aff[64];
@@ -231,8 +511,32 @@ static float* aff_ws(hipStream_t st) {
   if (g_naff == 64) return nullptr;
   float* p = nullptr;
   if (hipMalloc(&p, (size_t)(32 * RA_K + 400 * 32) * sizeof(float)) != hipSuccess) return nullptr;
-  g_aff[g_naff++] = AffWs{dev, st, p};
+  g_aff[g_naff++] = AffWs{dev, st, p, nullptr, 0};
   return p;
+}
+
+static float* aff_dsum(hipStream_t st, int Z) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (!aff_ws(st)) return nullptr;
+  std::lock_guard<std::mutex> lk(g_aff_mu);
+  for (int i = 0; i < g_naff; ++i)
+    if (g_aff[i].dev == dev && g_aff[i].stream == st) {
+      AffWs& w = g_aff[i];
+      if (Z > w.zcap) {
+        if (w.dsum) {
+          if (hipStreamSynchronize(st) != hipSuccess) return nullptr;   // its launches are done
+          (void)hipFree(w.dsum);
+        }
+        const int cap = Z > 512 ? Z : 512;
+        w.dsum = nullptr;
+        w.zcap = 0;
+        if (hipMalloc(&w.dsum, (size_t)cap * 32 * 400 * sizeof(float)) != hipSuccess) return nullptr;
+        w.zcap = cap;
+      }
+      return w.dsum;
+    }
+  return nullptr;
 }
 
 }  // namespace
@@ -271,5 +575,27 @@ int conv1_fwd_rgb_affine(const uint8_t* frames, const int64_t* idx, long long ro
   }
   if (prof) ppo_prof_end(slot, st, 2.0 * B * 400 * 32 * 256);
   PPO_LAUNCH_CHECK("conv1_fwd_rgbaff_kernel");
+  return 0;
+}
+
+// the affine-folded weight gradient (called by ppo_conv1_wgrad_rgb under the same
+// conditions as the forward): slab [Z][32][256] (rs-scaled) and bias partials [Z][32]
+int conv1_wgrad_rgb_affine(const float* dz1, const uint8_t* frames, const int64_t* idx, long long row0, int B,
+                           const float* mean, double stdv, int Z, float* slab, float* slab_bias, void* stream) {
+  if (B <= 0 || Z <= 0) return 0;
+  hipStream_t st = as_stream(stream);
+  float* dsum = aff_dsum(st, Z);
+  if (!dsum) {
+    ppo_set_error("ppo_conv1_wgrad_rgb: workspace allocation failed");
+    return PPO_EARG;
+  }
+  const double rs = 1.0 / stdv;
+  int slot;
+  const bool prof = ppo_prof_begin("conv1_wgrad_rgb", st, &slot);
+  conv1_wgrad_rgbaff_kernel<false><<<Z, 512, 0, st>>>(dz1, frames, idx, row0, B, (float)rs, slab, slab_bias, dsum);
+  conv1_wgrad_rgbaff_kernel<true><<<Z, 512, 0, st>>>(dz1, frames, idx, row0, B, (float)rs, slab, slab_bias, dsum);
+  if (mean) rgbaff_wfinal_kernel<<<32, 512, 0, st>>>(dsum, Z, mean, rs, slab);
+  if (prof) ppo_prof_end(slot, st, 2.0 * B * 400 * 32 * 256);
+  PPO_LAUNCH_CHECK("conv1_wgrad_rgbaff_kernel");
   return 0;
 }

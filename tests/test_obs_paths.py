@@ -207,14 +207,26 @@ def _fwd_vs_float64(gpu, src, products):
     assert np.array_equal(got_bits, want)
 
 
-@pytest.mark.parametrize("src", ["f32", "rgb"])
+@pytest.mark.parametrize("src", ["f32", "rgb", "rgb_decode", "rgb_few"])
 @pytest.mark.parametrize("products", [6, 9])
 def test_conv1_wgrad_vs_float64(gpu, src, products):
     """weight + bias gradient, rows gathered out of order, B = 300 over a Z that
-    leaves blocks with one and with two images: 1e-5 of max|ref|."""
+    leaves blocks with one and with two images: 1e-5 of max|ref|.  rgb: the affine
+    fold (two passes + the means' share, rgbaff.hip), rgb_few: the same with B = 100
+    < Z (blocks without images), rgb_decode: the fused-decode kernel."""
+    H = _hip()
+    old_aff = H.call("ppo_tune_get", b"rgb_aff")
+    H.call("ppo_tune_set", b"rgb_aff", 0 if src == "rgb_decode" else 1)
+    try:
+        _wgrad_vs_float64(gpu, "f32" if src == "f32" else "rgb", products, 100 if src == "rgb_few" else 300)
+    finally:
+        H.call("ppo_tune_set", b"rgb_aff", old_aff)
+
+
+def _wgrad_vs_float64(gpu, src, products, B):
     H = _hip()
     g = torch.Generator().manual_seed(17 + products)
-    B, rows = 300, 420
+    rows = 420
     idx = torch.randperm(rows, generator=g)[:B].contiguous()
     dz1 = torch.randn(B, 20, 20, 32, generator=g)
     if src == "f32":

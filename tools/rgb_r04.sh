@@ -4,7 +4,8 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_obs_paths.py tests/test_full_size.py -x -v --timeout 120 --timeout-method thread -k "rgb or fused or obs_paths or float_obs" > gpurun_out/r04_rgb_t.log 2>&1
-rc=$?; grep -cE "PASSED" gpurun_out/r04_rgb_t.log; grep -E "FAILED|Error|assert" gpurun_out/r04_rgb_t.log | head -10; tail -2 gpurun_out/r04_rgb_t.log; [ $rc -eq 0 ] || exit $rc
-TAG=r04_rgb KERNELS=conv1_fwd_rgb,conv1_fwd_mask TESTK=none bash tools/ab_conv.sh || exit 1
-TAG=r04_rgb LINES="rgb" bash tools/lines_r04.sh
+T="${TAG:-r04_rgb}"
+timeout -k 10 400 python -u -m pytest tests/test_obs_paths.py tests/test_full_size.py -x -v --timeout 120 --timeout-method thread -k "rgb or fused or obs_paths or float_obs" > gpurun_out/${T}_t.log 2>&1
+rc=$?; grep -cE "PASSED" gpurun_out/${T}_t.log; grep -E "FAILED|Error|assert" gpurun_out/${T}_t.log | head -10; tail -2 gpurun_out/${T}_t.log; [ $rc -eq 0 ] || exit $rc
+TAG=$T KERNELS=${KERNELS:-conv1_fwd_rgb,conv1_wgrad_rgb} TESTK=none bash tools/ab_conv.sh || exit 1
+TAG=$T LINES="rgb" bash tools/lines_r04.sh
