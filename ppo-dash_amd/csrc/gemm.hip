@@ -26,17 +26,6 @@
 #include "igemm_x9.h"
 #include "small.h"
 
-// experiment (build_variants -DPPO_STAGGER=N): odd blocks of the persistent image
-// kernels start N x 64 clocks late, so the chip's per-image load bursts spread out
-#ifndef PPO_STAGGER
-#define PPO_STAGGER 0
-#endif
-#define PPO_START_STAGGER()                                                 \
-  do {                                                                      \
-    if constexpr (PPO_STAGGER > 0)                                          \
-      if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(PPO_STAGGER);            \
-  } while (0)
-
 namespace {
 // ---------------------------------------------------------------------------
 // Forward problems
@@ -230,7 +219,6 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
       }
     }
   };
-  PPO_START_STAGGER();
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
   if (b < B) {
@@ -816,7 +804,6 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
   int vrow[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) vrow[t] = vtab[t][i16] + g * U;
-  PPO_START_STAGGER();
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
   if (b < B) {
@@ -1208,7 +1195,6 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
     }
   };
   __syncthreads();   // the zeroed pads
-  PPO_START_STAGGER();
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
   if (b < B) {
@@ -1345,7 +1331,6 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
     }
   };
   __syncthreads();   // the zeroed pad rows
-  PPO_START_STAGGER();
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
   if (b < B) {
@@ -1696,7 +1681,6 @@ __global__ __launch_bounds__(512) void conv2_dgrad_x9_kernel(const float* __rest
       }
     }
   };
-  PPO_START_STAGGER();
   const int G = gridDim.x;
   int b = blockIdx.x, cur = 0;
   if (b < B) {
