@@ -135,7 +135,12 @@ int ppo_conv1_fwd_mask(const void* obs, int obs_is_u8, const int64_t* idx, long 
  *         transposed grey plane; mean fp32 [84][84][3] (NULL: 0; then std 255
  *         gives u/255, std 1 the raw values — raw mode, where the frame is still
  *         u8 inside FrameStackMono and its grey plane is stored truncated to u8).  Weight gradients: split-K slab
- *         [Z][32][256] + bias partials [Z][32] (reduce with scale 1). */
+ *         [Z][32][256] + bias partials [Z][32] (reduce with scale 1).
+ *         Default (ppo_tune_set("rgb_aff", 1), every mode but raw): the affine fold
+ *         (rgbaff.hip) — conv1 of the decoded input as rs * (exact u8 MFMA sums over
+ *         the colour planes at the direct and the transposed patch origin, grey
+ *         weights folded in) + the means' per-pixel bias map; fp32-accurate but not
+ *         bit-identical to the decode chain.  rgb_aff 0: the bit-exact fused decode. */
 int ppo_conv1_fwd_f32(const float* obs, const int64_t* idx, long long row0, int B, const float* w1, const float* b1,
                       float* out, uint32_t* mbits, void* stream);
 int ppo_conv1_fwd_rgb(const uint8_t* frames, const int64_t* idx, long long row0, int B, const float* mean, double stdv,
@@ -217,7 +222,7 @@ int ppo_probe_conv2_fwd_anatomy(int dbg, const float* a1, int B, const float* w2
                                 uint16_t* mbits, void* stream);
 /* timing anatomy of ppo_conv2_wgrad's image-resident kernel (wrong results by design): dbg bit 1 skips
  * the MFMAs, 2 the LDS staging, 4 the global loads; 8 / 16 / 24 schedule experiments (right results:
- * loads over all 12 slots / odd blocks started half an image late / both) */
+ * loads over all 12 slots / no start stagger of the odd blocks / both) */
 int ppo_probe_conv2_wgrad_anatomy(int dbg, const float* dz2, const float* a1, int B, int Z, float* slab,
                                   float* slab_bias, void* stream);
 long long ppo_a1s_bytes(int B);
