@@ -19,7 +19,10 @@
 namespace {
 
 constexpr int GAE_THREADS = 256;
-constexpr int GAE_U = 8;  // time steps prefetched per chunk
+#ifndef PPO_GAE_U
+#define PPO_GAE_U 16
+#endif
+constexpr int GAE_U = PPO_GAE_U;  // time steps prefetched per chunk (16: 4.86 vs 4.75 TB/s for 8 on 1M lanes, tools/gae_ab.sh)
 
 // Advantage moments as (count, mean, M2) (the reference's
 // advantages.mean() / .std(), T/a2c_ppo_acktr/algo/ppo.py:35-37): each thread
