@@ -1432,25 +1432,30 @@ __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __rest
   f32x4 xs[XPER][2];
   float ds[7];
   float bsum = 0.f;   // bias partial of co = tid & 31 (threads < 256: slots of row oy = tid >> 5)
-  auto fetch = [&](int b) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(a2 + (size_t)b * 5184);
+  // the next image's loads in two parts (a2 units; dz3 slots), issued inside the
+  // MFMA stream of k-step 0 (as conv2's weight gradient), through per-image buffer
+  // resources: lanes past the units / the 7 dz rows read out of range (0), no branch
+  static_assert(XPER == 1, "one a2 unit per thread");
+  auto fetch_part = [&](int b, int part) {
+    if (part == 0) {
+      const auto ra = make_rsrc(a2 + (size_t)b * 5184, 5184 * 4);
+      const int off = tid < XU ? 32 * tid : 0x7fffffe0;
+      xs[0][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+      xs[0][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
+    } else {
+      const auto rd = make_rsrc(dz3 + (size_t)b * 1568, 1568 * 4);
+      const bool on = tid < DU && (tid >> 5) < 7;
+      const int o = ((tid >> 5) * 7 * 32 + (tid & 31)) * 4;
 #pragma unroll
-    for (int j = 0; j < XPER; ++j) {
-      const int u = tid + NT * j;
-      if (u < XU) { xs[j][0] = src[2 * u]; xs[j][1] = src[2 * u + 1]; }
-    }
-    if (tid < DU) {
-      const float* d = dz3 + (size_t)b * 1568 + (tid >> 5) * 7 * 32 + (tid & 31);
-      if ((tid >> 5) < 7) {
-#pragma unroll
-        for (int e = 0; e < 7; ++e) ds[e] = d[e * 32];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 7; ++e) ds[e] = 0.f;
-      }
+      for (int e = 0; e < 7; ++e)
+        ds[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rd, on ? o + 128 * e : 0x7ffffff0, 0, 0));
     }
   };
-  auto put = [&](int buf) {
+  auto fetch = [&](int b) {
+    fetch_part(b, 0);
+    fetch_part(b, 1);
+  };
+  auto put = [&](int buf, bool count) {   // count: add the dz to the bias partial
 #pragma unroll
     for (int j = 0; j < XPER; ++j) {
       const int u = tid + NT * j;
@@ -1468,7 +1473,7 @@ __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __rest
       Frag3 f;
       split8(f32x4{ds[0], ds[1], ds[2], ds[3]}, f32x4{ds[4], ds[5], ds[6], 0.f}, f, false);
 #pragma unroll
-      for (int e = 0; e < 7; ++e) bsum += ds[e];
+      for (int e = 0; e < 7; ++e) bsum += count ? ds[e] : 0.f;
       const int off = (tid & 31) * DR + 8 * (tid >> 5);
       *reinterpret_cast<bf16x8*>(&D[buf][off]) = f.h;
       *reinterpret_cast<bf16x8*>(&D[buf][DPL + off]) = f.m;
@@ -1482,14 +1487,17 @@ __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __rest
   int b = blockIdx.x, cur = 0;
   if (b < B) {
     fetch(b);
-    put(0);
-    if (b + Z < B) fetch(b + Z);
+    put(0, true);
+    fetch(b + Z < B ? b + Z : b);
   }
   __syncthreads();
   typedef short s16x4 __attribute__((ext_vector_type(4)));
   for (; b < B; b += Z) {
-    if (b + Z < B) put(cur ^ 1);
-    if (b + 2 * Z < B) fetch(b + 2 * Z);
+    // every load in flight is this stage's (no stores in the loop): one explicit
+    // wait, then the stage write unconditionally (past the end: not counted)
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+    put(cur ^ 1, b + Z < B);
+    const int bnn = b + 2 * Z < B ? b + 2 * Z : b;
     const uint16_t* Xc = X[cur];
     const uint16_t* Dc = D[cur];
 #pragma unroll
@@ -1523,6 +1531,10 @@ __global__ __launch_bounds__(768) void conv3_wgrad_x9_kernel(const float* __rest
   _Pragma("unroll") for (int mt = 0; mt < 2; ++mt) acc[j][mt] = mma(a[mt].XX, bf.YY, acc[j][mt]);
         PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
+        if (s == 0 && j < 2) {
+          fetch_part(bnn, j);
+          __builtin_amdgcn_sched_barrier(0);   // the loads stay in their slot
+        }
       }
     }
     __syncthreads();   // stage cur consumed; stage cur ^ 1 complete
