@@ -164,8 +164,8 @@ def parse():
                    help="kernels event-timed inside the timed region; the one with the most time is the roofline kernel")
     p.add_argument("--no-profile-pass", action="store_true",
                    help="skip the profiled iteration after the timed region (per-kernel breakdown)")
-    p.add_argument("--gru-persist", type=int, default=1, choices=(0, 1, 2, 3),
-                   help="recurrent: persistent whole-sequence GRU launches, bit 0 forward, bit 1 backward (1) or per-step launches (0)")
+    p.add_argument("--gru-persist", type=int, default=3, choices=(0, 1, 2, 3),
+                   help="recurrent: persistent whole-sequence GRU launches, bit 0 forward, bit 1 backward (3) or per-step launches (0)")
     p.add_argument("--products", type=int, default=6, choices=(6, 9),
                    help="part products per fp32 product in the split-bf16 GEMMs (9 = every product exact)")
     p.add_argument("--half-precision", action="store_true",

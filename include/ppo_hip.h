@@ -294,7 +294,8 @@ int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* idx, con
 /* ppo_gru_seq_fwd runs as ONE persistent launch when ceil(n/32)·H/16 blocks fit
  * one per CU (H in {64,128,256,512}, variant 0): row groups hand h(t) over with
  * write-through stores and relaxed agent-scope counters, every wait bounded;
- * bit-identical to the step launches.  persist 0 forces the step launches.
+ * bit-identical to the step launches.  ppo_gru_seq_bwd likewise (persist bit 1).
+ * persist: bit 0 forward, bit 1 backward (default 3); 0 forces the step launches.
  * Co-residency of the grid is assumed from its size, which holds on an unshared
  * device; when another process holds CUs a wait may run out: the launch then
  * sets its error word and every block returns without computing further steps
@@ -304,7 +305,8 @@ int ppo_gru_seq_fwd(const float* h0, const float* masks, const int64_t* idx, con
  * it set returns at once) and passes it to ppo_clip_adam_guarded. */
 int ppo_gru_persist_set(int v);
 int ppo_gru_persist_get(void);
-/* polls before a bounded wait gives up (default 2^21; tests force timeouts with 1) */
+/* polls before a bounded wait gives up (default 2^21; 0: every wait gives up at once —
+ * the tests force timeouts with it) */
 int ppo_gru_persist_spin_set(int polls);
 /* 1 if a ppo_gru_seq_fwd launch on `stream` timed out since the last call (its
  * results are invalid), 0 if not, -1 on error; waits for `stream` only (a

@@ -578,6 +578,7 @@ class RecurrentEngine(CNNEngine):
         dhz = ws.get("dhz", n * H, device=dev)
         carry = ws.get("carry", n * H, device=dev)
         # persistent BPTT on the same counters (the forward has finished on this stream) and error word
+        _dist.assert_no_pending("train_minibatch_rec bptt")
         call("ppo_gru_seq_bwd_ws", dout.data_ptr(), sv["r"].data_ptr(), sv["z"].data_ptr(), sv["n"].data_ptr(),
              sv["ghn"].data_ptr(), sv["hin"].data_ptr(), masks.data_ptr(), idx.data_ptr(), self.whhT, T, n, H,
              dgi.data_ptr(), dgh.data_ptr(), dhz.data_ptr(), carry.data_ptr(), cnt.data_ptr(), self.status_ptr(0), s)

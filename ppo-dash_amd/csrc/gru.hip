@@ -375,6 +375,10 @@ __global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict
 // (the caller clears it): a launch that starts with it set returns immediately,
 // and ppo_clip_adam_guarded skips the optimizer step while it is set, so a timed
 // out minibatch never changes the parameters.
+// The h-independent operands of step t + 1 (the A-row and epilogue masks, gi) are
+// loaded during step t, after its publish — they are in flight while the block
+// waits for its group — and the minibatch index rows two steps ahead, so no
+// index -> mask chain sits on the per-step path; the biases are loaded once.
 template <int H>
 __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict__ h0, const float* __restrict__ masks,
                                                         const int64_t* __restrict__ idx, const float* __restrict__ whh,
@@ -383,22 +387,70 @@ __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict_
                                                         float* __restrict__ sz, float* __restrict__ sn,
                                                         float* __restrict__ sghn, float* __restrict__ shin,
                                                         int* __restrict__ cnt, int* __restrict__ err, int spin_max) {
+  constexpr int KW = H / 16;   // k per lane group and wave (as gru_fwd_tile)
   __shared__ f32x4 P[4][6][64];
   __shared__ int s_abort;
+  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
   const int j0 = blockIdx.y * 16, m0 = blockIdx.x * 32, grp = blockIdx.x, need = H / 16;
+  const int k0 = q * 4 * KW + g * KW;
   if (threadIdx.x == 0) s_abort = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_abort) return;   // an earlier launch on these words timed out: its outputs (and ours) are invalid
   float b[3][H / 16];
   gru_load_whh<H>(whh, j0, b);
   const bool sv = sr != nullptr;
+  const auto rh = make_rsrc(hout, (uint32_t)((size_t)T * n * H * 4 < 0xffffffffu ? (size_t)T * n * H * 4 : 0xffffffffu));
+  // rows this thread touches: A rows ra[rt] (row tile rt, lane c), epilogue rows re[e]
+  int ra[2], re[2];
+  bool oka[2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int m = m0 + 16 * rt + c;
+    oka[rt] = m < n;
+    ra[rt] = oka[rt] ? m : 0;
+  }
+  float pb[2][3];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int p = tid + 256 * e;
+    re[e] = min(m0 + (p >> 4), n - 1);
+#pragma unroll
+    for (int gt = 0; gt < 3; ++gt) pb[e][gt] = bhh[gt * H + j0 + (p & 15)];
+  }
+  // step operands: mask-plane offsets (through idx) two steps ahead, masks / gi one ahead
+  long long xa[2][2], xe[2][2];   // [slot][r]: mask-plane index of step (slot parity)
+  auto load_idx = [&](int t, int slot) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      xa[slot][r] = idx ? (long long)idx[(size_t)t * n + ra[r]] : (long long)t * n + ra[r];
+      xe[slot][r] = idx ? (long long)idx[(size_t)t * n + re[r]] : (long long)t * n + re[r];
+    }
+  };
+  float mA[2], pm[2], pg[2][3];
+  auto load_step = [&](int t, int slot) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) mA[rt] = oka[rt] && masks ? masks[xa[slot][rt]] : 1.0f;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      pm[e] = masks ? masks[xe[slot][e]] : 1.0f;
+      const float* gr = gi + ((size_t)t * n + re[e]) * 3 * H + j0 + ((tid + 256 * e) & 15);
+#pragma unroll
+      for (int gt = 0; gt < 3; ++gt) pg[e][gt] = gr[gt * H];
+    }
+  };
+  if (masks) {
+    load_idx(0, 0);
+    if (T > 1) load_idx(1, 1);
+  }
+  load_step(0, 0);
   for (int t = 0; t < T; ++t) {
     const size_t o = (size_t)t * n * H;
     if (t > 0) {   // h(t-1) of the group's rows complete (all its unit blocks published)
       if (threadIdx.x == 0) {
         const int target = need * t;
         int it = 0, ab = 0;
-        while (__hip_atomic_load(cnt + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        // spin bound 0: every wait gives up at once (the forced-timeout test mode)
+        while (spin_max == 0 || __hip_atomic_load(cnt + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
           if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {   // another block gave up
             ab = 1;
             break;
@@ -416,14 +468,79 @@ __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict_
       __syncthreads();
       if (s_abort) return;   // never compute step t from an incomplete h(t-1)
     }
-    const float* mk = masks && !idx ? masks + (size_t)t * n : masks;
-    gru_fwd_tile<H, true>(m0, j0, t == 0 ? h0 : hout + o - (size_t)n * H, mk, idx ? idx + (size_t)t * n : nullptr, b, bhh,
-                    gi + 3 * o, n, hout + o, sv ? sr + o : nullptr, sv ? sz + o : nullptr, sv ? sn + o : nullptr,
-                    sv ? sghn + o : nullptr, sv ? shin + o : nullptr, P);
+    // h(t-1): the A operand (masked, as gru_fwd_tile) and the epilogue's h
+    float a[2][KW], ph[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int s = 0; s < KW; s += 4) {
+        f32x4 v;
+        if (t == 0)
+          v = *reinterpret_cast<const f32x4*>(h0 + (size_t)ra[rt] * H + k0 + s);
+        else
+          v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rh, (int)((o - (size_t)n * H) + (size_t)ra[rt] * H + k0 + s) * 4, 0, 16));
+        v = oka[rt] ? v * mA[rt] : zero4();
+        a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
+      }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = j0 + ((tid + 256 * e) & 15);
+      ph[e] = t == 0 ? h0[(size_t)re[e] * H + j]
+                     : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                     rh, (int)((o - (size_t)n * H) + (size_t)re[e] * H + j) * 4, 0, 16));
+    }
+    f32x4 acc[2][3];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int gt = 0; gt < 3; ++gt) acc[rt][gt] = zero4();
+#pragma unroll
+    for (int s = 0; s < KW; ++s)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int gt = 0; gt < 3; ++gt)
+          acc[rt][gt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], b[gt][s], acc[rt][gt], 0, 0, 0);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int gt = 0; gt < 3; ++gt) P[q][rt * 3 + gt][lane] = acc[rt][gt];
+    __syncthreads();
+    // epilogue (gru_fwd_tile's): the K quarters summed in a fixed order, the cell
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int p = tid + 256 * e, ml = p >> 4, jl = p & 15, m = m0 + ml, j = j0 + jl;
+      if (m >= n) continue;
+      const int rt = ml >> 4, ir = ml & 15, ln = jl + 16 * (ir >> 2), rg = ir & 3;
+      float v[3];
+#pragma unroll
+      for (int gt = 0; gt < 3; ++gt)
+        v[gt] = ((P[0][rt * 3 + gt][ln][rg] + P[1][rt * 3 + gt][ln][rg]) + P[2][rt * 3 + gt][ln][rg]) +
+                P[3][rt * 3 + gt][ln][rg];
+      const float ghr = v[0] + pb[e][0], ghz = v[1] + pb[e][1], ghn = v[2] + pb[e][2];
+      const float r = sigm(pg[e][0] + ghr);
+      const float z = sigm(pg[e][1] + ghz);
+      const float nn = tanhf(pg[e][2] + r * ghn);
+      const float hin = ph[e] * pm[e];
+      const size_t oo = o + (size_t)m * H + j;
+      const float hv = __fmaf_rn(z, hin, (1.0f - z) * nn);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, hv), rh, (int)oo * 4, 0, 16);
+      if (sv) {
+        sr[oo] = r;
+        sz[oo] = z;
+        sn[oo] = nn;
+        sghn[oo] = ghn;
+        shin[oo] = hin;
+      }
+    }
     if (t + 1 < T) {   // publish h(t) of this tile
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its sc1 h stores done
       __syncthreads();   // also: every wave has read P before the next step rewrites it
       if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // step t + 1's h-independent operands (in flight during the wait), t + 2's index rows
+      load_step(t + 1, (t + 1) & 1);
+      if (masks && t + 2 < T) load_idx(t + 2, t & 1);
     }
   }
 }
@@ -548,12 +665,47 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
     }
   }
   const uint32_t gbytes = (uint32_t)((size_t)n * 3 * H * 4);
+  // the epilogue's elements (as gru_step_bwd16_kernel): rows re[e] (clamped), units je[e]
+  int re[2], je[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int p = tid + 256 * e;
+    re[e] = min(m0 + (p >> 4), n - 1);
+    je[e] = j0 + (p & 15);
+  }
+  // h-independent operands of step t - 1 (its mask, the saved activations of step
+  // t - 2) loaded during step t after its publish, the index rows two steps ahead;
+  // dhz carried in registers (the thread wrote it in the step before)
+  long long xe[2][2];
+  auto load_idx = [&](int t, int slot) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) xe[slot][e] = idx ? (long long)idx[(size_t)t * n + re[e]] : (long long)t * n + re[e];
+  };
+  float pd[2], pm[2], pc[2][6];
+  auto load_step = [&](int t, int slot) {
+    const size_t op = (size_t)(t - 1) * n * H;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const size_t oe = (size_t)re[e] * H + je[e];
+      pm[e] = masks ? masks[xe[slot][e]] : 1.0f;
+      pc[e][0] = dout[op + oe]; pc[e][1] = sr[op + oe]; pc[e][2] = sz[op + oe];
+      pc[e][3] = sn[op + oe]; pc[e][4] = sghn[op + oe]; pc[e][5] = shin[op + oe];
+    }
+  };
+  if (masks) {
+    load_idx(T - 1, (T - 1) & 1);
+    if (T - 2 >= 1) load_idx(T - 2, (T - 2) & 1);
+  }
+  load_step(T - 1, (T - 1) & 1);
+#pragma unroll
+  for (int e = 0; e < 2; ++e) pd[e] = dhz[(size_t)re[e] * H + je[e]];
   for (int t = T - 1; t >= 1; --t) {
     if (t < T - 1) {   // dgh(t) of the group's rows complete
       if (tid == 0) {
         const int target = need * (T - 1 - t);
         int it = 0, ab = 0;
-        while (__hip_atomic_load(cnt + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        // spin bound 0: every wait gives up at once (the forced-timeout test mode)
+        while (spin_max == 0 || __hip_atomic_load(cnt + grp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
           if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
             ab = 1;
             break;
@@ -572,20 +724,7 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
       if (s_abort) return;
     }
     const size_t o = (size_t)t * n * H, op = o - (size_t)n * H;
-    const float* mk = masks && !idx ? masks + (size_t)t * n : masks;
-    const int64_t* mi = idx ? idx + (size_t)t * n : nullptr;
     const auto rs = make_rsrc(dgh + 3 * o, gbytes);
-    // epilogue operands (in flight during the MFMAs)
-    float pd[2], pm[2], pc[2][6];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int p = tid + 256 * e, m = min(m0 + (p >> 4), n - 1), j = j0 + (p & 15);
-      const size_t oe = (size_t)m * H + j;
-      pd[e] = dhz[oe];
-      pm[e] = mk ? mk[mi ? mi[m] : m] : 1.0f;
-      pc[e][0] = dout[op + oe]; pc[e][1] = sr[op + oe]; pc[e][2] = sz[op + oe];
-      pc[e][3] = sn[op + oe]; pc[e][4] = sghn[op + oe]; pc[e][5] = shin[op + oe];
-    }
     f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
     for (int half = 0; half < NH; ++half) {
@@ -634,11 +773,14 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.daz), rsp, (int)(gg + H) * 4, 0, 16);
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dghn), rsp, (int)(gg + 2 * H) * 4, 0, 16);
       dhz[oe] = cg.dhz;
+      pd[e] = cg.dhz;   // the next step's dhz operand
     }
     if (t > 1) {   // publish dgh(t - 1) of this tile
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();   // also: every wave has read P before the next step rewrites it
       if (tid == 0) __hip_atomic_fetch_add(cnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      load_step(t - 1, (t - 1) & 1);   // in flight during the wait
+      if (masks && t - 2 >= 1) load_idx(t - 2, t & 1);
     }
   }
 }
@@ -647,13 +789,14 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
 static int g_gru_variant = 0;
 // persistent whole-sequence launches where the grid fits one block per CU, bit 0:
 // forward (gru_seq16_kernel), bit 1: backward (gru_seq_bwd16_kernel); clear bits
-// run one step kernel per step.  Default forward only: the persistent BPTT is
-// bit-identical but measured slower (12.6 vs 10.9 us per step at n = 512, H = 256:
-// the per-step dgh hand-off through write-through stores and the group counter
-// costs more than a kernel boundary there)
-static int g_gru_persist = 1;
+// run one step kernel per step.  Both by default since each loads its next step's
+// h-independent operands during the group wait (n = 512, H = 256: forward 7.1 vs
+// 8.7 us per step launched, BPTT 10.0 vs 10.2; before that prefetch the persistent
+// BPTT was the slower, 12.6 vs 10.9)
+static int g_gru_persist = 3;
 
-// bounded-wait length of the persistent kernels (polls of ~64 clocks each)
+// bounded-wait length of the persistent kernels (polls of ~64 clocks each; 0: every
+// wait times out, which the fail-safe tests use)
 static int g_gru_spin = 1 << 21;
 
 // Library-held synchronisation words for ppo_gru_seq_fwd (callers that pass their
@@ -850,7 +993,7 @@ PPO_API int ppo_gru_seq_fwd_ws(const float* h0, const float* masks, const int64_
   PPO_REQUIRE(T >= 0 && n >= 0 && H > 0 && H % 32 == 0, "ppo_gru_seq_fwd: T=%d n=%d H=%d", T, n, H);
   ProfScope prof("gru_seq_fwd", as_stream(stream), 2.0 * T * n * 3.0 * H * H);
   if (T > 0 && n > 0 && g_gru_variant == 0 && (g_gru_persist & 1) && (long long)ceil_div(n, 32) * (H / 16) <= gru_cus() &&
-      (H == 64 || H == 128 || H == 256 || H == 512)) {
+      (H == 64 || H == 128 || H == 256 || H == 512) && (long long)T * n * H * 4 < (1LL << 31)) {   // 32-bit offsets
     PPO_REQUIRE(counters != nullptr && err != nullptr, "ppo_gru_seq_fwd_ws: the persistent launch needs counters "
                                                        "(ppo_gru_seq_counters(n) ints) and an error word");
     hipStream_t st = as_stream(stream);

@@ -68,7 +68,7 @@ def test_gru_timeout_raises_before_any_step(gpu):
     bit-unchanged, and with the default bound the next update succeeds."""
     H_ = _hip()
     pol, agent, st, fill = _rollout(gpu, recurrent=True)
-    assert H_.call("ppo_gru_persist_get") == 1
+    assert H_.call("ppo_gru_persist_get") == 3
     fill()
     agent.update(st)            # a clean update first: Adam state exists
     st.after_update()

@@ -1274,7 +1274,8 @@ def test_gru_persistent_sequence_equals_steps(gpu, T, n, H, use_idx):
         masks = (torch.rand(T * n, generator=g) > 0.1).float().cuda()
         idx = None
     outs = {}
-    for persist in (0, 1):
+    prev = Hh.call("ppo_gru_persist_get")
+    for persist in (0, 1):   # step launches, persistent launch
         o = {k: torch.full((T * n, H), float("nan"), device=gpu) for k in ("h", "r", "z", "n", "ghn", "hin")}
         Hh.call("ppo_gru_persist_set", persist)
         try:
@@ -1283,13 +1284,14 @@ def test_gru_persistent_sequence_equals_steps(gpu, T, n, H, use_idx):
                     o["z"].data_ptr(), o["n"].data_ptr(), o["ghn"].data_ptr(), o["hin"].data_ptr(), _s())
             torch.cuda.synchronize()
         finally:
-            Hh.call("ppo_gru_persist_set", 1)
+            Hh.call("ppo_gru_persist_set", prev)
         outs[persist] = o
-    assert Hh.call("ppo_gru_persist_timeouts", _s()) == 0
-    for k in outs[0]:
-        assert torch.isfinite(outs[1][k]).all(), k
-        assert torch.equal(outs[0][k], outs[1][k]), (k, (outs[0][k] - outs[1][k]).abs().max().item(),
-                                                      (outs[0][k] != outs[1][k]).sum().item())
+        assert Hh.call("ppo_gru_persist_timeouts", _s()) == 0, persist
+    for p in (1,):
+        for k in outs[0]:
+            assert torch.isfinite(outs[p][k]).all(), (p, k)
+            assert torch.equal(outs[0][k], outs[p][k]), (p, k, (outs[0][k] - outs[p][k]).abs().max().item(),
+                                                          (outs[0][k] != outs[p][k]).sum().item())
 
 
 @pytest.mark.parametrize("T,n,H,use_idx", [(24, 512, 256, True), (9, 37, 64, False), (5, 100, 128, True),
