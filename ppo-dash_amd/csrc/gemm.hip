@@ -1306,15 +1306,17 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
   wait_vm0();
   for (int i = tid; i < 2 * 3 * PL / 8; i += 512) reinterpret_cast<uint4*>(&S[0][0])[i] = uint4{0, 0, 0, 0};
   f32x4 stg[UPER][2];
+  // unit j of image b through a per-image buffer resource (units past the image
+  // read out of range: 0, no branch)
+  auto fetch_unit = [&](int b, int j) {
+    const auto ra = make_rsrc(a2 + (size_t)b * 5184, 5184 * 4);
+    const int u = tid + 512 * j, off = u < UNITS ? 32 * u : 0x7fffffe0;
+    stg[j][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+    stg[j][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
+  };
   auto fetch = [&](int b) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(a2 + (size_t)b * 5184);
 #pragma unroll
-    for (int j = 0; j < UPER; ++j) {
-      const int u = tid + 512 * j;
-      const int uu = u < UNITS ? u : 0;   // unconditional loads: no exec branch around them
-      stg[j][0] = src[2 * uu];
-      stg[j][1] = src[2 * uu + 1];
-    }
+    for (int j = 0; j < UPER; ++j) fetch_unit(b, j);
   };
   auto put = [&](int buf) {
 #pragma unroll
@@ -1336,15 +1338,16 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
   if (b < B) {
     fetch(b);
     put(0);
-    if (b + G < B) fetch(b + G);
+    fetch(b + G < B ? b + G : b);
   }
   __syncthreads();
-  const bool late = stagger && mh == 1;   // waves 4-7 stage after their compute (see conv3 dgrad)
+  (void)stagger;
   for (; b < B; b += G) {
-    if (!late) {
-      if (b + G < B) put(cur ^ 1);
-      if (b + 2 * G < B) fetch(b + 2 * G);
-    }
+    // the stage write unconditional (past the end: a copy of this image into the
+    // idle stage), the image after next fetched one unit per k-step 1, 3 inside the
+    // MFMA stream instead of in a burst here
+    put(cur ^ 1);
+    const int bnn = b + 2 * G < B ? b + 2 * G : b;
     const uint16_t* Sc = S[cur];
     f32x4 acc[2] = {zero4(), zero4()};
 #pragma unroll
@@ -1364,14 +1367,14 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
   _Pragma("unroll") for (int u = 0; u < 2; ++u) acc[u] = mma(w.Y, a[u].X, acc[u]);
       PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
+      if (s == 1 || s == 3) {
+        fetch_unit(bnn, s >> 1);
+        __builtin_amdgcn_sched_barrier(0);   // the loads stay in their slot
+      }
     }
     if (kh == 1) {
       R[cur][nt][mh][0][lane] = acc[0];
       R[cur][nt][mh][1][lane] = acc[1];
-    }
-    if (late) {
-      if (b + G < B) put(cur ^ 1);
-      if (b + 2 * G < B) fetch(b + 2 * G);
     }
     __syncthreads();   // stage cur consumed, stage cur ^ 1 complete, partials in R[cur]
     if (kh == 0) {
