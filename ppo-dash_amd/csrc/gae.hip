@@ -22,6 +22,20 @@ constexpr int GAE_THREADS = 256;
 #ifndef PPO_GAE_U
 #define PPO_GAE_U 16
 #endif
+#ifndef PPO_GAE_NT
+#define PPO_GAE_NT 0
+#endif
+// streaming planes: nontemporal loads and stores (PPO_GAE_NT 1), stores only (2), or plain (0)
+template <class T_>
+__device__ __forceinline__ T_ gld(const T_* p) {
+  if constexpr (PPO_GAE_NT == 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <class T_>
+__device__ __forceinline__ void gst(T_* p, T_ v) {
+  if constexpr (PPO_GAE_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 constexpr int GAE_U = PPO_GAE_U;  // time steps prefetched per chunk (16: 4.86 vs 4.75 TB/s for 8 on 1M lanes, tools/gae_ab.sh)
 
 // Advantage moments as (count, mean, M2) (the reference's
@@ -107,10 +121,10 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
       for (int j = 0; j < GAE_U; ++j) {
         const int t = t0 - j;
         if (t >= 0) {
-          rr[j] = rewards[(size_t)t * NN + n];
-          mm[j] = masks[(size_t)(t + 1) * NN + n];
-          vv[j] = (USE_GAE || PTL || FUSE_ADV) ? value_preds[(size_t)t * NN + n] : 0.0f;
-          bb[j] = PTL ? bad_masks[(size_t)(t + 1) * NN + n] : 1.0f;
+          rr[j] = gld(rewards + (size_t)t * NN + n);
+          mm[j] = gld(masks + (size_t)(t + 1) * NN + n);
+          vv[j] = (USE_GAE || PTL || FUSE_ADV) ? gld(value_preds + (size_t)t * NN + n) : 0.0f;
+          bb[j] = PTL ? gld(bad_masks + (size_t)(t + 1) * NN + n) : 1.0f;
         }
       }
 #pragma unroll
@@ -142,10 +156,10 @@ __global__ __launch_bounds__(GAE_THREADS) void gae_kernel(
             out = x;
             carry = x;
           }
-          returns[(size_t)t * NN + n] = out;
+          gst(returns + (size_t)t * NN + n, out);
           if (FUSE_ADV) {
             const float d = out - vv[j];       // returns[:-1] - value_preds[:-1]
-            adv[(size_t)t * NN + n] = d;
+            gst(adv + (size_t)t * NN + n, d);
             mom.add((double)d);
           }
         }
