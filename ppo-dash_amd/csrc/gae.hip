@@ -20,10 +20,10 @@ namespace {
 
 constexpr int GAE_THREADS = 256;
 #ifndef PPO_GAE_U
-#define PPO_GAE_U 16
+#define PPO_GAE_U 64
 #endif
 #ifndef PPO_GAE_NT
-#define PPO_GAE_NT 0
+#define PPO_GAE_NT 1
 #endif
 // streaming planes: nontemporal loads and stores (PPO_GAE_NT 1), stores only (2), or plain (0)
 template <class T_>
@@ -36,7 +36,11 @@ __device__ __forceinline__ void gst(T_* p, T_ v) {
   if constexpr (PPO_GAE_NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
-constexpr int GAE_U = PPO_GAE_U;  // time steps prefetched per chunk (16: 4.86 vs 4.75 TB/s for 8 on 1M lanes, tools/gae_ab.sh)
+// time steps prefetched per chunk; with nontemporal loads and stores 64 steps run
+// 5.15-5.17 TB/s on 1M lanes, 32 steps 5.05-5.07, against 4.79-4.84 for 16 plain
+// (16 + nontemporal 4.68-4.86, nontemporal stores only 4.69-4.72; tools/gae_ab.sh,
+// profiles/r04_gae_ab.log, r04_gae_ab2.log)
+constexpr int GAE_U = PPO_GAE_U;
 
 // Advantage moments as (count, mean, M2) (the reference's
 // advantages.mean() / .std(), T/a2c_ppo_acktr/algo/ppo.py:35-37): each thread
