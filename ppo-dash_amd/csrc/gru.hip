@@ -507,9 +507,14 @@ __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict_
 #pragma unroll
       for (int gt = 0; gt < 3; ++gt) P[q][rt * 3 + gt][lane] = acc[rt][gt];
     __syncthreads();
-    // epilogue (gru_fwd_tile's): the K quarters summed in a fixed order, the cell
+    // epilogue (gru_fwd_tile's): the K quarters summed in a fixed order, the cell;
+    // h stored first, the saved gates after the publish (no other block reads them)
+    float keep[2][5];
+    size_t ko[2];
+    bool kv[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
+      kv[e] = false;
       const int p = tid + 256 * e, ml = p >> 4, jl = p & 15, m = m0 + ml, j = j0 + jl;
       if (m >= n) continue;
       const int rt = ml >> 4, ir = ml & 15, ln = jl + 16 * (ir >> 2), rg = ir & 3;
@@ -526,21 +531,32 @@ __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict_
       const size_t oo = o + (size_t)m * H + j;
       const float hv = __fmaf_rn(z, hin, (1.0f - z) * nn);
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, hv), rh, (int)oo * 4, 0, 16);
-      if (sv) {
-        sr[oo] = r;
-        sz[oo] = z;
-        sn[oo] = nn;
-        sghn[oo] = ghn;
-        shin[oo] = hin;
-      }
+      kv[e] = true;
+      ko[e] = oo;
+      keep[e][0] = r; keep[e][1] = z; keep[e][2] = nn; keep[e][3] = ghn; keep[e][4] = hin;
     }
+    auto store_saves = [&]() {
+      if (!sv) return;
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        if (kv[e]) {
+          sr[ko[e]] = keep[e][0];
+          sz[ko[e]] = keep[e][1];
+          sn[ko[e]] = keep[e][2];
+          sghn[ko[e]] = keep[e][3];
+          shin[ko[e]] = keep[e][4];
+        }
+    };
     if (t + 1 < T) {   // publish h(t) of this tile
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its sc1 h stores done
       __syncthreads();   // also: every wave has read P before the next step rewrites it
       if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      store_saves();   // written during the wait
       // step t + 1's h-independent operands (in flight during the wait), t + 2's index rows
       load_step(t + 1, (t + 1) & 1);
       if (masks && t + 2 < T) load_idx(t + 2, t & 1);
+    } else {
+      store_saves();
     }
   }
 }
@@ -753,34 +769,52 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
     __syncthreads();
     float* dgh_p = dgh + 3 * op;
     const auto rsp = make_rsrc(dgh_p, gbytes);
+    // dgh stored first; dgi, carry and dhz after the publish (no other block reads them)
+    float keep[2][5];
+    size_t ko[2], kg[2];
+    bool kv[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
+      kv[e] = false;
       const int p = tid + 256 * e, ml = p >> 4, jl = p & 15, m = m0 + ml, j = j0 + jl;
       if (m >= n) continue;
       const int rt = ml >> 4, ir = ml & 15, ln = jl + 16 * (ir >> 2), rg = ir & 3;
       const float v = ((P[0][rt][ln][rg] + P[1][rt][ln][rg]) + P[2][rt][ln][rg]) + P[3][rt][ln][rg];
       const size_t oe = (size_t)m * H + j;
       const float cv = gru_carry(v, pd[e], pm[e]);
-      carry[oe] = cv;
       // gru_cell_bwd_elem for step t - 1, dgh stored write-through for the group
       const GruCellGrad cg = gru_cell_grad(pc[e][0] + cv, pc[e][1], pc[e][2], pc[e][3], pc[e][4], pc[e][5]);
       const size_t gg = (size_t)m * 3 * H + j;
-      float* dgi_p = dgi + 3 * op;
-      dgi_p[gg] = cg.dar;
-      dgi_p[gg + H] = cg.daz;
-      dgi_p[gg + 2 * H] = cg.dan;
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dar), rsp, (int)gg * 4, 0, 16);
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.daz), rsp, (int)(gg + H) * 4, 0, 16);
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dghn), rsp, (int)(gg + 2 * H) * 4, 0, 16);
-      dhz[oe] = cg.dhz;
+      kv[e] = true;
+      ko[e] = oe;
+      kg[e] = gg;
+      keep[e][0] = cv; keep[e][1] = cg.dar; keep[e][2] = cg.daz; keep[e][3] = cg.dan; keep[e][4] = cg.dhz;
       pd[e] = cg.dhz;   // the next step's dhz operand
     }
+    auto store_rest = [&]() {
+      float* dgi_p = dgi + 3 * op;
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        if (kv[e]) {
+          carry[ko[e]] = keep[e][0];
+          dgi_p[kg[e]] = keep[e][1];
+          dgi_p[kg[e] + H] = keep[e][2];
+          dgi_p[kg[e] + 2 * H] = keep[e][3];
+          dhz[ko[e]] = keep[e][4];
+        }
+    };
     if (t > 1) {   // publish dgh(t - 1) of this tile
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();   // also: every wave has read P before the next step rewrites it
       if (tid == 0) __hip_atomic_fetch_add(cnt + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      store_rest();   // written during the wait
       load_step(t - 1, (t - 1) & 1);   // in flight during the wait
       if (masks && t - 2 >= 1) load_idx(t - 2, t & 1);
+    } else {
+      store_rest();
     }
   }
 }
