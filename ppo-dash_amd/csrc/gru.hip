@@ -20,6 +20,7 @@
 //     dx = dgi · W_ih[:, :H] masked by the fc ReLU.
 // Saved per step for the backward: r, z, n, W_hn h + b_hn, h_in ([T][n][H] each).
 #include <mutex>
+#include <type_traits>
 
 #include "igemm.h"
 
@@ -680,6 +681,42 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
       b[s] = v[0]; b[s + 1] = v[1]; b[s + 2] = v[2]; b[s + 3] = v[3];
     }
   }
+  // L2 agreement: when every unit block of the row group runs on one XCD (the grid's
+  // round-robin dispatch puts group x on XCD x mod 8, but nothing guarantees it),
+  // dgh is handed over through that XCD's L2 — plain stores and loads instead of
+  // write-through sc1 ones (which re-read the group's dgh from the memory side 16
+  // times).  Each block publishes its XCC_ID (release / acquire, once per launch)
+  // and the group takes the L2 path only if all ids agree.
+  __shared__ int s_local;
+  {
+    int* start = cnt + gridDim.x;
+    int* xslot = cnt + 2 * gridDim.x + grp * 32;
+    if (tid == 0) {
+      const int xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11)) & 15;   // HW_REG_XCC_ID[3:0]
+      __hip_atomic_store(xslot + blockIdx.y, xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(start + grp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      int it = 0, ab = 0;
+      while (spin_max == 0 || __hip_atomic_load(start + grp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+          ab = 1;
+          break;
+        }
+        if (++it > spin_max) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ab = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      int loc = !ab;
+      for (int y = 0; y < need && loc; ++y)
+        loc = __hip_atomic_load(xslot + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == xcc + 1;
+      s_abort = ab;
+      s_local = loc;
+    }
+    __syncthreads();
+    if (s_abort) return;
+  }
   const uint32_t gbytes = (uint32_t)((size_t)n * 3 * H * 4);
   // the epilogue's elements (as gru_step_bwd16_kernel): rows re[e] (clamped), units je[e]
   int re[2], je[2];
@@ -715,6 +752,8 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
   load_step(T - 1, (T - 1) & 1);
 #pragma unroll
   for (int e = 0; e < 2; ++e) pd[e] = dhz[(size_t)re[e] * H + je[e]];
+  auto steps = [&](auto local) {
+  constexpr int CP = decltype(local)::value ? 0 : 16;   // dgh cache policy: L2 (plain) or sc1
   for (int t = T - 1; t >= 1; --t) {
     if (t < T - 1) {   // dgh(t) of the group's rows complete
       if (tid == 0) {
@@ -753,7 +792,7 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
 #pragma unroll
         for (int s = 0; s < KH; s += 4) {
           f32x4 v = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((ok ? m : 0) * 3 * H + kb + s) * 4, 0, 16));
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((ok ? m : 0) * 3 * H + kb + s) * 4, 0, CP));
           v = ok ? v : zero4();
           a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
         }
@@ -785,9 +824,9 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
       // gru_cell_bwd_elem for step t - 1, dgh stored write-through for the group
       const GruCellGrad cg = gru_cell_grad(pc[e][0] + cv, pc[e][1], pc[e][2], pc[e][3], pc[e][4], pc[e][5]);
       const size_t gg = (size_t)m * 3 * H + j;
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dar), rsp, (int)gg * 4, 0, 16);
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.daz), rsp, (int)(gg + H) * 4, 0, 16);
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dghn), rsp, (int)(gg + 2 * H) * 4, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dar), rsp, (int)gg * 4, 0, CP);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.daz), rsp, (int)(gg + H) * 4, 0, CP);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dghn), rsp, (int)(gg + 2 * H) * 4, 0, CP);
       kv[e] = true;
       ko[e] = oe;
       kg[e] = gg;
@@ -817,6 +856,11 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
       store_rest();
     }
   }
+  };
+  if (s_local)
+    steps(std::true_type{});
+  else
+    steps(std::false_type{});
 }
 
 // 0: register-tiled step kernels where H allows; 1: the tile-GEMM steps (A/B)
@@ -923,7 +967,7 @@ int launch_seq_bwd16(const float* dout, const float* sr, const float* sz, const 
                      const float* shin, const float* masks, const int64_t* idx, const float* whhT, int T, int n,
                      float* dgi, float* dgh, float* dhz, float* carry, int* cnt, int* err, hipStream_t st) {
   const int groups = ceil_div(n, 32);
-  PPO_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)groups * sizeof(int), st), "ppo_gru_seq_bwd: counter reset");
+  PPO_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)groups * (2 + 32) * sizeof(int), st), "ppo_gru_seq_bwd: counter reset");
   dim3 grid((unsigned)groups, H / 16);
   gru_seq_bwd16_kernel<H><<<grid, 256, 0, st>>>(dout, sr, sz, sn, sghn, shin, masks, idx, whhT, T, n, dgi, dgh, dhz,
                                                 carry, cnt, err, g_gru_spin);
@@ -1018,7 +1062,9 @@ PPO_API int ppo_gru_variant_get(void) { return g_gru_variant; }
 // which at ~10 us per step kernel were the critical path of the recurrent update.
 // Rows of step t are t*n .. t*n + n - 1; mask of row j at step t: masks[idx[t*n + j]]
 // (idx NULL: masks[t*n + j]).
-PPO_API int ppo_gru_seq_counters(int n) { return n > 0 ? ceil_div(n, 32) : 1; }
+// per 32-row group: the step counter, the BPTT's start counter and XCC_ID slots of
+// up to 32 unit blocks (gru_seq_bwd16_kernel's L2 agreement)
+PPO_API int ppo_gru_seq_counters(int n) { return n > 0 ? ceil_div(n, 32) * (2 + 32) : 1; }
 
 PPO_API int ppo_gru_seq_fwd_ws(const float* h0, const float* masks, const int64_t* idx, const float* whh,
                                const float* bhh, const float* gi, int T, int n, int H, float* hout, float* save_r,
