@@ -312,7 +312,8 @@ int ppo_gru_persist_spin_set(int polls);
  * results are invalid), 0 if not, -1 on error; waits for `stream` only (a
  * stream-ordered read of the word) and clears it */
 int ppo_gru_persist_timeouts(void* stream);
-/* counters a persistent launch over n rows needs (ints) */
+/* counters a persistent launch over n rows needs (ints; per 32-row group the step
+ * counter, the BPTT start counter and 32 XCC_ID slots of its L2 agreement) */
 int ppo_gru_seq_counters(int n);
 /* ppo_gru_seq_fwd with caller-owned synchronisation words: counters
  * (ppo_gru_seq_counters(n) ints, reset by the call on `stream`) and err (one int,
