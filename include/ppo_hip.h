@@ -312,9 +312,16 @@ int ppo_gru_persist_spin_set(int polls);
  * results are invalid), 0 if not, -1 on error; waits for `stream` only (a
  * stream-ordered read of the word) and clears it */
 int ppo_gru_persist_timeouts(void* stream);
-/* counters a persistent launch over n rows needs (ints; per 32-row group the step
- * counter, the BPTT start counter and 32 XCC_ID slots of its L2 agreement) */
+/* counters a persistent launch over n rows needs (ints; G = ceil(n/32) groups):
+ * [G step counters][G BPTT start counters][32·G XCC_ID slots of the L2
+ * agreement][G BPTT path reports: 1 sc1 hand-off, 2 L2 hand-off, 0 not run] */
 int ppo_gru_seq_counters(int n);
+/* the persistent BPTT's dgh hand-off (gru_seq_bwd16_kernel): 1 (default) a row
+ * group whose unit blocks all report one XCC_ID stores dgh plain (kept in that
+ * XCD's L2), else sc1 (write-through); 0 sc1 for every group.  The loads are sc1
+ * (L1 bypassed) on both paths. */
+int ppo_gru_l2_set(int v);
+int ppo_gru_l2_get(void);
 /* ppo_gru_seq_fwd with caller-owned synchronisation words: counters
  * (ppo_gru_seq_counters(n) ints, reset by the call on `stream`) and err (one int,
  * see above); both may be NULL when the step launches run (persist 0) */

@@ -19,6 +19,7 @@ A CPU restatement (numpy) of the reference's PPO hot path:
                                      algo/ppo.py:51-81   -> ppo_loss_grads()
   * clip_grad_norm_ + Adam.step      algo/ppo.py:82-84   -> clip_adam()
   * one whole iteration in T/run.py:168-248 order -> run_iteration()
+  * PPO.update over recurrent_generator (GRU BPTT)  -> run_update_recurrent()
 
 All paths above are relative to ppo-dash-study/001_baseline/ppo/ (identical to
 ppo-dash-training/pytorch-a2c-ppo-acktr-gail/a2c_ppo_acktr/ up to the V=0 edits,
@@ -654,3 +655,49 @@ def run_iteration(flat_params, shapes, obs_u8, exp_noise, rewards, masks, perms,
     return dict(values=vals, actions=acts, log_probs=logps, next_value=nv, returns=ret,
                 value_preds=vp, advantages=adv, final_params=flat, losses=losses, first=first,
                 last_clipped_grad=gc)
+
+
+def run_update_recurrent(flat_params, shapes, obs_u8, vec, h0, masks, actions, old_logp, value_preds, returns,
+                         perms, *, num_mini_batch, clip=0.1, value_coef=0.5, entropy_coef=0.01, lr=1e-3,
+                         eps=1e-5, max_grad_norm=0.5, dtype=np.float64):
+    """PPO.update of a recurrent policy (algo/ppo.py:34-96 with
+    recurrent_generator, storage.py:162-223; the GRU over each env column from
+    the rollout's first hidden state, model.py:116-165) replayed on a recorded
+    rollout: obs_u8 [T+1,N,C,84,84], vec [T+1,N,V], h0 [N,H] (hidden state of
+    step 0), masks [T+1,N], actions / old_logp [T,N], value_preds / returns
+    [T+1,N] (fp32, as compute_returns left them), perms [E,N] (the randperms
+    the update draws).  Returns final params, per-minibatch losses, each
+    minibatch's pre-clip gradient and total norm, and the epoch-mean losses."""
+    T1, N = obs_u8.shape[:2]
+    T = T1 - 1
+    adv = normalize_advantages(np.asarray(returns, np.float32).reshape(T + 1, N),
+                               np.asarray(value_preds, np.float32).reshape(T + 1, N))
+    flat = np.asarray(flat_params, dtype).copy()
+    m = np.zeros_like(flat)
+    v = np.zeros_like(flat)
+    step = 0
+    mb_losses, preclip, norms = [], [], []
+    vp = np.asarray(value_preds, np.float64).reshape(T + 1, N)
+    ret = np.asarray(returns, np.float64).reshape(T + 1, N)
+    acts = np.asarray(actions).reshape(T, N)
+    olp = np.asarray(old_logp, np.float64).reshape(T, N)
+    mk = np.asarray(masks, np.float64).reshape(T + 1, N)
+    for perm in perms:
+        for envs in rec_minibatches(perm, num_mini_batch):
+            p = unflatten(flat, shapes, dtype)
+            obs = obs_u8[:T][:, envs].reshape(T * len(envs), *obs_u8.shape[2:])
+            x_vec = np.asarray(vec, np.float64)[:T][:, envs].reshape(T * len(envs), -1)
+            value, logits, cache = recurrent_forward(p, decode_obs(obs), x_vec, np.asarray(h0, dtype)[envs],
+                                                     mk[:T][:, envs])
+            f = lambda a: a[:, envs].reshape(-1)  # noqa: E731  rows t * n + j (_flatten_helper order)
+            lg = loss_head_grads(value, logits, f(acts), f(olp), f(adv), f(vp[:T]), f(ret[:T]), clip,
+                                 value_coef, entropy_coef)
+            g = flatten(recurrent_backward(p, cache, lg["g_value"], lg["g_logits"]), shapes).astype(dtype)
+            step += 1
+            flat, m, v, _, total = clip_adam(flat, g, m, v, step, lr, eps, max_grad_norm)
+            mb_losses.append([lg["value_loss"], lg["action_loss"], lg["entropy"]])
+            preclip.append(g)
+            norms.append(total)
+    mb_losses = np.array(mb_losses)
+    return dict(final_params=flat, mb_losses=mb_losses, preclip_grads=preclip, total_norms=np.array(norms),
+                losses=mb_losses.mean(0), advantages=adv)

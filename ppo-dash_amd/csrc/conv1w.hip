@@ -93,11 +93,14 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw_kernel(const float* __
   float bacc = 0.f;
   // the k-steps of one image this wave computes: s = wave, wave + 8, wave + 16 (all tiles) and
   // k-step 24 for tile `wave` only; dz of k-step s for this lane: pixels 16 s + 8 h .. +7, channel l32
-  auto dz_load = [&](int b, int s, float (&d)[8]) {
+  // one dz_load = DZ_LOADS single-dword buffer loads (128 B apart, so never merged);
+  // the vmcnt of barrier Y below counts them
+  constexpr int DZ_LOADS = 8;
+  auto dz_load = [&](int b, int s, float (&d)[DZ_LOADS]) {
     const auto rs = make_rsrc(dz1 + (size_t)b * 12800, 12800 * 4);
     const int o = ((16 * s + 8 * h) * 32 + l32) * 4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, o + 128 * j, 0, 0));
+    for (int j = 0; j < DZ_LOADS; ++j) d[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, o + 128 * j, 0, 0));
   };
   // B fragment of tile tt for quads (oy0, Q0), (oy1, Q1) of k-step s: 8 bf16
   auto bfrag = [&](const uint16_t* S, int tt, int q0off, int q1off) {
@@ -287,11 +290,14 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw2_kernel(const float* _
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   float bacc = 0.f;
-  auto dz_load = [&](int b, int s, float (&d)[8]) {
+  // one dz_load = DZ_LOADS single-dword buffer loads (128 B apart, so never merged);
+  // the vmcnt of barrier Y below counts them
+  constexpr int DZ_LOADS = 8;
+  auto dz_load = [&](int b, int s, float (&d)[DZ_LOADS]) {
     const auto rs = make_rsrc(dz1 + (size_t)b * 12800, 12800 * 4);
     const int o = ((16 * s + 8 * h) * 32 + l32) * 4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, o + 128 * j, 0, 0));
+    for (int j = 0; j < DZ_LOADS; ++j) d[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, o + 128 * j, 0, 0));
   };
   auto bfrag = [&](const uint16_t* S, int tt, int q0off, int q1off) {
     const int toff = ((tt >> 1) * IMG + 4 * (tt & 1)) * ROWE + lbase;
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw2_kernel(const float* _
     for (int j = 0; j < 8; ++j) bacc += d[j];
   };
   int b = blockIdx.x, cur = 0;
-  float dA[8], dB[8], dC[8], dD[8];
+  float dA[DZ_LOADS], dB[DZ_LOADS], dC[DZ_LOADS], dD[DZ_LOADS];
   if (b < B) {
     dma_raw(b);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -346,9 +352,12 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw2_kernel(const float* _
     kstep(S, wave + 8, dB, 0, 8);
     add8(dB);
     if (nxt) {
-      // raw(b + G) is older than dB's loads, which k-step B waited for; the explicit wait
-      // (dC, dD may stay in flight) makes the order independent of the compiler's waits
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      // raw(b + G)'s DMA was issued after dA / dB's loads of image b + G (previous
+      // iteration, or the prologue) and before this iteration's dz_load(dC) and
+      // dz_load(dD); both asm statements clobber memory, so the compiler moves no
+      // load across them and exactly those 2 * DZ_LOADS loads are younger than the
+      // DMA: vmcnt(2 * DZ_LOADS) retires the DMA and leaves dC, dD in flight
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DZ_LOADS) : "memory");
       lds_barrier();   // Y: every wave's pieces of raw(b + G) are in LDS
       put(cur ^ 1);
       lds_barrier();   // Z: raw consumed, E[cur ^ 1] complete

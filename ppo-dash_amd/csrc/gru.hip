@@ -661,7 +661,7 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
     const float* __restrict__ sn, const float* __restrict__ sghn, const float* __restrict__ shin,
     const float* __restrict__ masks, const int64_t* __restrict__ idx, const float* __restrict__ whhT, int T, int n,
     float* __restrict__ dgi, float* __restrict__ dgh, float* __restrict__ dhz, float* __restrict__ carry,
-    int* __restrict__ cnt, int* __restrict__ err, int spin_max) {
+    int* __restrict__ cnt, int* __restrict__ err, int spin_max, int l2_mode) {
   constexpr int KW = 3 * H / 16;
   constexpr int NH = KW % 8 == 0 ? 2 : 1, KH = KW / NH;
   __shared__ f32x4 P[4][2][64];
@@ -681,12 +681,24 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
       b[s] = v[0]; b[s + 1] = v[1]; b[s + 2] = v[2]; b[s + 3] = v[3];
     }
   }
-  // L2 agreement: when every unit block of the row group runs on one XCD (the grid's
-  // round-robin dispatch puts group x on XCD x mod 8, but nothing guarantees it),
-  // dgh is handed over through that XCD's L2 — plain stores and loads instead of
-  // write-through sc1 ones (which re-read the group's dgh from the memory side 16
-  // times).  Each block publishes its XCC_ID (release / acquire, once per launch)
-  // and the group takes the L2 path only if all ids agree.
+  // L2 agreement: when every unit block of the row group runs on one XCD, dgh is
+  // handed over through that XCD's L2: the producers store it plain (the line stays
+  // in the XCD's L2; a write-through sc1 store drops it, so 16 readers re-fetched
+  // the group's dgh from the memory side) and the consumers load it sc1.  The
+  // consumer's loads are sc1 on BOTH paths, so no dgh byte is ever served from a
+  // CU's vector L1 — the stale-L1 hazard of a plain load after a relaxed poll
+  // (MI355X_MICROARCH "Correctness boundaries") cannot arise whatever the L1 holds.
+  // Invariant of the L2 path (gru_seq_bwd16 row): (1) a producer's plain
+  // store is acknowledged (vmcnt) once it is in its XCD's L2, and every storing wave
+  // waits vmcnt(0) and joins a barrier before lane 0 adds to the group counter;
+  // (2) the consumer polls that counter, joins a barrier, then loads with sc1, which
+  // skips L1 and reads the XCD's L2; (3) producer and consumer share that L2 — each
+  // block reads its own HW_REG_XCC_ID and publishes it (release / acquire, once per
+  // launch), and the group takes the path only if all ids agree.  (3) is checked,
+  // never assumed: the grid's round-robin dispatch puts the unit blocks of group x
+  // on one XCD only when gridDim.x (= ceil(n/32)) is a multiple of 8; other groups,
+  // and every group with ppo_gru_l2_set(0), keep sc1 stores.  Block (x, 0) reports
+  // the path its group took (1 sc1, 2 L2) in the counter buffer (ppo_gru_seq_counters).
   __shared__ int s_local;
   {
     int* start = cnt + gridDim.x;
@@ -708,9 +720,11 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      int loc = !ab;
+      int loc = !ab && l2_mode != 0;
       for (int y = 0; y < need && loc; ++y)
         loc = __hip_atomic_load(xslot + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == xcc + 1;
+      if (blockIdx.y == 0 && !ab)   // the group's path, for ppo_gru_seq_counters' report slots
+        __hip_atomic_store(cnt + (2 + 32) * gridDim.x + grp, loc ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_abort = ab;
       s_local = loc;
     }
@@ -753,7 +767,9 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
 #pragma unroll
   for (int e = 0; e < 2; ++e) pd[e] = dhz[(size_t)re[e] * H + je[e]];
   auto steps = [&](auto local) {
-  constexpr int CP = decltype(local)::value ? 0 : 16;   // dgh cache policy: L2 (plain) or sc1
+  // dgh stores: plain on the L2 path (the line stays in the group's L2), else sc1;
+  // dgh loads: sc1 on both (L1 bypassed, L2-served)
+  constexpr int CP_ST = decltype(local)::value ? 0 : 16, CP_LD = 16;
   for (int t = T - 1; t >= 1; --t) {
     if (t < T - 1) {   // dgh(t) of the group's rows complete
       if (tid == 0) {
@@ -792,7 +808,7 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
 #pragma unroll
         for (int s = 0; s < KH; s += 4) {
           f32x4 v = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((ok ? m : 0) * 3 * H + kb + s) * 4, 0, CP));
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((ok ? m : 0) * 3 * H + kb + s) * 4, 0, CP_LD));
           v = ok ? v : zero4();
           a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
         }
@@ -824,9 +840,9 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
       // gru_cell_bwd_elem for step t - 1, dgh stored write-through for the group
       const GruCellGrad cg = gru_cell_grad(pc[e][0] + cv, pc[e][1], pc[e][2], pc[e][3], pc[e][4], pc[e][5]);
       const size_t gg = (size_t)m * 3 * H + j;
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dar), rsp, (int)gg * 4, 0, CP);
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.daz), rsp, (int)(gg + H) * 4, 0, CP);
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dghn), rsp, (int)(gg + 2 * H) * 4, 0, CP);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dar), rsp, (int)gg * 4, 0, CP_ST);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.daz), rsp, (int)(gg + H) * 4, 0, CP_ST);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, cg.dghn), rsp, (int)(gg + 2 * H) * 4, 0, CP_ST);
       kv[e] = true;
       ko[e] = oe;
       kg[e] = gg;
@@ -876,6 +892,10 @@ static int g_gru_persist = 3;
 // bounded-wait length of the persistent kernels (polls of ~64 clocks each; 0: every
 // wait times out, which the fail-safe tests use)
 static int g_gru_spin = 1 << 21;
+
+// BPTT dgh hand-off: 1 (default) the L2 path where a row group's XCC_IDs agree,
+// 0 sc1 stores everywhere (gru_seq_bwd16_kernel)
+static int g_gru_l2 = 1;
 
 // Library-held synchronisation words for ppo_gru_seq_fwd (callers that pass their
 // own use ppo_gru_seq_fwd_ws): one buffer {err, counters...} per (device, stream),
@@ -967,10 +987,10 @@ int launch_seq_bwd16(const float* dout, const float* sr, const float* sz, const 
                      const float* shin, const float* masks, const int64_t* idx, const float* whhT, int T, int n,
                      float* dgi, float* dgh, float* dhz, float* carry, int* cnt, int* err, hipStream_t st) {
   const int groups = ceil_div(n, 32);
-  PPO_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)groups * (2 + 32) * sizeof(int), st), "ppo_gru_seq_bwd: counter reset");
+  PPO_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)groups * (3 + 32) * sizeof(int), st), "ppo_gru_seq_bwd: counter reset");
   dim3 grid((unsigned)groups, H / 16);
   gru_seq_bwd16_kernel<H><<<grid, 256, 0, st>>>(dout, sr, sz, sn, sghn, shin, masks, idx, whhT, T, n, dgi, dgh, dhz,
-                                                carry, cnt, err, g_gru_spin);
+                                                carry, cnt, err, g_gru_spin, g_gru_l2);
   PPO_LAUNCH_CHECK("gru_seq_bwd16_kernel");
   return 0;
 }
@@ -1062,9 +1082,11 @@ PPO_API int ppo_gru_variant_get(void) { return g_gru_variant; }
 // which at ~10 us per step kernel were the critical path of the recurrent update.
 // Rows of step t are t*n .. t*n + n - 1; mask of row j at step t: masks[idx[t*n + j]]
 // (idx NULL: masks[t*n + j]).
-// per 32-row group: the step counter, the BPTT's start counter and XCC_ID slots of
-// up to 32 unit blocks (gru_seq_bwd16_kernel's L2 agreement)
-PPO_API int ppo_gru_seq_counters(int n) { return n > 0 ? ceil_div(n, 32) * (2 + 32) : 1; }
+// per 32-row group: the step counter, the BPTT's start counter, XCC_ID slots of up
+// to 32 unit blocks (gru_seq_bwd16_kernel's L2 agreement) and the BPTT's path
+// report; layout [G step counters][G start counters][32 G XCC slots][G paths]
+// with G = ceil(n/32), path 1 = sc1 hand-off, 2 = L2 hand-off, 0 = not run
+PPO_API int ppo_gru_seq_counters(int n) { return n > 0 ? ceil_div(n, 32) * (3 + 32) : 1; }
 
 PPO_API int ppo_gru_seq_fwd_ws(const float* h0, const float* masks, const int64_t* idx, const float* whh,
                                const float* bhh, const float* gi, int T, int n, int H, float* hout, float* save_r,
@@ -1173,6 +1195,15 @@ PPO_API int ppo_gru_persist_set(int v) {
   return 0;
 }
 PPO_API int ppo_gru_persist_get(void) { return g_gru_persist; }
+
+// persistent BPTT's dgh hand-off: 1 L2 path where a row group's XCC_IDs agree
+// (default), 0 sc1 stores for every group
+PPO_API int ppo_gru_l2_set(int v) {
+  PPO_REQUIRE(v == 0 || v == 1, "ppo_gru_l2_set: %d (0 sc1 everywhere, 1 L2 where the XCC_IDs agree)", v);
+  g_gru_l2 = v;
+  return 0;
+}
+PPO_API int ppo_gru_l2_get(void) { return g_gru_l2; }
 
 // bounded-wait length (polls) of the persistent kernels; tests force a timeout with 1
 PPO_API int ppo_gru_persist_spin_set(int polls) {

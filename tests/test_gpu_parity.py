@@ -591,6 +591,80 @@ def test_recurrent_ppo_iteration_runs(gpu):
     assert torch.equal(st.recurrent_hidden_states[0], st.recurrent_hidden_states[-1])
 
 
+def test_recurrent_iteration_replays_reference(gpu):
+    """The reference's recurrent iteration recorded in gru_update.npz (T/ GRU +
+    vector obs, hidden 32, V 14, 8 envs x 16 steps, masks with zeros, a carried
+    initial hidden state; PPO.update over recurrent_generator, E = 2, M = 2)
+    replayed through the drop-in API in host-sampling mode: actions bit-exact,
+    log-probs / values / returns / the carried hidden state within 1e-5, the first
+    minibatch's gradient (BPTT through the masked sequences) within 1e-5 of each
+    tensor's max |g|, every minibatch's losses within 1e-4 relative, the final
+    parameters within 2e-5 (T/a2c_ppo_acktr/storage.py:162-223, model.py:111-166,
+    algo/ppo.py:43-96)."""
+    from a2c_ppo_acktr import model as M
+    from a2c_ppo_acktr.algo import PPO
+    from a2c_ppo_acktr.storage import RolloutStorage
+    from a2c_ppo_acktr.synthetic import Discrete
+    d = golden("gru_update.npz")
+    hidden, V, N, T, E, Mb = (int(x) for x in d["meta"])
+    clip, vcoef, ecoef = (float(x) for x in d["coefs"])
+    torch.set_num_threads(1)
+    torch.manual_seed(31)   # the generator's seed: construction consumes the same draws as the reference's
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase, base_kwargs={"recurrent": True, "hidden_size": hidden},
+                   vector_obs_len=V)
+    _load_flat(pol, d["init_params"])
+    pol.to(gpu)
+    agent = PPO(pol, clip, E, Mb, vcoef, ecoef, lr=float(d["lr"][0]), eps=1e-5, max_grad_norm=0.5)
+    st = RolloutStorage(T, N, (4, 84, 84), [V], Discrete(8), pol.recurrent_hidden_state_size,
+                        obs_dtype=torch.uint8, device=gpu)
+    st.obs.copy_(_dev(d["obs_u8"]))
+    st.vector_obs.copy_(_dev(d["vector_obs"]))
+    st.recurrent_hidden_states[0].copy_(_dev(d["h0"]))
+    st.masks[0].copy_(_dev(d["masks0"]))
+    eng = pol.hip_engine()
+    grads, accs = [], []
+    orig_step = agent.optimizer._step_flat
+
+    def step_capture(e):
+        grads.append(e.grad.clone())          # before clip + Adam (the reference's clip_grad_norm_ input)
+        accs.append(agent._loss_acc[:3].clone())
+        return orig_step(e)
+
+    agent.optimizer._step_flat = step_capture
+    M.set_sampling_mode("host")
+    try:
+        for step in range(T):
+            v, a, lp, h = pol.act(st.obs[step], st.vector_obs[step], st.recurrent_hidden_states[step],
+                                  st.masks[step])
+            st.insert(st.obs[step + 1], st.vector_obs[step + 1], h, a, lp, v, _dev(d["rewards"][step]),
+                      _dev(d["masks"][step]), torch.ones(N, 1, device=gpu))
+        nv = pol.get_value(st.obs[-1], st.vector_obs[-1], st.recurrent_hidden_states[-1], st.masks[-1])
+        st.compute_returns(nv, True, 0.99, 0.95, False)
+        losses = agent.update(st)
+    finally:
+        M.set_sampling_mode("device")
+        agent.optimizer._step_flat = orig_step
+    assert eng is pol.hip_engine()
+    assert np.array_equal(st.actions.cpu().numpy(), d["actions"])
+    np.testing.assert_allclose(st.action_log_probs.cpu().numpy(), d["action_log_probs"], atol=1e-5)
+    np.testing.assert_allclose(st.value_preds[:T].cpu().numpy(), d["values"], atol=1e-5)
+    np.testing.assert_allclose(st.recurrent_hidden_states[-1].cpu().numpy(), d["hidden_T"], atol=1e-5)
+    np.testing.assert_allclose(st.returns.cpu().numpy(), d["returns"], atol=1e-5)
+    assert len(grads) == E * Mb
+    shapes = O.cnn_param_shapes(hidden, recurrent=True, vector_obs_len=V)
+    got, ref = O.unflatten(grads[0].cpu().numpy(), shapes), O.unflatten(d["mb0_preclip_grad"], shapes)
+    for name, _ in shapes:
+        err = np.abs(got[name] - ref[name]).max()
+        assert err <= 1e-5 * max(np.abs(ref[name]).max(), 1e-6), (name, err, np.abs(ref[name]).max())
+    acc = torch.stack(accs + [agent._loss_acc[:3].clone()]).cpu().numpy()
+    # the loss accumulator before each step holds the minibatches up to and including it
+    mb = np.diff(np.concatenate([np.zeros((1, 3)), acc[:-1]], 0), axis=0)
+    np.testing.assert_allclose(mb, d["mb_losses"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(losses, d["losses"], rtol=1e-4, atol=1e-6)
+    final = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).cpu().numpy()
+    np.testing.assert_allclose(final, d["final_params"], rtol=0, atol=2e-5)
+
+
 # ------------------------------------------------------------- MLPBase (c1)
 def _mlp_policy(gpu, I, V, H, A, seed):
     from a2c_ppo_acktr import model as M
@@ -1294,18 +1368,27 @@ def test_gru_persistent_sequence_equals_steps(gpu, T, n, H, use_idx):
                                                           (outs[0][k] != outs[p][k]).sum().item())
 
 
-@pytest.mark.parametrize("T,n,H,use_idx", [(24, 512, 256, True), (9, 37, 64, False), (5, 100, 128, True),
-                                            (3, 16, 512, False), (2, 64, 256, True)])
-def test_gru_persistent_bptt_equals_steps(gpu, T, n, H, use_idx):
+@pytest.mark.parametrize("T,n,H,use_idx,l2", [(24, 512, 256, True, 1), (9, 37, 64, False, 1), (5, 100, 128, True, 1),
+                                               (3, 16, 512, False, 1), (2, 64, 256, True, 1),
+                                               (256, 512, 256, True, 1), (256, 512, 256, True, 0),
+                                               (48, 512, 64, True, 1), (48, 512, 64, True, 0),
+                                               (40, 256, 64, False, 1), (40, 256, 64, False, 0)])
+def test_gru_persistent_bptt_equals_steps(gpu, T, n, H, use_idx, l2):
     """ppo_gru_seq_bwd_ws as one persistent launch (gru_seq_bwd16_kernel: W_hh^T
     slices resident, dgh handed over between the unit blocks of a row group) equals
     the T - 1 step launches bit for bit — dgi and dgh over all T steps, the final
     dhz and carry — with masks direct or through the minibatch index, and the error
-    word stays clear."""
+    word stays clear.  Each dgh hand-off path is run and reported: l2 = 0 forces the
+    sc1 (write-through) stores in every group (the report must say so), l2 = 1 lets a
+    group whose unit blocks agree on one XCC_ID keep dgh in that XCD's L2 (plain
+    stores, sc1 loads) — at c5's shape (T = 256, n = 512, H = 256) and at H = 64 with
+    16 and 8 row groups, where the round-robin dispatch places every group on one
+    XCD, so the L2 path must have run."""
     Hh = _hip()
     g = torch.Generator().manual_seed(T * n + H + 1)
     N = 3 * n
     R = T * n
+    G = (n + 31) // 32
     dout = torch.randn(R, H, generator=g).cuda()
     sv = {"r": torch.rand(R, H, generator=g), "z": torch.rand(R, H, generator=g),
           "n": torch.rand(R, H, generator=g) * 2 - 1, "ghn": torch.randn(R, H, generator=g),
@@ -1319,13 +1402,17 @@ def test_gru_persistent_bptt_equals_steps(gpu, T, n, H, use_idx):
         masks = (torch.rand(R, generator=g) > 0.1).float().cuda()
         idx = None
     cnt = torch.zeros(Hh.call("ppo_gru_seq_counters", n), dtype=torch.int32, device=gpu)
+    assert cnt.numel() == G * (3 + 32)
     err = torch.zeros(1, dtype=torch.int32, device=gpu)
     outs = {}
+    prev, prev_l2 = Hh.call("ppo_gru_persist_get"), Hh.call("ppo_gru_l2_get")
+    paths = None
     for persist in (0, 3):
         o = {"dgi": torch.full((R, 3 * H), float("nan"), device=gpu), "dgh": torch.full((R, 3 * H), float("nan"),
                                                                                        device=gpu),
              "dhz": torch.zeros(n, H, device=gpu), "carry": torch.zeros(n, H, device=gpu)}
         Hh.call("ppo_gru_persist_set", persist)
+        Hh.call("ppo_gru_l2_set", l2)
         try:
             Hh.call("ppo_gru_seq_bwd_ws", dout.data_ptr(), sv["r"].data_ptr(), sv["z"].data_ptr(), sv["n"].data_ptr(),
                     sv["ghn"].data_ptr(), sv["hin"].data_ptr(), masks.data_ptr(),
@@ -1334,9 +1421,20 @@ def test_gru_persistent_bptt_equals_steps(gpu, T, n, H, use_idx):
                     _s())
             torch.cuda.synchronize()
         finally:
-            Hh.call("ppo_gru_persist_set", 1)
+            Hh.call("ppo_gru_persist_set", prev)
+            Hh.call("ppo_gru_l2_set", prev_l2)
         outs[persist] = o
+        if persist == 3 and T > 1 and G * (H // 16) <= torch.cuda.get_device_properties(0).multi_processor_count:
+            paths = cnt[G * (2 + 32):].cpu()
     assert err.item() == 0
+    if paths is not None:
+        print(f"BPTT dgh hand-off paths (l2={l2}, {G} groups): sc1 {(paths == 1).sum().item()} "
+              f"L2 {(paths == 2).sum().item()}")
+        assert ((paths == 1) | (paths == 2)).all(), paths
+        if l2 == 0:
+            assert (paths == 1).all(), paths
+        elif G % 8 == 0:
+            assert (paths == 2).any(), paths
     outs[1] = outs.pop(3)
     for k in outs[0]:
         assert torch.isfinite(outs[1][k]).all(), k
@@ -1371,6 +1469,7 @@ def test_gru_persistent_bptt_timeout_sets_error(gpu):
                 H, dgi.data_ptr(), dgh.data_ptr(), dhz.data_ptr(), carry.data_ptr(), cnt.data_ptr(), err.data_ptr(),
                 _s())
         torch.cuda.synchronize()
+    prev = Hh.call("ppo_gru_persist_get")
     Hh.call("ppo_gru_persist_set", 3)
     Hh.call("ppo_gru_persist_spin_set", 0)
     try:
@@ -1386,7 +1485,7 @@ def test_gru_persistent_bptt_timeout_sets_error(gpu):
     try:
         run()
     finally:
-        Hh.call("ppo_gru_persist_set", 1)
+        Hh.call("ppo_gru_persist_set", prev)
     assert err.item() == 0 and torch.isfinite(dgi).all() and (dgi[: n] != 0).any()
 
 

@@ -72,13 +72,28 @@ def test_half_minibatch_gradient_vs_float64(gpu, obs_dtype):
         print(f"{name:28s} half-mode relative Frobenius error {fro:.2e}", flush=True)
         assert fro <= BF16_TOL, (name, fro)
     np.testing.assert_allclose(loss[:3].cpu().numpy(), losses, rtol=BF16_TOL, atol=1e-4)
+    pol.float()
     if obs_dtype != torch.float16:
+        # back to fp32 on the u8 plane: the engine repacks the fp32 weights, so its
+        # gradient equals, bit for bit, that of a fresh fp32 policy that never ran in
+        # half mode (whose accuracy test_full_size.py holds against float64)
+        torch.manual_seed(4)
+        fresh = M.Policy((4, 84, 84), Discrete(A), base=M.CNNBase, base_kwargs={"recurrent": False, "hidden_size": H})
+        with torch.no_grad():
+            fresh.dist.linear.weight.mul_(30.0)
+        fresh.to(gpu)
+        assert torch.equal(torch.cat([q.detach().reshape(-1) for q in fresh.parameters()]),
+                           torch.cat([q.detach().reshape(-1) for q in pol.parameters()]))
+        cap_back, cap_fresh = _GradCapture(), _GradCapture()
+        eng.train_minibatch(st, adv, idx, HP, loss, cap_back)
+        fresh.hip_engine().train_minibatch(st, adv, idx, HP, loss, cap_fresh)
+        torch.cuda.synchronize()
+        assert torch.equal(cap_back.grad, cap_fresh.grad)
         return
     # back to fp32 arithmetic on the fp16 plane: its rows are widened exactly (fp16 ->
     # fp32) and then take conv1's fp32-row kernels, whose accuracy test_full_size.py
     # holds against independent float64 references at the u8 bar.  Here: the fp16
     # plane gives bit for bit the gradient of an fp32 plane holding the same values.
-    pol.float()
     cap16, cap32 = _GradCapture(), _GradCapture()
     eng.train_minibatch(st, adv, idx, HP, loss, cap16)
     st.obs = st.obs.float()

@@ -93,6 +93,20 @@ def test_policy_construction_matches_reference_init():
                    vector_obs_len=14)
     assert [n for n, _ in pol.named_parameters()] == [str(x) for x in g["names"]]
     assert np.array_equal(torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy(), g["params"])
+    # gru_update.npz: the recurrent policy of the recorded update, and the default
+    # generator's state after construction (the replay's sampling / randperm draws
+    # start from it: tests/test_gpu_parity.py test_recurrent_iteration_replays_reference)
+    u = golden("gru_update.npz")
+    torch.manual_seed(31)
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase, base_kwargs={"recurrent": True, "hidden_size": 32},
+                   vector_obs_len=14)
+    assert np.array_equal(torch.get_rng_state().numpy(), u["rng_after_init"])
+    gw = torch.Generator().manual_seed(32)
+    with torch.no_grad():
+        pol.dist.linear.weight.mul_(40.0)
+        pol.base.gru.bias_ih_l0.copy_(torch.rand(96, generator=gw) * 0.6 - 0.3)
+        pol.base.gru.bias_hh_l0.copy_(torch.rand(96, generator=gw) * 0.6 - 0.3)
+    assert np.array_equal(torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy(), u["init_params"])
     torch.set_num_threads(nt)
 
 

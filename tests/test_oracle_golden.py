@@ -197,3 +197,106 @@ def test_torch_ref_minibatch_grads_match_oracle():
     for (name, _), g in zip(shapes, grads):
         np.testing.assert_allclose(g.numpy(), ref[name], rtol=1e-9, atol=1e-12 * max(1.0, np.abs(ref[name]).max()))
     np.testing.assert_allclose(losses, [lg["value_loss"], lg["action_loss"], lg["entropy"]], rtol=1e-10)
+
+
+def _gru_step_forward(p, obs_u8, vec, h, mask):
+    """The act path of a recurrent CNNBase (model.py:111-115 single-step branch)."""
+    feat, _ = O.cnn_trunk(p, O.decode_obs(obs_u8))
+    x = np.concatenate([feat, np.asarray(vec, np.float64)], 1)
+    h = O.gru_cell(p, x, np.asarray(h, np.float64) * np.asarray(mask, np.float64).reshape(-1, 1))
+    value, logits = O.heads(p, h)
+    return value, logits, h
+
+
+def test_oracle_replays_reference_recurrent_rollout():
+    """gru_update.npz (tools/gen_golden.py gen_gru_update: the reference's own
+    T/ GRU + vector-obs Policy): the oracle's single-step forward replays the
+    rollout — actions bit-exact from the recorded Exp(1) noise, values and
+    log-probs within 1e-6, the carried hidden state within 1e-6."""
+    d = golden("gru_update.npz")
+    hidden, V, N, T, E, Mb = (int(x) for x in d["meta"])
+    shapes = O.cnn_param_shapes(hidden, recurrent=True, vector_obs_len=V)
+    assert [str(n) for n in d["names"]] == [n for n, _ in shapes]
+    p = O.unflatten(d["init_params"], shapes)
+    h = d["h0"].astype(np.float64)
+    masks = np.concatenate([d["masks0"][None], d["masks"]], 0)[..., 0]
+    for t in range(T):
+        value, logits, h = _gru_step_forward(p, d["obs_u8"][t], d["vector_obs"][t], h, masks[t])
+        c = O.categorical(logits, d["exp_noise"][t])
+        assert np.array_equal(c["action"], d["actions"][t][:, 0]), t
+        np.testing.assert_allclose(value, d["values"][t][:, 0], atol=1e-6)
+        np.testing.assert_allclose(c["log_prob"], d["action_log_probs"][t][:, 0], atol=1e-6)
+    np.testing.assert_allclose(h, d["hidden_T"], atol=1e-6)
+    nv, _, _ = _gru_step_forward(p, d["obs_u8"][T], d["vector_obs"][T], h, masks[T])
+    np.testing.assert_allclose(nv, d["next_value"][:, 0], atol=1e-6)
+
+
+def test_oracle_recurrent_update_pinned_to_reference():
+    """The recurrent PPO.update recorded from the reference (recurrent_generator
+    env orders, GRU BPTT over masked sequences, clip_grad_norm_, Adam; E = 2,
+    M = 2): oracle.run_update_recurrent's first-minibatch gradient (BPTT included)
+    equals the reference's within 1e-5 of each tensor's max |g|, every
+    minibatch's (value loss, action loss, entropy) and total norm within 1e-5
+    relative, the last minibatch's gradient within 1e-3 of max |g| (three fp32 vs
+    float64 Adam steps in between move ReLU boundaries of the conv trunk: 2e-4
+    measured on conv2), the final parameters within 2e-5 (4e-7 measured)."""
+    d = golden("gru_update.npz")
+    hidden, V, N, T, E, Mb = (int(x) for x in d["meta"])
+    clip, vcoef, ecoef = (float(x) for x in d["coefs"])
+    shapes = O.cnn_param_shapes(hidden, recurrent=True, vector_obs_len=V)
+    masks = np.concatenate([d["masks0"][None], d["masks"]], 0)[..., 0]
+    r = O.run_update_recurrent(d["init_params"], shapes, d["obs_u8"], d["vector_obs"], d["h0"], masks,
+                               d["actions"][..., 0], d["action_log_probs"][..., 0], d["value_preds_after"][..., 0],
+                               d["returns"][..., 0], d["perms"], num_mini_batch=Mb, clip=clip, value_coef=vcoef,
+                               entropy_coef=ecoef, lr=float(d["lr"][0]))
+    for got, ref, tol in ((r["preclip_grads"][0], d["mb0_preclip_grad"], 1e-5),
+                          (r["preclip_grads"][-1], d["last_preclip_grad"], 1e-3)):
+        g, rf = O.unflatten(got, shapes), O.unflatten(ref, shapes)
+        for name, _ in shapes:
+            err = np.abs(g[name] - rf[name]).max()
+            assert err <= tol * max(np.abs(rf[name]).max(), 1e-6), (name, err, np.abs(rf[name]).max())
+    np.testing.assert_allclose(r["mb_losses"], d["mb_losses"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(r["total_norms"], d["total_norms"], rtol=1e-5)
+    np.testing.assert_allclose(r["losses"], d["losses"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(r["final_params"], d["final_params"], rtol=0, atol=2e-5)
+
+
+def test_oracle_gru_backward_vs_finite_difference():
+    """oracle.gru_backward (the BPTT the GPU kernels are checked against) vs
+    central finite differences of gru_sequence_cache in float64, masks with zeros
+    included: every weight / bias gradient and dx within 1e-6 relative."""
+    rng = np.random.default_rng(17)
+    T, n, I, H = 5, 3, 6, 4
+    p = {"base.gru.weight_ih_l0": rng.standard_normal((3 * H, I)) * 0.5,
+         "base.gru.weight_hh_l0": rng.standard_normal((3 * H, H)) * 0.5,
+         "base.gru.bias_ih_l0": rng.standard_normal(3 * H) * 0.3,
+         "base.gru.bias_hh_l0": rng.standard_normal(3 * H) * 0.3}
+    x = rng.standard_normal((T * n, I))
+    h0 = rng.standard_normal((n, H))
+    masks = (rng.random((T, n)) > 0.3).astype(np.float64)
+    w = rng.standard_normal((T * n, H))     # loss = sum(w * outputs)
+
+    def loss(pp, xx):
+        out, _ = O.gru_sequence_cache(pp, xx, h0, masks)
+        return float((w * out).sum())
+
+    _, cache = O.gru_sequence_cache(p, x, h0, masks)
+    g, dx = O.gru_backward(p, x, masks, cache, w)
+    eps = 1e-6
+    for k in p:
+        fd = np.zeros_like(p[k])
+        for i in np.ndindex(p[k].shape):
+            q = {kk: vv.copy() for kk, vv in p.items()}
+            q[k][i] += eps
+            lp = loss(q, x)
+            q[k][i] -= 2 * eps
+            fd[i] = (lp - loss(q, x)) / (2 * eps)
+        np.testing.assert_allclose(g[k], fd, rtol=1e-6, atol=1e-8, err_msg=k)
+    fdx = np.zeros_like(x)
+    for i in np.ndindex(x.shape):
+        xx = x.copy()
+        xx[i] += eps
+        lp = loss(p, xx)
+        xx[i] -= 2 * eps
+        fdx[i] = (lp - loss(p, xx)) / (2 * eps)
+    np.testing.assert_allclose(dx, fdx, rtol=1e-6, atol=1e-8)

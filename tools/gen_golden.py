@@ -14,7 +14,9 @@ Reference modules used (SURVEY.md §8c "How to import"):
 A stub `<pkg>.envs` module stands in for the gym/baselines-backed envs.py,
 which only provides the VecNormalize type to utils.py.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [name ...]
+      (names: gae advnorm sampler categorical cnn_update adam mlp gru gru_update;
+       none = all)
 """
 import importlib
 import importlib.util
@@ -28,6 +30,11 @@ sys.dont_write_bytecode = True
 os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
 
 import torch  # noqa: E402
+
+# distributions.py patches torch.distributions.Categorical.sample in place
+# (sample = old_sample(self).unsqueeze(-1)); importing a second reference tree
+# would wrap the wrapper, so each load starts from torch's own method
+_TORCH_CAT_SAMPLE = torch.distributions.Categorical.sample
 
 REF_ROOT = "/root/reference"
 B_DIR = f"{REF_ROOT}/ppo-dash-study/001_baseline"
@@ -52,6 +59,7 @@ def load_ref(variant):
         while other in sys.path:
             sys.path.remove(other)
     sys.path.insert(0, ref)
+    torch.distributions.Categorical.sample = _TORCH_CAT_SAMPLE
     stub = types.ModuleType(pkg + ".envs")
     stub.VecNormalize = type("VecNormalize", (), {})
     sys.modules[pkg + ".envs"] = stub
@@ -315,6 +323,130 @@ def gen_gru(S, M, P):
 
 
 # ---------------------------------------------------------------------------
+# (6b) one whole recurrent iteration (T/ GRU + vector obs): rollout (act with the
+#      hidden-state carry, masks with zeros), get_value, compute_returns, then the
+#      reference's own PPO.update over recurrent_generator (storage.py:162-223,
+#      model.py:111-166, algo/ppo.py:43-96): BPTT -> clip_grad_norm_ -> Adam
+# ---------------------------------------------------------------------------
+def gen_gru_update(S, M, P, *, hidden=32, V=14, N=8, T=16, E=2, Mb=2, lr=1e-3, fname="gru_update.npz"):
+    torch.manual_seed(31)
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase,
+                   base_kwargs={"recurrent": True, "hidden_size": hidden}, vector_obs_len=V)
+    # widen the action head and give the GRU non-zero biases so that the policy is
+    # far from uniform (ratio clipping engages in epoch 2) — still the module's own forward
+    gw = torch.Generator().manual_seed(32)
+    with torch.no_grad():
+        pol.dist.linear.weight.mul_(40.0)
+        pol.base.gru.bias_ih_l0.copy_(torch.rand(3 * hidden, generator=gw) * 0.6 - 0.3)
+        pol.base.gru.bias_hh_l0.copy_(torch.rand(3 * hidden, generator=gw) * 0.6 - 0.3)
+    agent = P.PPO(pol, 0.1, E, Mb, 0.5, 0.01, lr=lr, eps=1e-5, max_grad_norm=0.5)
+    st = S.RolloutStorage(T, N, (4, 84, 84), [V], Discrete(8), pol.recurrent_hidden_state_size)
+    init = flat_params(pol)
+    rng_init = torch.get_rng_state().numpy().copy()   # the default generator after construction
+    genv = torch.Generator().manual_seed(321)
+
+    def frame():   # 21x21 random bytes upsampled x4: full 0..255 range, compressible fixture
+        lo = torch.randint(0, 256, (N, 4, 21, 21), dtype=torch.uint8, generator=genv)
+        return lo.repeat_interleave(4, 2).repeat_interleave(4, 3).contiguous()
+
+    obs_u8 = np.zeros((T + 1, N, 4, 84, 84), np.uint8)
+    vec = np.zeros((T + 1, N, V), np.float32)
+    o0 = frame()
+    obs_u8[0] = o0.numpy()
+    st.obs[0].copy_(o0.float() / 255.0)
+    v0 = torch.rand(N, V, generator=genv)
+    vec[0] = v0.numpy()
+    st.vector_obs[0].copy_(v0)
+    h0 = torch.randn(N, hidden, generator=genv) * 0.5        # a mid-training rollout's carried state
+    st.recurrent_hidden_states[0].copy_(h0)
+    m0 = (torch.rand(N, 1, generator=genv) > 0.3).float()     # episodes that ended on the previous step
+    st.masks[0].copy_(m0)
+    noise, values, actions, logps, rewards, masks = [], [], [], [], [], []
+    for step in range(T):
+        with torch.no_grad():
+            rs = torch.get_rng_state()
+            value, action, logp, hxs = pol.act(st.obs[step], st.vector_obs[step],
+                                               st.recurrent_hidden_states[step], st.masks[step])
+            after = torch.get_rng_state()
+            torch.set_rng_state(rs)
+            En = torch.empty(N, 8).exponential_(1)
+            assert torch.equal(torch.get_rng_state(), after)
+        o = frame()
+        vo = torch.rand(N, V, generator=genv)
+        rew = torch.rand(N, 1, generator=genv)
+        done = torch.rand(N, generator=genv) < 0.25
+        mk = torch.FloatTensor([[0.0] if d else [1.0] for d in done])
+        bmk = torch.ones(N, 1)
+        obs_u8[step + 1] = o.numpy()
+        vec[step + 1] = vo.numpy()
+        st.insert(o.float() / 255.0, vo, hxs, action, logp, value, rew, mk, bmk)
+        noise.append(En.numpy()); values.append(value.numpy()); actions.append(action.numpy())
+        logps.append(logp.numpy()); rewards.append(rew.numpy()); masks.append(mk.numpy())
+    hid_T = st.recurrent_hidden_states[-1].numpy().copy()
+    with torch.no_grad():
+        next_value = pol.get_value(st.obs[-1], st.vector_obs[-1], st.recurrent_hidden_states[-1],
+                                   st.masks[-1]).detach()
+    st.compute_returns(next_value, True, 0.99, 0.95, False)
+    returns = st.returns.numpy().copy()
+    vpreds = st.value_preds.numpy().copy()
+
+    # capture: env orders (replayed randperms), per-minibatch losses (the .item()
+    # calls of ppo.py:86-88, on graph tensors only), the pre-clip gradient and total
+    # norm (clip_grad_norm_'s input and result), the clipped gradient (at step())
+    rng_before_update = torch.get_rng_state()
+    items, preclip, norms, clipped = [], [], [], []
+    orig_item = torch.Tensor.item
+
+    def item_wrap(self):
+        v = orig_item(self)
+        if self.requires_grad:
+            items.append(v)
+        return v
+
+    orig_clip = torch.nn.utils.clip_grad_norm_
+
+    def clip_wrap(params, max_norm, *a, **k):
+        params = list(params)
+        preclip.append(np.concatenate([p.grad.reshape(-1).numpy().copy() for p in params]))
+        tn = orig_clip(params, max_norm, *a, **k)
+        norms.append(float(tn))
+        return tn
+
+    orig_step = agent.optimizer.step
+
+    def step_wrap(*a, **k):
+        clipped.append(np.concatenate([p.grad.reshape(-1).numpy().copy() for p in pol.parameters()]))
+        return orig_step(*a, **k)
+
+    agent.optimizer.step = step_wrap
+    torch.Tensor.item = item_wrap
+    torch.nn.utils.clip_grad_norm_ = clip_wrap
+    try:
+        vl, al, ent = agent.update(st)
+    finally:
+        torch.Tensor.item = orig_item
+        torch.nn.utils.clip_grad_norm_ = orig_clip
+    rng_after_update = torch.get_rng_state()
+    torch.set_rng_state(rng_before_update)
+    perms = np.stack([torch.randperm(N).numpy() for _ in range(E)]).astype(np.int64)
+    assert torch.equal(torch.get_rng_state(), rng_after_update)
+    assert len(items) == 3 * E * Mb and len(preclip) == E * Mb == len(clipped)
+    for g, c, tn in zip(preclip, clipped, norms):   # step() saw clip_grad_norm_'s scaling of its input
+        np.testing.assert_allclose(c, g * min(0.5 / (tn + 1e-6), 1.0), rtol=1e-6, atol=1e-12)
+    final = flat_params(pol)
+    save(fname, init_params=init, rng_after_init=rng_init, final_params=final, names=param_names(pol),
+         obs_u8=obs_u8, vector_obs=vec, h0=h0.numpy(), masks0=m0.numpy(), hidden_T=hid_T,
+         exp_noise=np.stack(noise), values=np.stack(values),
+         actions=np.stack(actions).astype(np.int64), action_log_probs=np.stack(logps),
+         rewards=np.stack(rewards), masks=np.stack(masks), next_value=next_value.numpy(),
+         returns=returns, value_preds_after=vpreds, perms=perms,
+         mb_losses=np.array(items, np.float64).reshape(E * Mb, 3),
+         mb0_preclip_grad=preclip[0], last_preclip_grad=preclip[-1], total_norms=np.array(norms),
+         losses=np.array([vl, al, ent]),
+         meta=np.array([hidden, V, N, T, E, Mb]), coefs=np.array([0.1, 0.5, 0.01]), lr=np.array([lr]))
+
+
+# ---------------------------------------------------------------------------
 # (7) clip_grad_norm_ + Adam.step (ppo.py:82-84; torch 2.10 semantics)
 # ---------------------------------------------------------------------------
 def gen_adam():
@@ -361,16 +493,28 @@ def gen_mlp(M, D):
 
 def main():
     torch.set_num_threads(1)  # as T/run.py:55
+    want = set(sys.argv[1:])
+    on = lambda k: not want or k in want  # noqa: E731
     S, M, D, P = load_ref("B")
-    gen_gae(S)
-    gen_advnorm(S, P)
-    gen_sampler(S)
-    gen_categorical(D)
-    gen_cnn_update(S, M, P, hidden=64, N=4, T=4, E=2, Mb=2, lr=1e-3, fname="cnn_update.npz")
-    gen_adam()
-    gen_mlp(M, D)
+    if on("gae"):
+        gen_gae(S)
+    if on("advnorm"):
+        gen_advnorm(S, P)
+    if on("sampler"):
+        gen_sampler(S)
+    if on("categorical"):
+        gen_categorical(D)
+    if on("cnn_update"):
+        gen_cnn_update(S, M, P, hidden=64, N=4, T=4, E=2, Mb=2, lr=1e-3, fname="cnn_update.npz")
+    if on("adam"):
+        gen_adam()
+    if on("mlp"):
+        gen_mlp(M, D)
     S, M, D, P = load_ref("T")
-    gen_gru(S, M, P)
+    if on("gru"):
+        gen_gru(S, M, P)
+    if on("gru_update"):
+        gen_gru_update(S, M, P)
 
 
 if __name__ == "__main__":

@@ -4,7 +4,9 @@ schedule puts its global loads / stores, waits and barriers:
   python tools/kseq.py csrc/gemm.hip mangled_name_substring [--waits]   (in ppo-dash_amd/)
 M mfma, L global/buffer load, S global/buffer store, D LDS-DMA load, r/W ds read/write,
 w s_waitcnt with a vmcnt, | s_barrier; one line per basic block.  --waits lists the
-vmcnt waits with their line in the kernel body."""
+vmcnt waits with their line in the kernel body; --mem prints every global / buffer
+load, store and atomic, poll load, vmcnt wait, barrier, sleep and branch target with
+its line (the order evidence for a hand-off protocol)."""
 import re
 import subprocess
 import sys
@@ -18,6 +20,13 @@ if not m:
     sys.exit(f"no kernel matching {pat}")
 body = asm[m.end():asm.find(".Lfunc_end", m.end())].split("\n")
 print(m.group(1))
+if "--mem" in sys.argv:
+    for i, ln in enumerate(body):
+        t = ln.strip()
+        if (t.startswith(("s_barrier", "buffer_load", "buffer_store", "global_load", "global_store", "global_atomic",
+                          "s_sleep", ".LBB")) or (t.startswith("s_waitcnt") and "vmcnt" in t)):
+            print(f"{i:5d} {t.split(';')[0].rstrip()[:110]}")
+    sys.exit(0)
 out = []
 for i, ln in enumerate(body):
     t = ln.strip().split(" ")[0]
