@@ -137,17 +137,6 @@ CONV_HBM = {
 CONV1_FWD_BYTES_PER_FLOP = 79424.0 / (2.0 * 400 * 32 * 256)
 
 
-def a1split_bytes():
-    """conv1's output leaves as three bf16 planes (a1split.hip): 76,800 B per image
-    written by conv1 and read by conv2's forward and weight gradient instead of the
-    51,200 B fp32 a1 (+ conv1's 1,600 B of mask bits in the training forward)"""
-    global CONV1_FWD_BYTES_PER_FLOP
-    CONV_HBM["conv1_fwd_u8"] = (3276800, 28224 + 76800)
-    CONV_HBM["conv2_fwd"] = (2654208, 76800 + 20736)
-    CONV_HBM["conv2_wgrad"] = (2654208, 20736 + 76800)
-    CONV1_FWD_BYTES_PER_FLOP = (28224 + 76800.0) / (2.0 * 400 * 32 * 256)
-
-
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -581,8 +570,6 @@ def main():
         k, v = kv.split("=")
         _hip.call("ppo_tune_set", k.encode(), int(v))
         tune[k] = int(v)
-    if _hip.call("ppo_a1split_enabled") and args.obs == "u8" and not args.half_precision:
-        a1split_bytes()
     _hip.call("ppo_gru_persist_set", args.gru_persist)
     N, T, E, M = args.envs, args.num_steps, args.ppo_epoch, args.num_mini_batch
     H = args.hidden or (256 if args.recurrent else 512)
@@ -765,7 +752,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if args.half_precision else "f32",
         "split_products": 1 if args.half_precision else args.products,
-        "tune": tune or None, "a1split": bool(_hip.call("ppo_a1split_enabled")) and args.obs == "u8",
+        "tune": tune or None,
         "data": ("synthetic: counter-hash u8 4x84x84 obs" if args.obs == "u8" else
                  "synthetic: counter-hash u8 84x84x3 RGB frames, NormalizeWrapper(synthetic fp32 mean, std 36.31) + "
                  "FrameStackMono(2)") + ", U[0,1) rewards, Bernoulli(0.01) dones; random-init weights",

@@ -185,14 +185,14 @@ int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N,
                           void* stream);
 int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream);
 /* conv3 dgrad with conv2's ReLU mask as bits (from ppo_conv2_fwd_mask): 648 B instead of
- * 20.7 KB read per image; available when ppo_conv3_dgrad_bits_ok() */
+ * 20.7 KB read per image; ppo_conv3_dgrad_bits_ok() is 1 (kept for ABI stability) */
 int ppo_conv3_dgrad_bits_ok(void);
 int ppo_conv3_dgrad_bits(const float* dz3, int B, const float* w3d, const uint64_t* m2bits, float* dz2,
                          void* stream);
 int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const float* a1, float* dz1, void* stream);
 /* conv2 dgrad with conv1's ReLU mask as bits (from ppo_conv1_fwd_mask) instead of
- * the fp32 activations: 1.6 KB instead of 51.2 KB read per image; available when
- * ppo_conv2_dgrad_bits_ok() (the image-resident kernel is selected) */
+ * the fp32 activations: 1.6 KB instead of 51.2 KB read per image;
+ * ppo_conv2_dgrad_bits_ok() is 1 (kept for ABI stability) */
 int ppo_conv2_dgrad_bits_ok(void);
 int ppo_conv2_dgrad_bits(const float* dz2, int B, const float* w2d, const uint32_t* m1bits, float* dz1,
                          void* stream);
@@ -203,36 +203,11 @@ int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, float* slab
 int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, float* slab, float* slab_bias, void* stream);
 int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int K, int Z, float* slab, float* slab_bias,
                      void* stream);
-/* conv1 -> conv2 with conv1's output pre-split (a1split.hip; replaces the a1 hand-off
- * of model.py:177-178 inside ppo_conv1_fwd / ppo_conv2_fwd / ppo_conv2_wgrad): conv1
- * on u8 observations (C = 4) writes a1 = relu(conv1) as three exact bf16 planes
- * a1s [B][4800 units of 16 B] (unit (p, c, rho) = channels 8c..8c+7 of pixel (y, x)
- * in plane p, rho = 100 (2 (y & 1) + (x & 1)) + 10 (y >> 1) + (x >> 1)); conv2's
- * forward stages it by LDS-DMA and its weight gradient without the split.  Results
- * are bit-identical to the fp32-a1 kernels.  fp32 arithmetic only (products 6 / 9):
- * ppo_a1split_enabled() says whether the engine takes this path (tune "a1split"). */
 /* CU-contention probe (probe.hip; diagnostics, not on the training path): `blocks`
  * workgroups that each spin for `ticks` of the 100 MHz s_memrealtime counter and record
  * (start, end) into stamps [blocks][2]; ppo_probe_now writes the counter's current value */
 int ppo_probe_side_kernel(int blocks, int threads, long long ticks, long long* stamps, void* stream);
 int ppo_probe_now(long long* out, void* stream);
-/* timing anatomy of ppo_conv2_fwd_mask's image-resident kernel (wrong results by design): dbg bit 1
- * skips the MFMAs, 2 the staging, 4 the global loads, 8 the epilogue stores */
-int ppo_probe_conv2_fwd_anatomy(int dbg, const float* a1, int B, const float* w2p, const float* b2, float* out,
-                                uint16_t* mbits, void* stream);
-/* timing anatomy of ppo_conv2_wgrad's image-resident kernel (wrong results by design): dbg bit 1 skips
- * the MFMAs, 2 the LDS staging, 4 the global loads; 8 / 16 / 24 schedule experiments (right results:
- * loads over all 12 slots / no start stagger of the odd blocks / both) */
-int ppo_probe_conv2_wgrad_anatomy(int dbg, const float* dz2, const float* a1, int B, int Z, float* slab,
-                                  float* slab_bias, void* stream);
-long long ppo_a1s_bytes(int B);
-int ppo_a1split_enabled(void);
-int ppo_conv1_fwd_split(const uint8_t* obs, const int64_t* idx, long long row0, int B, const float* w1,
-                        const float* b1, uint16_t* a1s, uint32_t* mbits, void* stream);
-int ppo_conv2_fwd_split(const uint16_t* a1s, int B, const float* w2p, const float* b2, float* out, uint64_t* mbits,
-                        void* stream);
-int ppo_conv2_wgrad_split(const float* dz2, const uint16_t* a1s, int B, int Z, float* slab, float* slab_bias,
-                          void* stream);
 /* scale multiplies the weight sums only (conv1 with u8 observations stages the
  * bytes as integers: pass 1/255); bias sums are unscaled */
 int ppo_wgrad_reduce(const float* slab, const float* slab_bias, int Z, int M, int NW, int kind, int a, int b,
@@ -240,9 +215,17 @@ int ppo_wgrad_reduce(const float* slab, const float* slab_bias, int Z, int M, in
 /* deterministic column sums out[c] = scale·Σ_r src[r*ld + c] (split-partial reduces) */
 int ppo_colsum(const float* src, long long ld, int rows, long long cols, float* out, float scale, int accumulate,
                void* stream);
-/* tile-configuration variant of a GEMM family (development A/B knob; 0 = default).
- * key "products": part products per operand pair of the split-bf16 fp32 GEMMs,
- * 6 (default: dropped terms < 2^-26 |a·b|) or 9 (every product exact) */
+/* run-time knobs (A/B and test hooks; each key selects between the default and the
+ * one kept alternative, any other value is refused with PPO_EARG):
+ *   "products"    part products per operand pair of the split-bf16 fp32 GEMMs:
+ *                 6 (default: dropped terms < 2^-26 |a·b|), 9 (every product exact),
+ *                 1 (the half-precision mode's one bf16 product)
+ *   "conv1_fwd"   0 image-resident kernel (default), 9 the generic tile GEMM
+ *   "conv1_wgrad" 8 k-split kernel (default), 5 part-pipelined kernel
+ *   "x9"          1 split-bf16 dense GEMMs (default), 0 fp32 MFMA, 2 split everywhere
+ *   "fc_splitk"   K slices of the rollout-sized fc forward (default 2)
+ *   "rgb_aff"     1 affine-folded raw RGB conv1 (default), 0 bit-exact decode
+ *   "stagger", "small_b", "heads_lds": schedule / small-batch / heads-kernel switches */
 int ppo_tune_set(const char* key, int value);
 /* current value of a tune key (-1 if unknown) */
 int ppo_tune_get(const char* key);

@@ -230,29 +230,13 @@ class CNNEngine:
         output (post-ReLU) to `out` (row stride ldo) or a workspace [B,H]."""
         dev = self.device
         obs, idx = self._obs_f32(obs, idx, B, ws)
-        a1 = None if self._a1_split(obs, B) else ws.get("a1", B * 400 * 32, device=dev)
+        a1 = ws.get("a1", B * 400 * 32, device=dev)
         a2 = ws.get("a2", B * 81 * 64, device=dev)
         a3 = ws.get("a3", B * FEAT, device=dev)
         if out is None:
             out, ldo = ws.get("h", B * self.H, device=dev), self.H
         s = stream()
-        split = self._a1_split(obs, B)
         if ws is self.ws["train"]:
-            self._split_rows = B if split else None
-        if split:
-            # conv1 writes its output as three exact bf16 planes in conv2's stage order
-            # (a1split.hip): conv2 forward stages it by LDS-DMA, its weight gradient
-            # without the split; bit-identical to the fp32 a1 hand-off below
-            a1s = ws.get("a1s", call("ppo_a1s_bytes", B) // 2, dtype=torch.int16, device=dev)
-            train = ws is self.ws["train"]
-            m1 = ws.get("m1bits", B * 400, dtype=torch.int32, device=dev) if train else None
-            m2 = ws.get("m2bits", B * 81, dtype=torch.int64, device=dev) if train else None
-            call("ppo_conv1_fwd_split", obs.data_ptr(), ptr(idx, torch.int64, "idx"), 0, B, self.pv(self.W1),
-                 self.pv(self.B1), a1s.data_ptr(), ptr(m1), s)
-            call("ppo_conv2_fwd_split", a1s.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), ptr(m2), s)
-            if train:
-                self._mask_rows = B
-        elif ws is self.ws["train"]:
             # training forward: conv1 and conv2 also write their ReLU masks as bits,
             # read by the conv2 / conv3 dgrads instead of the fp32 activations
             m1 = ws.get("m1bits", B * 400, dtype=torch.int32, device=dev)
@@ -273,12 +257,6 @@ class CNNEngine:
         else:
             call("ppo_fc_fwd", a3.data_ptr(), B, self.pk(2), self.pv(self.B4), self.H, out.data_ptr(), ldo, s)
         return out
-
-    def _a1_split(self, obs, B):
-        """the pre-split conv1 -> conv2 hand-off (a1split.hip): 4-channel u8 rows, fp32
-        arithmetic (not the half-precision mode), batches above the small-batch path"""
-        return (obs.dtype == torch.uint8 and self.C == 4 and not self._is_rgb(obs)
-                and B > call("ppo_tune_get", b"small_b") and bool(call("ppo_a1split_enabled")))
 
     def _check_obs(self, obs):
         obs = obs if obs.is_cuda else obs.to(self.device)
@@ -346,8 +324,7 @@ class CNNEngine:
     def _trunk_backward(self, B, dh, obs, idx):
         """dh: dL/d(fc pre-activation) [B,H] (ReLU mask applied) -> trunk gradients."""
         ws, dev, s = self.ws["train"], self.device, stream()
-        split = getattr(self, "_split_rows", None) == B   # this minibatch's forward wrote a1s
-        a1 = ws.bufs["a1s"] if split else ws.bufs["a1"]
+        a1 = ws.bufs["a1"]
         a2, a3 = ws.bufs["a2"], ws.bufs["a3"]
         dz3 = ws.get("dz3", B * FEAT, device=dev)
         dz2 = ws.get("dz2", B * 81 * 64, device=dev)
@@ -359,20 +336,18 @@ class CNNEngine:
         # the conv backward on a side stream (_dist.start_bucket); PPO's step waits for it
         _dist.start_bucket(self.grad[self.offsets[self.W4]:])
         bits = getattr(self, "_mask_rows", None) == B   # masks of this minibatch's forward
-        if bits and call("ppo_conv3_dgrad_bits_ok"):
+        if bits:
             call("ppo_conv3_dgrad_bits", dz3.data_ptr(), B, self.pk(4), ws.bufs["m2bits"].data_ptr(), dz2.data_ptr(),
                  s)
         else:
             call("ppo_conv3_dgrad", dz3.data_ptr(), B, self.pk(4), a2.data_ptr(), dz2.data_ptr(), s)
         self._wgrad("conv3", B, dz3, a2, None, s)
-        if bits and call("ppo_conv2_dgrad_bits_ok"):
+        if bits:
             call("ppo_conv2_dgrad_bits", dz2.data_ptr(), B, self.pk(5), ws.bufs["m1bits"].data_ptr(), dz1.data_ptr(),
                  s)
-        elif split:
-            raise RuntimeError("the pre-split a1 path needs the mask-bit conv2 dgrad (tune conv2_dgrad 8)")
         else:
             call("ppo_conv2_dgrad", dz2.data_ptr(), B, self.pk(5), a1.data_ptr(), dz1.data_ptr(), s)
-        self._wgrad("conv2", B, dz2, a1, None, s, a1_split=split)
+        self._wgrad("conv2", B, dz2, a1, None, s)
         if obs.dtype == torch.float16:   # the rows trunk() converted for this minibatch
             obs, idx = ws.bufs["obs32"], None
         self._wgrad("conv1", B, dz1, obs, idx, s)
@@ -397,7 +372,7 @@ class CNNEngine:
         self._trunk_backward(B, dh, storage.obs, idx)
         self._finish_step(optimizer)
 
-    def _wgrad(self, layer, B, dz, x, idx, s, a1_split=False):
+    def _wgrad(self, layer, B, dz, x, idx, s):
         dev = self.device
         ws = self.ws["train"]
         if layer == "conv1":
@@ -425,8 +400,6 @@ class CNNEngine:
         elif layer == "conv1":
             call("ppo_conv1_wgrad", dz.data_ptr(), x.data_ptr(), self._obs_args(x), ptr(idx), 0, self.C, B, Z,
                  slab.data_ptr(), slab_b.data_ptr(), s)
-        elif layer == "conv2" and a1_split:
-            call("ppo_conv2_wgrad_split", dz.data_ptr(), x.data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), s)
         elif layer == "conv2":
             call("ppo_conv2_wgrad", dz.data_ptr(), x.data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), s)
         elif layer == "conv3":

@@ -70,14 +70,6 @@ SIGNATURES = {
     # probe.hip (CU-contention diagnostics)
     "ppo_probe_side_kernel": [c_int, c_int, c_ll, c_p, c_p],
     "ppo_probe_now": [c_p, c_p],
-    "ppo_probe_conv2_fwd_anatomy": [c_int, c_p, c_int, c_p, c_p, c_p, c_p, c_p],
-    "ppo_probe_conv2_wgrad_anatomy": [c_int, c_p, c_p, c_int, c_int, c_p, c_p, c_p],
-    # a1split.hip (conv1 output pre-split for conv2)
-    "ppo_a1s_bytes": [c_int],
-    "ppo_a1split_enabled": [],
-    "ppo_conv1_fwd_split": [c_p, c_p, c_ll, c_int, c_p, c_p, c_p, c_p, c_p],
-    "ppo_conv2_fwd_split": [c_p, c_int, c_p, c_p, c_p, c_p, c_p],
-    "ppo_conv2_wgrad_split": [c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     "ppo_conv3_wgrad": [c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     "ppo_linear_wgrad": [c_p, c_p, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
     "ppo_wgrad_reduce": [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_f, c_int, c_p],
@@ -127,12 +119,11 @@ SIGNATURES = {
     "ppo_clip_adam_guarded": [c_p, c_p, c_p, c_p, c_ll, c_p, c_f, c_d, c_d, c_d, c_d, c_d, c_ll, c_p, c_p, c_p, c_p,
                               c_p],
 }
-_RESTYPES = {"ppo_last_error": ctypes.c_char_p, "ppo_packed_weights_size": c_ll, "ppo_fc_fwd_ws_bytes": c_ll,
-             "ppo_a1s_bytes": c_ll}
+_RESTYPES = {"ppo_last_error": ctypes.c_char_p, "ppo_packed_weights_size": c_ll, "ppo_fc_fwd_ws_bytes": c_ll}
 # functions whose int return value is a result, not a status
 _VALUE_FUNCS = {"ppo_abi_version", "ppo_gae_partials_count", "ppo_gae_scan_partials_count", "ppo_adv_diff_partials_count",
                 "ppo_packed_weights_size", "ppo_fc_fwd_ws_bytes", "ppo_wgrad_splits", "ppo_heads_train_blocks", "ppo_grad_partials_count",
-                "ppo_conv2_dgrad_bits_ok", "ppo_conv3_dgrad_bits_ok", "ppo_tune_get", "ppo_a1split_enabled",
+                "ppo_conv2_dgrad_bits_ok", "ppo_conv3_dgrad_bits_ok", "ppo_tune_get",
                 "ppo_gru_persist_get", "ppo_gru_l2_get", "ppo_gru_persist_timeouts", "ppo_gru_seq_counters"}
 
 _LIB = None

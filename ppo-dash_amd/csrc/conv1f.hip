@@ -1001,12 +1001,8 @@ static int conv1_wgrad_x6_launch(int src, const float* dz1, const void* obs, con
   else { W1(S, 6); }
   if (src == SRC_F32) {
     W2(SRC_F32)
-  } else if (src == SRC_RGB) {
-    W2(SRC_RGB)
-  } else if (np == 1) {   // u8: products are the dz parts against the exact pixels
-    W1(SRC_U8, 1);
   } else {
-    W1(SRC_U8, 6);
+    W2(SRC_RGB)
   }
 #undef W2
 #undef W1
@@ -1032,10 +1028,3 @@ PPO_API int ppo_conv1_wgrad_rgb(const float* dz1, const uint8_t* frames, const i
   return conv1_wgrad_x6_launch(SRC_RGB, dz1, frames, idx, row0, B, mean, stdv, Z, slab, slab_bias, stream);
 }
 
-// u8 4-channel rows through the tr_b16 weight-gradient kernel (ppo_conv1_wgrad
-// with conv1_wgrad tune 6; A/B against the part-pipelined expanded-E kernel);
-// the slab holds integer-pixel sums (reduce with scale 1/255, as the u8 kernels)
-int conv1_wgrad_u8_tr(const float* dz1, const uint8_t* obs, const int64_t* idx, long long row0, int B, int Z,
-                      float* slab, float* slab_bias, void* stream) {
-  return conv1_wgrad_x6_launch(SRC_U8, dz1, obs, idx, row0, B, nullptr, 1.0, Z, slab, slab_bias, stream);
-}

@@ -1,5 +1,5 @@
 // conv1 weight gradient on u8 observations, k-split over waves (round 4;
-// ppo_tune_set("conv1_wgrad", 7)):
+// ppo_tune_set("conv1_wgrad", 8), the default):
 //   dW1[co][(c, ky, kx)] = Σ_images Σ_px dz1[px][co] · u[c][4oy+ky][4ox+kx]
 // (the conv1 backward of CNNBase, T/a2c_ppo_acktr/model.py:177), exact: u8 pixels
 // are exact in bf16 and dz = hi + mid + lo (split_bf16x3), three
@@ -22,9 +22,11 @@
 //     four pixels of an output-row quad are four consecutive elements; the
 //     kx >= 4 half reads them one element later, realigned with two
 //     v_alignbyte (8-B read + 4-B read per quad);
-//   * two E stages (2 x 64,512 B); the next image's u8 rows are loaded into
-//     registers during the current image and converted into the other stage;
-//     one barrier per image.
+//   * two E stages (2 x 64,512 B); the next image's raw u8 bytes arrive by
+//     LDS-DMA into a 28-KB buffer beside them and are converted into the other
+//     stage mid-image (schedule below).  A first form held the next image in
+//     registers (tune 7, 1.674-1.680 ms per c3 minibatch against 1.597; removed
+//     in round 5, see DESIGN.md §6 run records).
 // Output: the split-K slab [Z][32][256] of u8-integer sums (the reduce applies
 // 1/255) and bias partials [Z][32], as every conv1 wgrad variant.
 #include "igemm_x9.h"
@@ -32,187 +34,6 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw_kernel(const float* __restrict__ dz1,
-                                                                const uint8_t* __restrict__ obs,
-                                                                const int64_t* __restrict__ idx, long long row0,
-                                                                int B, float* __restrict__ slab,
-                                                                float* __restrict__ slab_bias) {
-  static_assert(NW == 8, "8 waves");
-  constexpr int C = 4, IMG = 84, IMGB = C * IMG * IMG;   // 28,224 B per u8 image
-  constexpr int XW = 24;                                 // phase-row width (elements, 21 used)
-  constexpr int ROWE = 4 * XW;                           // elements per input row (4 phases)
-  constexpr int EST = C * IMG * ROWE;                    // elements per stage (32,256)
-  constexpr int NITEM = C * IMG * 6, IPER = (NITEM + NW * 64 - 1) / (NW * 64);   // 16-B u8 items: 2016, 4 / thread
-  __shared__ __attribute__((aligned(16))) uint16_t E[2 * EST];   // 129,024 B
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
-  const int G = gridDim.x;
-  // B-fragment lane constants: column n = 32 tt + l32 -> (c = tt >> 1, ky = 4 (tt & 1) + (l32 >> 3), kx = l32 & 7)
-  const int kx = l32 & 7, dxl = kx & 3, sh = 2 * (kx >> 2);   // alignbyte shift: 0 or 2 bytes
-  const int lbase = ((l32 >> 3) * 4 + dxl) * XW;              // + tile offset + 384 oy + 4 Q
-  // u8 staging items: item = tid + 512 j -> row r = item / 6 (c = r / 84, y = r % 84), X group g6 = item % 6
-  int isrc[IPER], idst[IPER];
-#pragma unroll
-  for (int j = 0; j < IPER; ++j) {
-    const int it = min(tid + NW * 64 * j, NITEM - 1), r = it / 6, g6 = it - 6 * r;
-    isrc[j] = r * IMG + 16 * g6;          // byte offset in the image (4-B aligned)
-    idst[j] = r * ROWE + 4 * g6;          // element offset in a stage (+ dx * XW)
-  }
-  const bool ion3 = tid + NW * 64 * (IPER - 1) < NITEM;
-  u32x4_t stg[IPER];
-  auto fetch = [&](int b) {   // range-checked: the last row's last group reads past the image as zeros
-    const auto rs = make_rsrc(obs + obs_row(idx, row0, b) * (long long)IMGB, IMGB);
-#pragma unroll
-    for (int j = 0; j < IPER; ++j)   // 4-B aligned rows (84 B): dword loads
-#pragma unroll
-      for (int k = 0; k < 4; ++k) stg[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, isrc[j] + 4 * k, 0, 0);
-  };
-  auto put = [&](int st) {   // u8 -> bf16 (exact), de-interleaved by x mod 4
-    uint16_t* S = E + st * EST;
-#pragma unroll
-    for (int j = 0; j < IPER; ++j) {
-      if (j == IPER - 1 && !ion3) break;
-      const u32x4_t w = stg[j];
-#pragma unroll
-      for (int dx = 0; dx < 4; ++dx) {
-        float f[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) f[k] = (float)((w[k] >> (8 * dx)) & 255u);
-        const uint2 q = {__builtin_amdgcn_perm(__float_as_uint(f[1]), __float_as_uint(f[0]), 0x07060302u),
-                         __builtin_amdgcn_perm(__float_as_uint(f[3]), __float_as_uint(f[2]), 0x07060302u)};
-        *reinterpret_cast<uint2*>(S + idst[j] + dx * XW) = q;
-      }
-    }
-  };
-  f32x16 acc[8];
-#pragma unroll
-  for (int t = 0; t < 8; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  float bacc = 0.f;
-  // the k-steps of one image this wave computes: s = wave, wave + 8, wave + 16 (all tiles) and
-  // k-step 24 for tile `wave` only; dz of k-step s for this lane: pixels 16 s + 8 h .. +7, channel l32
-  // one dz_load = DZ_LOADS single-dword buffer loads (128 B apart, so never merged);
-  // the vmcnt of barrier Y below counts them
-  constexpr int DZ_LOADS = 8;
-  auto dz_load = [&](int b, int s, float (&d)[DZ_LOADS]) {
-    const auto rs = make_rsrc(dz1 + (size_t)b * 12800, 12800 * 4);
-    const int o = ((16 * s + 8 * h) * 32 + l32) * 4;
-#pragma unroll
-    for (int j = 0; j < DZ_LOADS; ++j) d[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, o + 128 * j, 0, 0));
-  };
-  // B fragment of tile tt for quads (oy0, Q0), (oy1, Q1) of k-step s: 8 bf16
-  auto bfrag = [&](const uint16_t* S, int tt, int q0off, int q1off) {
-    const int toff = ((tt >> 1) * IMG + 4 * (tt & 1)) * ROWE + lbase;
-    bf16x8 r;
-    uint32_t o[4];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const uint16_t* p = S + toff + (k ? q1off : q0off);
-      const uint2 d01 = *reinterpret_cast<const uint2*>(p);
-      const uint32_t d2 = *reinterpret_cast<const uint32_t*>(p + 4);
-      o[2 * k] = __builtin_amdgcn_alignbyte(d01.y, d01.x, sh);
-      o[2 * k + 1] = __builtin_amdgcn_alignbyte(d2, d01.y, sh);
-    }
-    r = __builtin_bit_cast(bf16x8, uint4{o[0], o[1], o[2], o[3]});
-    return r;
-  };
-  auto qoff = [&](int q) { const int oy = q / 5; return 4 * oy * ROWE + 4 * (q - 5 * oy); };
-  // one k-step: tiles [t0, t1) of k-step s on stage S with the dz values d
-  auto kstep = [&](const uint16_t* S, int s, const float (&d)[8], int t0, int t1) {
-    Frag3 a;
-    split8(f32x4{d[0], d[1], d[2], d[3]}, f32x4{d[4], d[5], d[6], d[7]}, a, false);
-    const int q0 = 4 * s + 2 * h, o0 = qoff(q0), o1 = qoff(q0 + 1);
-#pragma unroll
-    for (int tt = 0; tt < 8; ++tt) {
-      if (tt < t0 || tt >= t1) continue;
-      const bf16x8 bq = bfrag(S, tt, o0, o1);
-      acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, bq, acc[tt], 0, 0, 0);
-      acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, bq, acc[tt], 0, 0, 0);
-      acc[tt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, bq, acc[tt], 0, 0, 0);
-    }
-  };
-  int b = blockIdx.x, cur = 0;
-  if (b < B) {
-    fetch(b);
-    put(0);
-    if (b + G < B) fetch(b + G);
-  }
-  __syncthreads();
-  float d[8], dn[8];
-  if (b < B) dz_load(b, wave, d);
-  for (; b < B; b += G) {
-    const uint16_t* S = E + cur * EST;
-    const bool nxt = b + G < B;
-    // k-step wave (all tiles); next: wave + 8
-    dz_load(b, wave + 8, dn);
-    kstep(S, wave, d, 0, 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bacc += d[j];
-    if (nxt) put(cur ^ 1);                  // image b + G into the other stage (its last reader: image b - G)
-    if (b + 2 * G < B) fetch(b + 2 * G);
-    dz_load(b, wave + 16, d);
-    kstep(S, wave + 8, dn, 0, 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bacc += dn[j];
-    dz_load(b, 24, dn);
-    kstep(S, wave + 16, d, 0, 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bacc += d[j];
-    if (nxt) dz_load(b + G, wave, d);
-    kstep(S, 24, dn, wave, wave + 1);     // k-step 24: tile `wave` (its bias share: wave 0)
-    if (wave == 0) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bacc += dn[j];
-    }
-    lds_barrier();   // stage cur consumed; stage cur ^ 1 complete
-    cur ^= 1;
-  }
-  __syncthreads();
-  // fixed-order sum of the eight waves' partials through the (free) stages, four
-  // tiles at a time (4 waves x 4 tiles x 16 x 64 floats = 64 KB): round 1 waves
-  // 4-7 -> 0-3, round 2 waves 2-3 -> 0-1, round 3 wave 1 -> 0
-  float* X = reinterpret_cast<float*>(E);
-#pragma unroll
-  for (int half = 4; half >= 1; half >>= 1)
-#pragma unroll
-    for (int t0 = 0; t0 < 8; t0 += 4) {
-      if (wave >= half && wave < 2 * half) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) X[(((wave - half) * 4 + t) * 16 + r) * 64 + lane] = acc[t0 + t][r];
-      }
-      __syncthreads();
-      if (wave < half) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[t0 + t][r] += X[((wave * 4 + t) * 16 + r) * 64 + lane];
-      }
-      __syncthreads();
-    }
-  float* out = slab + (size_t)blockIdx.x * 32 * 256;
-  if (wave == 0) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = (r & 3) + 8 * (r >> 2) + 4 * h, n = 32 * t + l32;
-        out[co * 256 + n] = acc[t][r];
-      }
-  }
-  // bias: lane (l32, h) of wave w holds channel l32's sums over its pixels
-  X[tid] = bacc;
-  __syncthreads();
-  if (tid < 32) {
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) t += X[w * 64 + tid] + X[w * 64 + 32 + tid];
-    slab_bias[(size_t)blockIdx.x * 32 + tid] = t;
-  }
-}
 
 // One 1-KB LDS-DMA piece (inline asm: invisible to the compiler's waitcnt pass,
 // retired by the explicit / in-order vmcnt waits described at the use).
@@ -416,16 +237,15 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw2_kernel(const float* _
 }  // namespace
 
 // conv1 weight gradient of u8 observations (C = 4) with the k-split kernel: slab [Z][32][256]
-// (integer-scaled: reduce with 1/255) and bias partials [Z][32]; called by ppo_conv1_wgrad (tune 7)
+// (integer-scaled: reduce with 1/255) and bias partials [Z][32]; called by ppo_conv1_wgrad (tune 8)
 int conv1_wgrad_kw(const float* dz1, const uint8_t* obs, const int64_t* idx, long long row0, int B, int Z,
-                   float* slab, float* slab_bias, int variant, void* stream) {
+                   float* slab, float* slab_bias, void* stream) {
   if (B <= 0 || Z <= 0) return 0;
   hipStream_t st = as_stream(stream);
   int slot;
   const bool prof = ppo_prof_begin("conv1_wgrad_u8", st, &slot);
-  if (variant == 8) conv1_wgrad_kw2_kernel<8><<<Z, 512, 0, st>>>(dz1, obs, idx, row0, B, slab, slab_bias);
-  else conv1_wgrad_kw_kernel<8><<<Z, 512, 0, st>>>(dz1, obs, idx, row0, B, slab, slab_bias);
+  conv1_wgrad_kw2_kernel<8><<<Z, 512, 0, st>>>(dz1, obs, idx, row0, B, slab, slab_bias);
   if (prof) ppo_prof_end(slot, st, 2.0 * B * 400 * 32 * 256);
-  PPO_LAUNCH_CHECK("conv1_wgrad_kw_kernel");
+  PPO_LAUNCH_CHECK("conv1_wgrad_kw2_kernel");
   return 0;
 }

@@ -61,92 +61,6 @@ struct Conv1Fwd : C_ {
   }
 };
 
-// conv1 forward, image-resident (u8 observations, C = 4).  One persistent
-// block of 8 waves per CU walks image pairs with two LDS stages of 2 x 28,224 B:
-// while the waves compute the pair in one stage, LDS-DMA loads (gathered by
-// the minibatch index) fill the other, so HBM latency never meets the MFMAs.
-// Wave w computes image (w >> 2), output channels 16 * ((w >> 1) & 1) + [0, 16),
-// row tiles {w & 1, (w & 1) + 2, ...} of 16 output pixels, with
-// v_mfma_f32_16x16x4_f32 fed straight from the image: a lane's im2col fragment
-// is one 4-byte LDS read (4 adjacent kx); the wave's weight fragments stay in
-// registers.  k order inside a 16-deep group: MFMA s takes k = 16q + 4g + s
-// from lane group g = lane >> 4.  No per-k-step staging and no barrier in the
-// k loop.
-template <int C>
-__global__ __launch_bounds__(512) void conv1_fwd_img_kernel(const uint8_t* __restrict__ obs,
-                                                            const int64_t* __restrict__ idx, long long row0, int B,
-                                                            const float* __restrict__ w,
-                                                            const float* __restrict__ bias, float* __restrict__ out) {
-  constexpr int IMGB = C * IMG2, CH = IMGB / 16, K = C * 64, NQ = K / 16, NT = 13;
-  static_assert(IMGB % 16 == 0, "16-B chunks");
-  __shared__ __attribute__((aligned(16))) uint8_t img[2][2 * IMGB];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int npairs = (B + 1) / 2;
-  const int im = wave >> 2, ct = (wave >> 1) & 1, half = wave & 1;
-  const int ntile = half ? 12 : 13;   // row tiles half, half + 2, ... < 25
-  const int i16 = lane & 15, g = lane >> 4;
-  const float* wp = w + (size_t)(ct * 16 + i16) * K + 4 * g;
-  const int col = ct * 16 + i16;
-  const float bv = bias[col];
-  f32x4 wreg[NQ];   // this wave's 16 x K weight fragments, resident for the block's lifetime
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) wreg[q] = *reinterpret_cast<const f32x4*>(wp + 16 * q);
-  auto fetch = [&](int pair, uint8_t* dst) {   // LDS-DMA: 64 lanes x 16 B contiguous per instruction
-    const int b0 = 2 * pair, n = B - b0 < 2 ? B - b0 : 2;
-    const uint8_t* s0 = obs + obs_row(idx, row0, b0) * (long long)IMGB;
-    const uint8_t* s1 = n > 1 ? obs + obs_row(idx, row0, b0 + 1) * (long long)IMGB : s0;
-    for (int c0 = wave * 64; c0 < n * CH; c0 += 512) {
-      const int c = c0 + lane;
-      if (c < n * CH) {
-        const uint8_t* src = c < CH ? s0 + 16 * c : s1 + 16 * (c - CH);
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
-                                         (__attribute__((address_space(3))) void*)(dst + 16 * c0), 16, 0, 0);
-      }
-    }
-  };
-  int pair = blockIdx.x, cur = 0;
-  if (pair < npairs) fetch(pair, img[0]);
-  __syncthreads();
-  for (; pair < npairs; pair += gridDim.x) {
-    const int nxt = pair + gridDim.x;
-    if (nxt < npairs) fetch(nxt, img[cur ^ 1]);
-    const int b0 = 2 * pair, nimg = B - b0 < 2 ? B - b0 : 2;
-    if (im < nimg) {   // wave-uniform
-      const uint8_t* I = img[cur] + im * IMGB;
-      f32x4 acc[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = zero4();
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const f32x4 bf = wreg[q];
-        const int k16 = 16 * q + 4 * g;
-        const uint8_t* Iq = I + (k16 >> 6) * IMG2 + ((k16 >> 3) & 7) * IMG + (k16 & 7);
-        f32x4 a[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const int row = (half + 2 * t) * 16 + i16, oy = row / 20, ox = row - oy * 20;
-          a[t] = t < ntile ? to_f32x4(*reinterpret_cast<const uint32_t*>(Iq + oy * (4 * IMG) + ox * 4)) : zero4();
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int t = 0; t < NT; ++t)
-            if (t < ntile) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][s], bf[s], acc[t], 0, 0, 0);
-      }
-      float* o = out + (size_t)(b0 + im) * (400 * 32) + col;
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-        if (t < ntile) {
-          const int rt = half + 2 * t;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[(rt * 16 + 4 * g + r) * 32] = fmaxf(acc[t][r] * (1.0f / 255.0f) + bv, 0.f);
-        }
-    }
-    __syncthreads();   // the next stage has landed; every wave is done with this one
-    cur ^= 1;
-  }
-}
-
 // conv1 forward on the bf16 matrix cores, exact (u8 observations, C = 4).
 // A pixel u in 0..255 is exact in bf16 and W = W_hi + W_mid + W_lo exactly
 // (split_bf16x3), so conv1 = Σ u·W_hi + Σ u·W_mid + Σ u·W_lo where every
@@ -587,109 +501,14 @@ __global__ __launch_bounds__(256) void relu_bits_kernel(const float* __restrict_
   }
 }
 
-// NHWC conv (conv2, conv3): k = (ky, kx, ci), weights packed [COUT][K]
-template <int HIN, int CIN, int KS, int ST, int HOUT, int COUT, class C_>
-struct ConvFwd : C_ {
-  static constexpr int K = KS * KS * CIN, P = HOUT * HOUT;
-  const float* in; const float* w; const float* bias; float* out; int M;
-  using ACtx = typename C_::ACtx;
-  using BCtx = typename C_::BCtx;
-  __device__ ACtx a_ctx(int m, int) const {
-    if (m >= M) return {in, 0, 0, false};
-    const int b = m / P, pp = m - b * P, oy = pp / HOUT, ox = pp - oy * HOUT;
-    return {in + ((size_t)(b * HIN + ST * oy) * HIN + ST * ox) * CIN, 0, 0, true};
-  }
-  __device__ f32x4 a_load(const ACtx& c, int k) const {
-    if (!c.ok) return zero4();
-    const int ky = k / (KS * CIN), rem = k - ky * (KS * CIN), kx = rem / CIN, ci = rem - kx * CIN;
-    return *reinterpret_cast<const f32x4*>(c.p + (ky * HIN + kx) * CIN + ci);
-  }
-  __device__ BCtx b_ctx(int n, int) const { return {w + (size_t)n * K, 0, n < COUT}; }
-  __device__ f32x4 b_load(const BCtx& c, int k) const {
-    return c.ok ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
-  }
-  __device__ void k_range(int, int& b, int& e) const { b = 0; e = K; }
-  __device__ void store(int m, int n, int, float v) const {
-    if (m < M && n < COUT) out[(size_t)m * COUT + n] = fmaxf(v + bias[n], 0.f);
-  }
-};
-
 // ---------------------------------------------------------------------------
-// Input-gradient (dgrad) problems; epilogue applies the ReLU mask of the
-// layer below (threshold_backward: pass where the saved output is > 0).
+// Image-resident conv2 / conv3 kernels on the bf16 matrix cores (exact split,
+// DESIGN.md §3): forward, input gradient (the epilogue applies the ReLU mask of
+// the layer below, threshold_backward: pass where the saved output is > 0) and
+// weight gradient.
 // ---------------------------------------------------------------------------
-// stride-1 conv dgrad (conv3): m = (b, y, x) input pixel, n = ci,
-// k = (ky, kx, co): dy[b][y-ky][x-kx][co] (0 outside), wd packed [CIN][K]
-template <int HIN, int CIN, int KS, int HOUT, int COUT, class C_>
-struct ConvDgradS1 : C_ {
-  static constexpr int K = KS * KS * COUT, PIN = HIN * HIN;
-  const float* dy; const float* wd; const float* act; float* dx; int M;
-  struct ACtx { const float* p; int y; int x; bool ok; };
-  using BCtx = typename C_::BCtx;
-  __device__ ACtx a_ctx(int m, int) const {
-    if (m >= M) return {dy, 0, 0, false};
-    const int b = m / PIN, pp = m - b * PIN, y = pp / HIN, x = pp - y * HIN;
-    return {dy + (size_t)b * HOUT * HOUT * COUT, y, x, true};
-  }
-  __device__ f32x4 a_load(const ACtx& c, int k) const {
-    const int ky = k / (KS * COUT), rem = k - ky * (KS * COUT), kx = rem / COUT, co = rem - kx * COUT;
-    const int oy = c.y - ky, ox = c.x - kx;
-    if (!c.ok || oy < 0 || oy >= HOUT || ox < 0 || ox >= HOUT) return zero4();
-    return *reinterpret_cast<const f32x4*>(c.p + (oy * HOUT + ox) * COUT + co);
-  }
-  __device__ BCtx b_ctx(int n, int) const { return {wd + (size_t)n * K, 0, n < CIN}; }
-  __device__ f32x4 b_load(const BCtx& c, int k) const {
-    return c.ok ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
-  }
-  __device__ void k_range(int, int& b, int& e) const { b = 0; e = K; }
-  __device__ void store(int m, int n, int, float v) const {
-    if (m < M && n < CIN) {
-      const size_t i = (size_t)m * CIN + n;
-      dx[i] = act[i] > 0.f ? v : 0.f;
-    }
-  }
-};
-
-// conv2 dgrad (4x4 stride 2, 20x20 <- 9x9), the four output-pixel phases
-// (py, px) = (y&1, x&1) merged into one GEMM: every phase of the 2x2 pixel
-// block (yy, xx) reads the same dy taps (oy, ox) = (yy-ty, xx-tx) and differs
-// only in its weights (ky = py+2ty), so m = (b, yy, xx), k = (ty, tx, co) and
-// n = (phase, ci) with wd packed [4 phases][CIN][4*COUT] = [128][256] —
-// a 128-wide B operand instead of four 32-wide passes over the same A rows.
-template <class C_>
-struct Conv2Dgrad : C_ {
-  using BCtx = typename C_::BCtx;
-  static constexpr int HIN = 20, CIN = 32, HOUT = 9, COUT = 64, K = 4 * COUT, PPH = 100, N = 4 * CIN;
-  const float* dy; const float* wd; const float* act; float* dx; int M;  // M = B*100
-  struct ACtx { const float* p; int yy; int xx; bool ok; };
-  __device__ ACtx a_ctx(int m, int) const {
-    if (m >= M) return {dy, 0, 0, false};
-    const int b = m / PPH, pp = m - b * PPH, yy = pp / 10, xx = pp - yy * 10;
-    return {dy + (size_t)b * HOUT * HOUT * COUT, yy, xx, true};
-  }
-  __device__ f32x4 a_load(const ACtx& c, int k) const {
-    const int ty = k >> 7, tx = (k >> 6) & 1, co = k & 63;
-    const int oy = c.yy - ty, ox = c.xx - tx;
-    if (!c.ok || oy < 0 || oy >= HOUT || ox < 0 || ox >= HOUT) return zero4();
-    return *reinterpret_cast<const f32x4*>(c.p + (oy * HOUT + ox) * COUT + co);
-  }
-  __device__ BCtx b_ctx(int n, int) const { return {wd + (size_t)n * K, 0, n < N}; }
-  __device__ f32x4 b_load(const BCtx& c, int k) const {
-    return c.ok ? *reinterpret_cast<const f32x4*>(c.p + k) : zero4();
-  }
-  __device__ void k_range(int, int& b, int& e) const { b = 0; e = K; }
-  __device__ void store(int m, int n, int, float v) const {
-    if (m < M && n < N) {
-      const int b = m / PPH, pp = m - b * PPH, yy = pp / 10, xx = pp - yy * 10, ph = n >> 5;
-      const int y = 2 * yy + (ph >> 1), x = 2 * xx + (ph & 1);
-      const size_t i = ((size_t)(b * HIN + y) * HIN + x) * CIN + (n & 31);
-      dx[i] = act[i] > 0.f ? v : 0.f;
-    }
-  }
-};
-
 // conv2 forward, image-resident on the bf16 matrix cores (exact split, DESIGN.md
-// §3), two LDS stages (ppo_tune_set("conv2_fwd", 12), default): a2[b][m][co] =
+// §3), two LDS stages: a2[b][m][co] =
 // relu(b2[co] + Σ_k im2col(a1)[m][k] W2p[co][k]), m = (oy, ox), k = (ky, kx, ci).
 // One persistent block (8 waves) per CU walks images.  Wave w: n tile w & 3 (16
 // co), taps 8 (w >> 2) .. +7 (ky rows 0-1 / 2-3), its weight fragments
@@ -714,8 +533,9 @@ struct Conv2Dgrad : C_ {
 //     registers one unit per k-step (1-4), each once its register has been staged.
 //   * Epilogue in the swapped MFMA orientation (weights as A): one 16-B store of
 //     four consecutive channels per tile, dummy rows dropped by buffer range.
-// DBG (timing anatomy only, ppo_probe_conv2_fwd_anatomy; wrong results): 1 skips
-// the MFMAs, 2 the staging (split + ds_write), 4 the global loads, 8 the epilogue stores
+// DBG (timing anatomy of a diagnostic build only — the library instantiates DBG = 0;
+// wrong results): 1 skips the MFMAs, 2 the staging (split + ds_write), 4 the global
+// loads, 8 the epilogue stores (profiles/r04_c2f_anatomy_kbench.log)
 template <int NP, bool MASK = false, int DBG = 0>
 __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restrict__ a1, int B,
                                                            const uint16_t* __restrict__ wpl,
@@ -919,8 +739,8 @@ __device__ __forceinline__ int c2w_pix(int r) {
   return r < 72 ? (r >> 3) * 9 + (r & 7) : (r - 72) * 9 + 8;
 }
 
-// DBG (timing anatomy only, ppo_probe_conv2_wgrad_anatomy; wrong results): 1 skips
-// the MFMAs, 2 the LDS staging (split + ds_write), 4 the global loads; schedule
+// DBG (timing anatomy of a diagnostic build only — the library instantiates DBG = 0;
+// wrong results): 1 skips the MFMAs, 2 the LDS staging (split + ds_write), 4 the global loads; schedule
 // experiments (right results): 8 spreads the 8 load parts over all 12 slots, 16
 // starts every block at once (no s_sleep stagger of the odd blocks)
 template <int NP, int DBG = 0>
@@ -1859,23 +1679,6 @@ struct Conv1Wgrad : WgradBase<C_> {
   }
 };
 
-// NHWC conv wgrad (conv2, conv3): kk = (ky, kx, ci)
-template <int HIN, int CIN, int KS, int ST, int HOUT, class C_>
-struct ConvWgrad : WgradBase<C_> {
-  static constexpr int K = KS * KS * CIN, P = HOUT * HOUT;
-  const float* in;
-  struct BCtx { int off; bool ok; };
-  __device__ BCtx b_ctx(int n, int) const {
-    const int ky = n / (KS * CIN), rem = n - ky * (KS * CIN), kx = rem / CIN, ci = rem - kx * CIN;
-    return {(ky * HIN + kx) * CIN + ci, n < K};
-  }
-  __device__ f32x4 b_load(const BCtx& c, int r) const {
-    if (!c.ok || r >= this->R) return zero4();
-    const int b = r / P, pp = r - b * P, oy = pp / HOUT, ox = pp - oy * HOUT;
-    return *reinterpret_cast<const f32x4*>(in + ((size_t)(b * HIN + ST * oy) * HIN + ST * ox) * CIN + c.off);
-  }
-};
-
 // Pack torch-layout weights into the loaders' k orders (once per optimizer step).
 //   W2p [64][512]  (ky,kx,ci)       W3p [32][576] (ky,kx,ci)
 //   W4p [H][1568]  (p,c)            W4T [1568][H] (p,c) x n
@@ -1933,10 +1736,8 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
   }
 }
 
-using CfgN32 = Cfg<256, 32, 4, 1, true, true>;
 using CfgN64 = Cfg<128, 64, 2, 2, true, true>;
 using CfgN128 = Cfg<128, 128, 2, 2, true, true>;
-using CfgN64s = Cfg<256, 64, 4, 1, true, true>;
 
 }  // namespace
 
@@ -1977,26 +1778,37 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 }
 
 // ---------------------------------------------------------------------------
-// Tile-configuration variants (A/B knobs for tools/kbench.py; defaults are the
-// measured best on MI355X).  ppo_tune_set("conv1_fwd", v) etc.
+// Run-time knobs (ppo_tune_set / ppo_tune_get).  Each selects between the default
+// kernel and one kept alternative that a test or a documented A/B depends on;
+// the superseded variants of rounds 1-4 live in git history, not in the library.
+//   conv1_fwd    0: image-resident bf16x3 kernel (u8, C = 4); 9: the generic tile GEMM
+//                (the path any other C takes), for A/B and its parity test
+//   conv1_wgrad  8: k-split kernel, u8 image by LDS-DMA (conv1w.hip, default);
+//                5: part-pipelined kernel (the half-precision mode's, bf16 dz)
+//   x9           1: fp32 GEMMs on the bf16 matrix cores (exact split, igemm_x9.h) where
+//                they measured faster; 0: fp32 MFMA (igemm.h); 2: the split core everywhere
+//   fc_splitk    K slices of the rollout-sized fc forward with a workspace (<= 1: unsplit)
+//   rgb_aff      1: conv1 on raw RGB frames by the affine fold (rgbaff.hip); 0: bit-exact decode
 // ---------------------------------------------------------------------------
-enum { TK_CONV1_FWD, TK_CONV3_FWD, TK_CONV2_DGRAD, TK_CONV3_DGRAD, TK_CONV1_WGRAD, TK_FC_FWD, TK_CONV2_FWD, TK_X9,
-       TK_CONV2_WGRAD, TK_CONV3_WGRAD, TK_FC_DGRAD, TK_FC_WGRAD, TK_ORDER, TK_FC_SPLITK, TK_A1SPLIT, TK_RGB_AFF, TK_N };
-static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv3_fwd", "conv2_dgrad", "conv3_dgrad", "conv1_wgrad",
-                                         "fc_fwd", "conv2_fwd", "x9", "conv2_wgrad", "conv3_wgrad", "fc_dgrad", "fc_wgrad",
-                                         "order", "fc_splitk", "a1split", "rgb_aff"};
-// x9: 1 = fp32 GEMMs on the bf16 matrix cores with exact 3-way operand splits (igemm_x9.h), 0 = fp32 MFMA
+enum { TK_CONV1_FWD, TK_CONV1_WGRAD, TK_X9, TK_FC_SPLITK, TK_RGB_AFF, TK_N };
+static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv1_wgrad", "x9", "fc_splitk", "rgb_aff"};
+static int g_tune[TK_N] = {0, 8, 1, 2, 1};
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
 static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measured best
 // small_b: forwards of at most this many samples (images / linear rows) take the
 // small-batch path of small.hip (an output element per thread or wave, fp32 FMA)
 static int g_small_b = 4;
-// order: fc tile order override for A/B (0: per-layer default, 1: m fastest, 2: n fastest; igemm_x9.h tile_of;
-// 3: the default order with the fc weight gradient's scalar epilogue, for A/B)
-// fc_splitk: K slices of the rollout-sized fc forward with a workspace (ppo_fc_fwd_ws; <= 1: unsplit)
-// a1split: conv1 writes its output pre-split for conv2 (a1split.hip; 1 on, 0 the fp32 a1 hand-off)
-static int g_tune[TK_N] = {0, 8, 8, 8, 8, 0, 12, 1, 8, 8, 0, 0, 0, 2, 0, 1};  // fc_fwd 0: tile by M (x9 path)  // measured best (kbench sweep, profiles/)
+
+static bool tune_ok(int k, int v) {
+  switch (k) {
+    case TK_CONV1_FWD: return v == 0 || v == 9;
+    case TK_CONV1_WGRAD: return v == 5 || v == 8;
+    case TK_X9: return v >= 0 && v <= 2;
+    case TK_FC_SPLITK: return v >= 0 && v <= 8;
+    default: return v == 0 || v == 1;
+  }
+}
 
 int heads_lds_knob(int set, int value);   // heads.hip (the LDS-weight heads_train kernel, default on)
 
@@ -2021,6 +1833,7 @@ PPO_API int ppo_tune_set(const char* key, int value) {
   }
   for (int i = 0; i < TK_N; ++i)
     if (strcmp(key, g_tune_names[i]) == 0) {
+      PPO_REQUIRE(tune_ok(i, value), "ppo_tune_set: %s = %d is not a kept variant", key, value);
       g_tune[i] = value;
       return 0;
     }
@@ -2038,44 +1851,20 @@ PPO_API int ppo_tune_get(const char* key) {
   return -1;
 }
 
-// fp32-MFMA tile core (x9 = 0 and the generic fallbacks): one tile shape per
-// problem class, the measured best of the round-1 sweep
-// (profiles/r01_kbench_sweep_v2.log); the other shapes were removed.
-// N = 32 output-channel problems (conv1/conv3 fwd, conv2 dgrad)
+// fp32-MFMA tile core (x9 = 0 and the generic fallbacks): the measured best tile
+// of the round-1 sweep (profiles/r01_kbench_sweep_v2.log) for the N = 32 problem
 using V32_0 = Cfg<256, 32, 4, 1, true, true>;           // 4 waves x 64 rows, 46 KB LDS
-// N = 64 problems (conv2 fwd, conv3 dgrad)
-using V64_0 = Cfg<128, 64, 2, 2, true, true>;
-
-#define PPO_VARIANTS32(TEMPL, SETUP, M, N, Z, NAME, FLOPS) \
-  { TEMPL(V32_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }
-
-// N = 128 problems (conv2 dgrad, phases merged)
-using V128_0 = Cfg<128, 128, 2, 2, true, true>;           // 2x2 waves of 64x64, 32 KB
-
-#define PPO_VARIANTS128(TEMPL, SETUP, M, N, Z, NAME, FLOPS) \
-  { TEMPL(V128_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }
 
 // exact-split bf16 core (igemm_x9.h)
-using X32 = CfgX<128, 32, 4, 1, true, true>;          // N = 32: waves of 32x32
 using X64 = CfgX<128, 64, 2, 2, true, true>;          // N = 64: waves of 64x32
 using X128 = CfgX<128, 128, 2, 2, true, true>;        // N >= 128: waves of 64x64
-using XW32 = CfgX<32, 128, 1, 4, false, false, true>;   // wgrad, 32 output channels
 using XW64 = CfgX<64, 128, 2, 2, false, false, true>;   // wgrad, 64 output channels
-using XW128 = CfgX<128, 128, 2, 2, false, false, true>; // wgrad, >= 128 output channels
-using XW256x128 = CfgX<256, 128, 4, 2, false, false, true>; // 8 waves of 64x64
-using XP32 = CfgX<128, 32, 4, 1, true, true, false, false, false, true>;    // B from planes, waves 32x32
-using XP64 = CfgX<128, 64, 4, 1, true, true, false, false, false, true>;    // waves 32x64
-using XP128 = CfgX<128, 128, 4, 1, true, true, false, false, false, true>;  // waves 32x128
+using XP128 = CfgX<128, 128, 4, 1, true, true, false, false, false, true>;  // B from planes, waves 32x128
 using XP128w8 = CfgX<128, 128, 8, 1, true, true, false, false, false, true>;      // 8 waves of 16x128
 using XP128x64w8 = CfgX<128, 64, 8, 1, true, true, false, false, false, true>;    // 8 waves of 16x64 (2 blocks/CU)
-// split-at-staging forms (igemm_x9s_kernel): operands split once per block into bf16 planes in LDS
-using SP128 = CfgS<128, 128, 4, 2, true, true, false, true>;     // 8 waves of 32x64, B planes (96 KB LDS)
-using SP256 = CfgS<256, 128, 4, 2, true, true, false, true>;     // 8 waves of 64x64, B planes (144 KB LDS)
-using SP128x64 = CfgS<128, 64, 4, 2, true, true, false, true>;   // 8 waves of 32x32, B planes (72 KB LDS)
+// split-at-staging form (igemm_x9s_kernel): both operands split once per block into bf16 planes in LDS
 using SW256x128 = CfgS<256, 128, 4, 2, false, false, true>;      // wgrad: 8 waves of 64x64 (144 KB LDS)
-using SW128 = CfgS<128, 128, 2, 2, false, false, true>;          // wgrad: 4 waves of 64x64 (96 KB LDS)
-// x9 = 1: the split-bf16 core where it measured faster (forward GEMMs, fc dgrad); the gather-heavy
-// conv dgrads and the wgrads stay on fp32 MFMA (their split path is VALU-bound); x9 = 2: everywhere
+
 // compute units of the current device (persistent-kernel grid size)
 static int device_cus() {
   static int n_cu = 0;
@@ -2089,11 +1878,8 @@ static int device_cus() {
   return n_cu;
 }
 
-// accessors for the kernels in other translation units (a1split.hip)
-int gemm_products() { return g_products; }
-int gemm_device_cus() { return device_cus(); }
-PPO_API int ppo_a1split_enabled() { return g_tune[TK_A1SPLIT] != 0 && g_products != 1 ? 1 : 0; }
-
+// x9 = 1: the split-bf16 core where it measured faster (the dense forward / dgrad, the
+// fc weight gradient); x9 = 2: also the narrow GRU / MLP weight gradients; 0: fp32 MFMA
 static inline bool use_x9() { return g_tune[TK_X9] != 0; }
 static inline bool use_x9_all() { return g_tune[TK_X9] == 2; }
 template <class P>
@@ -2101,21 +1887,16 @@ static inline void set_planes(P& p, const float* seg, long long n, int rows, int
   p.bpl = planes_of(seg, n); p.bps = n; p.bld = K; p.bnr = rows;
 }
 
-// fp32-MFMA core (x9 = 0): fc forward (N multiple of 128), conv2 forward (N = 64)
-#define PPO_VARIANTS_FC(TEMPL, SETUP, M, N, Z, NAME, FLOPS) \
-  { TEMPL(CfgN128) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }
-#define PPO_VARIANTS_C2F(TEMPL, SETUP, M, N, Z, NAME, FLOPS) \
-  { TEMPL(V64_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }
-
-#define PPO_VARIANTS64(TEMPL, SETUP, M, N, Z, NAME, FLOPS) \
-  { TEMPL(V64_0) p; SETUP; return launch(p, M, N, Z, as_stream(stream), NAME, FLOPS); }
+// persistent image-resident grid: one block per CU (fewer for a small batch)
+static inline unsigned img_grid(int B) {
+  const int n_cu = device_cus();
+  return (unsigned)(B < n_cu ? B : n_cu);
+}
 
 static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
                           const float* w1, const float* b1, float* out, uint16_t* mbits, void* stream);
-int conv1_wgrad_u8_tr(const float* dz1, const uint8_t* obs, const int64_t* idx, long long row0, int B, int Z,
-                      float* slab, float* slab_bias, void* stream);   // conv1f.hip
 int conv1_wgrad_kw(const float* dz1, const uint8_t* obs, const int64_t* idx, long long row0, int B, int Z,
-                   float* slab, float* slab_bias, int variant, void* stream);   // conv1w.hip
+                   float* slab, float* slab_bias, void* stream);   // conv1w.hip
 
 // conv1 forward: out [B][20][20][32] = relu(conv(obs rows, W1 torch layout) + b1)
 PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
@@ -2137,11 +1918,12 @@ static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, lo
   if (!mbits && B > 0 && B <= g_small_b)
     return small_conv1_fwd(obs, obs_is_u8, idx, row0, C, B, w1, b1, out, as_stream(stream));
   // float observations (the reference's fp32 storage plane): the image-resident
-  // split-bf16 kernel of conv1f.hip (tune 7: the fp32-MFMA tile GEMM, for A/B)
-  if (!obs_is_u8 && C == 4 && g_tune[TK_CONV1_FWD] != 7 && ((uintptr_t)obs & 15) == 0)
+  // split-bf16 kernel of conv1f.hip
+  if (!obs_is_u8 && C == 4 && ((uintptr_t)obs & 15) == 0)
     return ppo_conv1_fwd_f32((const float*)obs, idx, row0, B, w1, b1, out, reinterpret_cast<uint32_t*>(mbits), stream);
-  if (mbits && !(obs_is_u8 && C == 4 && g_tune[TK_CONV1_FWD] != 9 && g_tune[TK_CONV1_FWD] != 8)) {
-    // paths without the fused mask epilogue: the conv, then the mask from its output
+  const bool img = obs_is_u8 && C == 4 && g_tune[TK_CONV1_FWD] == 0;
+  if (mbits && !img) {
+    // the generic path has no fused mask epilogue: the conv, then the mask from its output
     const int rc = conv1_fwd_impl(obs, obs_is_u8, idx, row0, C, B, w1, b1, out, nullptr, stream);
     if (rc != 0 || B == 0) return rc;
     const long long halves = (long long)B * 800;
@@ -2151,49 +1933,56 @@ static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, lo
     return 0;
   }
   const long long M = (long long)B * 400;
-  const int tk = TK_CONV1_FWD;
   const double fl = 2.0 * M * 32 * C * 64;
-#define SETUP1(T_)                                                                                 \
-  p.obs = (const T_*)obs; p.idx = idx; p.row0 = row0; p.C = C; p.M = (int)M; p.w = w1; p.bias = b1; p.out = out
-  if (obs_is_u8 && C == 4 && g_tune[tk] != 9) {
+  if (img) {
     if (B == 0) return 0;
-    const int n_cu = device_cus();
-    const int npairs = (B + 1) / 2;
-    const unsigned blocks = (unsigned)(npairs < n_cu ? npairs : n_cu);   // persistent, one per CU
+    const unsigned nb = img_grid(B);
     int slot;
     const bool prof = ppo_prof_begin("conv1_fwd_u8", as_stream(stream), &slot);
-    if (g_tune[tk] == 8) {
-      conv1_fwd_img_kernel<4><<<blocks, 512, 0, as_stream(stream)>>>((const uint8_t*)obs, idx, row0, B, w1, b1, out);
+    const uint8_t* o8 = (const uint8_t*)obs;
+    hipStream_t st = as_stream(stream);
+    if (g_products == 1) {   // half-precision mode: bf16 weights
+      if (mbits) conv1_fwd_bf16x3_kernel<4, true, 1><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, mbits);
+      else conv1_fwd_bf16x3_kernel<4, false, 1><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, nullptr);
+    } else if (mbits) {
+      conv1_fwd_bf16x3_kernel<4, true><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, mbits);
     } else {
-      const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
-      const uint8_t* o8 = (const uint8_t*)obs;
-      hipStream_t st = as_stream(stream);
-      if (g_products == 1) {   // half-precision mode: bf16 weights
-        if (mbits) conv1_fwd_bf16x3_kernel<4, true, 1><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, mbits);
-        else conv1_fwd_bf16x3_kernel<4, false, 1><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, nullptr);
-      } else if (mbits) {
-        conv1_fwd_bf16x3_kernel<4, true><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, mbits);
-      } else {
-        conv1_fwd_bf16x3_kernel<4, false><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, nullptr);
-      }
+      conv1_fwd_bf16x3_kernel<4, false><<<nb, 512, 0, st>>>(o8, idx, row0, B, w1, b1, out, nullptr);
     }
-    if (prof) ppo_prof_end(slot, as_stream(stream), fl);
+    if (prof) ppo_prof_end(slot, st, fl);
     PPO_LAUNCH_CHECK("conv1_fwd_u8 (image-resident)");
     return 0;
   }
+#define SETUP1(T_)                                                                                 \
+  p.obs = (const T_*)obs; p.idx = idx; p.row0 = row0; p.C = C; p.M = (int)M; p.w = w1; p.bias = b1; p.out = out
   if (obs_is_u8) {
-#define T1(C_) Conv1Fwd<uint8_t, C_>
-    PPO_VARIANTS32(T1, SETUP1(uint8_t), M, 32, 1, "conv1_fwd_u8", fl)
-#undef T1
+    Conv1Fwd<uint8_t, V32_0> p;
+    SETUP1(uint8_t);
+    return launch(p, M, 32, 1, as_stream(stream), "conv1_fwd_u8", fl);
   }
-#define T1(C_) Conv1Fwd<float, C_>
-  PPO_VARIANTS32(T1, SETUP1(float), M, 32, 1, "conv1_fwd_f32", fl)
-#undef T1
+  Conv1Fwd<float, V32_0> p;
+  SETUP1(float);
+  return launch(p, M, 32, 1, as_stream(stream), "conv1_fwd_f32", fl);
 #undef SETUP1
 }
 
 static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float* b2, float* out, uint16_t* mbits,
-                          void* stream);
+                          void* stream) {
+  if (!mbits && B > 0 && B <= g_small_b) return small_conv2_fwd(a1, B, w2p, b2, out, as_stream(stream));
+  if (B <= 0) return 0;
+  const unsigned nb = img_grid(B);
+  int slot;
+  const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
+  const uint16_t* wpl = planes_of(w2p, 64 * 512);
+  hipStream_t st = as_stream(stream);
+  if (mbits && g_products == 9) conv2_fwd_x9c_kernel<9, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+  else if (mbits && g_products == 1) conv2_fwd_x9c_kernel<1, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+  else if (mbits) conv2_fwd_x9c_kernel<6, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+  else PPO_LAUNCH_NP(conv2_fwd_x9c_kernel, nb, 512, st, a1, B, wpl, b2, out, nullptr);
+  if (prof) ppo_prof_end(slot, st, 2.0 * B * 81 * 64 * 512);
+  PPO_LAUNCH_CHECK("conv2_fwd_x9c_kernel");
+  return 0;
+}
 
 PPO_API int ppo_conv2_fwd(const float* a1, int B, const float* w2p, const float* b2, float* out, void* stream) {
   return conv2_fwd_impl(a1, B, w2p, b2, out, nullptr, stream);
@@ -2207,76 +1996,17 @@ PPO_API int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const f
   return conv2_fwd_impl(a1, B, w2p, b2, out, reinterpret_cast<uint16_t*>(mbits), stream);
 }
 
-static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float* b2, float* out, uint16_t* mbits,
-                          void* stream) {
-  if (!mbits && B > 0 && B <= g_small_b) return small_conv2_fwd(a1, B, w2p, b2, out, as_stream(stream));
-  if (mbits && g_tune[TK_CONV2_FWD] != 12) {   // no fused mask epilogue
-    const int rc = conv2_fwd_impl(a1, B, w2p, b2, out, nullptr, stream);
-    if (rc != 0 || B <= 0) return rc;
-    const long long halves = (long long)B * 81 * 4;
-    const long long nb = (halves + 255) / 256;
-    relu_bits_kernel<<<(unsigned)(nb < 8192 ? nb : 8192), 256, 0, as_stream(stream)>>>(out, halves, mbits);
-    PPO_LAUNCH_CHECK("relu_bits_kernel");
-    return 0;
-  }
-  if (g_tune[TK_CONV2_FWD] == 12) {   // two LDS stages, staging inside the k-steps
-    if (B <= 0) return 0;
-    const int n_cu = device_cus();
-    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
-    int slot;
-    const bool prof = ppo_prof_begin("conv2_fwd", as_stream(stream), &slot);
-    const uint16_t* wpl = planes_of(w2p, 64 * 512);
-    hipStream_t st = as_stream(stream);
-    if (mbits && g_products == 9) conv2_fwd_x9c_kernel<9, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
-    else if (mbits && g_products == 1) conv2_fwd_x9c_kernel<1, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
-    else if (mbits) conv2_fwd_x9c_kernel<6, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
-    else PPO_LAUNCH_NP(conv2_fwd_x9c_kernel, nb, 512, st, a1, B, wpl, b2, out, nullptr);
-    if (prof) ppo_prof_end(slot, st, 2.0 * B * 81 * 64 * 512);
-    PPO_LAUNCH_CHECK("conv2_fwd_x9c_kernel");
-    return 0;
-  }
-  if (use_x9()) {
-    ConvFwd<20, 32, 4, 2, 9, 64, XP64> p;
-    p.in = a1; p.w = w2p; p.bias = b2; p.out = out; p.M = B * 81;
-    set_planes(p, w2p, 64 * 512, 64, 512);
-    return launch_x9(p, (long long)B * 81, 64, 1, as_stream(stream), "conv2_fwd", 2.0 * B * 81 * 64 * 512);
-  }
-#define T2(C_) ConvFwd<20, 32, 4, 2, 9, 64, C_>
-  PPO_VARIANTS_C2F(T2, (p.in = a1, p.w = w2p, p.bias = b2, p.out = out, p.M = B * 81), (long long)B * 81, 64, 1,
-                   "conv2_fwd", 2.0 * B * 81 * 64 * 512)
-#undef T2
-}
-
 PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream) {
   if (B > 0 && B <= g_small_b) return small_conv3_fwd(a2, B, w3p, b3, out, as_stream(stream));
-  if (g_tune[TK_CONV3_FWD] == 8) {
-    if (B <= 0) return 0;
-    const int n_cu = device_cus();
-    const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
-    int slot;
-    const bool prof = ppo_prof_begin("conv3_fwd", as_stream(stream), &slot);
-    PPO_LAUNCH_NP(conv3_fwd_x9_kernel, nb, 512, as_stream(stream), a2, B, planes_of(w3p, 32 * 576), b3, out,
-                  g_stagger);
-    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
-    PPO_LAUNCH_CHECK("conv3_fwd_x9_kernel");
-    return 0;
-  }
-  if (use_x9()) {
-    ConvFwd<9, 64, 3, 1, 7, 32, XP32> p;
-    p.in = a2; p.w = w3p; p.bias = b3; p.out = out; p.M = B * 49;
-    set_planes(p, w3p, 32 * 576, 32, 576);
-    return launch_x9(p, (long long)B * 49, 32, 1, as_stream(stream), "conv3_fwd", 2.0 * B * 49 * 32 * 576);
-  }
-#define T3(C_) ConvFwd<9, 64, 3, 1, 7, 32, C_>
-  PPO_VARIANTS32(T3, (p.in = a2, p.w = w3p, p.bias = b3, p.out = out, p.M = B * 49), (long long)B * 49, 32, 1,
-                 "conv3_fwd", 2.0 * B * 49 * 32 * 576)
-#undef T3
+  if (B <= 0) return 0;
+  int slot;
+  const bool prof = ppo_prof_begin("conv3_fwd", as_stream(stream), &slot);
+  PPO_LAUNCH_NP(conv3_fwd_x9_kernel, img_grid(B), 512, as_stream(stream), a2, B, planes_of(w3p, 32 * 576), b3, out,
+                g_stagger);
+  if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
+  PPO_LAUNCH_CHECK("conv3_fwd_x9_kernel");
+  return 0;
 }
-
-#include "dense_x32.h"
-
-// tile order of an fc GEMM launch: the layer's measured default unless the "order" knob overrides it
-static int fc_order(int dflt) { return g_tune[TK_ORDER] == 1 || g_tune[TK_ORDER] == 2 ? g_tune[TK_ORDER] - 1 : dflt; }
 
 // CNNBase fc (model.py:181): out[m * ldo + n] = relu(x [M][1568] · W4p [H][1568]^T + b), W4p the packed
 // segment of ppo_pack_weights (its bf16 planes follow it)
@@ -2285,35 +2015,23 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
   PPO_REQUIRE(H > 0 && H % 8 == 0 && ldo >= H, "ppo_fc_fwd: H=%d ldo=%d", H, ldo);
   const int K = 1568;
   if (M > 0 && M <= g_small_b) return small_linear_fwd(x, nullptr, M, K, K, w4p, b, H, out, ldo, 1, as_stream(stream));
-  if (use_x9() && (g_tune[TK_FC_FWD] >= 6 && g_tune[TK_FC_FWD] <= 8) && ldo % 4 == 0) {   // dense_x32.h
-    DenseX32Args a{};
-    a.wpl = planes_of(w4p, (long long)H * K); a.wps = (long long)H * K;
-    a.x = x; a.ldx = K; a.out = out; a.ldo = ldo; a.bias = b; a.M = M; a.N = H; a.K = K;
-    return dense_x32_launch<DX_BIAS_RELU>(a, as_stream(stream), "fc_fwd", g_tune[TK_FC_FWD] - 6);
-  }
   if (use_x9()) {
-    // rollout-sized M (4096 rows) fills a quarter of the chip with 128 x 128
-    // tiles: narrower tiles there (fc_fwd tune: 0 auto, 1 128x128, 5 8 waves of 16x64)
-    int v = g_tune[TK_FC_FWD];
-    if (v == 0) {
-      const long long t128 = ((M + 127LL) / 128) * ((H + 127) / 128);
-      v = t128 >= 2LL * device_cus() ? 1 : 5;   // measured at M = 4096: 8 waves of 16x64 0.060 ms, 128x64 0.070
-    }
+    // tiles dealt n-fastest per XCD (igemm_x9.h tile_of); rollout-sized M (4096 rows)
+    // fills a quarter of the chip with 128 x 128 tiles: 8 waves of 16 x 64 there
+    // (0.060 vs 0.070 ms for 128 x 64)
+    const bool wide = ((M + 127LL) / 128) * ((H + 127) / 128) >= 2LL * device_cus();
 #define PPO_FC(CFG)                                                                                  \
   {                                                                                                  \
     DenseReluFwd<CFG> p;                                                                             \
     p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1; \
     set_planes(p, w4p, (long long)H * K, H, K);                                                      \
-    p.n_fast = fc_order(1);                                                                          \
-    p.vec = g_tune[TK_FC_FWD] != 1 && H % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)out & 15) == 0 &&   \
+    p.n_fast = 1;                                                                                    \
+    p.vec = H % 4 == 0 && ldo % 4 == 0 && ((uintptr_t)out & 15) == 0 &&                              \
             (b == nullptr || ((uintptr_t)b & 15) == 0);                                              \
     return launch_x9(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);                      \
   }
-    if (v == 5) PPO_FC(XP128x64w8)
-    if (v == 10) PPO_FC(SP128)      // split-at-staging forms: 0.69 / 0.62 / 0.70 vs 0.58 ms (slower)
-    if (v == 11) PPO_FC(SP256)
-    if (v == 12) PPO_FC(SP128x64)
-    PPO_FC(XP128)
+    if (wide) PPO_FC(XP128)
+    PPO_FC(XP128x64w8)
 #undef PPO_FC
   }
   DenseReluFwd<CfgN128> p;
@@ -2372,12 +2090,12 @@ PPO_API int ppo_fc_fwd_ws(const float* x, int M, const float* w4p, const float* 
   if (!use_x9() || need == 0 || ws == nullptr || ws_bytes < need || ldo % 4 != 0 || H % 4 != 0 ||
       ((uintptr_t)out & 15) != 0 || ((uintptr_t)ws & 15) != 0 || ((uintptr_t)b & 15) != 0)
     return ppo_fc_fwd(x, M, w4p, b, H, out, ldo, stream);
-  const int K = 1568, Z = g_tune[TK_FC_SPLITK];
+  const int K = 1568, Z = (int)(need / (4LL * M * H));
   hipStream_t st = as_stream(stream);
   DenseFwdSplitK<XP128x64w8> p;
   p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1;
   set_planes(p, w4p, (long long)H * K, H, K);
-  p.n_fast = fc_order(1);
+  p.n_fast = 1;
   p.slab = ws;
   p.chunk = ((K + Z - 1) / Z + 31) / 32 * 32;
   int rc = launch_x9(p, M, H, Z, st, "fc_fwd", 2.0 * M * H * K);
@@ -2400,10 +2118,9 @@ PPO_API int ppo_linear_relu_fwd(const float* x, int M, int K, const float* w, co
     return launch_x9(p, M, N, 1, as_stream(stream), "linear_relu_fwd", 2.0 * M * N * K);
   }
   if (N % 128 == 0) {
-#define TF(C_) DenseReluFwd<C_>
-    PPO_VARIANTS_FC(TF, (p.x = x, p.w = w, p.bias = b, p.out = out, p.M = M, p.N = N, p.K = K), M, N, 1,
-                    "linear_relu_fwd", 2.0 * M * N * K)
-#undef TF
+    DenseReluFwd<CfgN128> p;
+    p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K;
+    return launch(p, M, N, 1, as_stream(stream), "linear_relu_fwd", 2.0 * M * N * K);
   }
   DenseReluFwd<CfgN64> p;
   p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K;
@@ -2427,7 +2144,7 @@ PPO_API int ppo_linear_fwd_ex(const float* x, const int64_t* idx, int M, int K, 
     DenseReluFwd<X128> p;
     p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = act;
     p.idx = idx;
-    p.vec = g_tune[TK_FC_FWD] != 1 && N % 4 == 0 && (ldo ? ldo : N) % 4 == 0 && ((uintptr_t)out & 15) == 0 &&
+    p.vec = N % 4 == 0 && (ldo ? ldo : N) % 4 == 0 && ((uintptr_t)out & 15) == 0 &&
             (b == nullptr || ((uintptr_t)b & 15) == 0);
     return launch_x9(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);
   }
@@ -2451,7 +2168,7 @@ PPO_API int ppo_linear_dgrad_ex(const float* dy, int M, int K, const float* wt, 
   if (use_x9()) {
     DenseDgradMask<X128> p;
     p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K; p.ldact = ldact; p.mode = mode;
-    p.vec = g_tune[TK_FC_DGRAD] != 1 && N % 4 == 0 && (ldact ? ldact : N) % 4 == 0 && ((uintptr_t)dx & 15) == 0 &&
+    p.vec = N % 4 == 0 && (ldact ? ldact : N) % 4 == 0 && ((uintptr_t)dx & 15) == 0 &&
             (act == nullptr || ((uintptr_t)act & 15) == 0);
     return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_ex", 2.0 * M * N * K);
   }
@@ -2482,28 +2199,14 @@ PPO_API int ppo_transpose(const float* src, int rows, int cols, float* dst, void
 PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
                                   void* stream) {
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 4", K);
-  if (use_x9() && (g_tune[TK_FC_DGRAD] >= 6 && g_tune[TK_FC_DGRAD] <= 8) && K % 32 == 0 && N % 4 == 0) {
-    DenseX32Args a{};
-    a.wpl = planes_of(wt, (long long)N * K); a.wps = (long long)N * K;
-    a.x = dy; a.ldx = K; a.out = dx; a.ldo = N; a.act = act; a.ldact = N; a.M = M; a.N = N; a.K = K;
-    return dense_x32_launch<DX_MASK>(a, as_stream(stream), "linear_dgrad_mask", g_tune[TK_FC_DGRAD] - 6);
-  }
-  if (use_x9()) {   // wt = the packed W4T segment [1568][H] (planes follow)
-    PPO_REQUIRE(K % 8 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 8", K);
-#define PPO_FCD(CFG)                                                                \
-  {                                                                                 \
-    DenseDgradMask<CFG> p;                                                          \
-    p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;        \
-    set_planes(p, wt, (long long)N * K, N, K);                                      \
-    p.n_fast = fc_order(0);                                                         \
-    p.vec = g_tune[TK_FC_DGRAD] != 1 && N % 4 == 0 && ((uintptr_t)dx & 15) == 0 &&  \
-            (act == nullptr || ((uintptr_t)act & 15) == 0);                         \
-    return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K); \
-  }
-    if (g_tune[TK_FC_DGRAD] == 10) PPO_FCD(SP128)   // split-at-staging: 1.06 / 1.00 vs 0.74 ms (slower)
-    if (g_tune[TK_FC_DGRAD] == 11) PPO_FCD(SP256)
-    PPO_FCD(XP128w8)   // measured: 0.75 vs 0.87 ms (XP128) at the c3 minibatch
-#undef PPO_FCD
+  if (use_x9()) {   // wt = the packed W4T segment [1568][H] (planes follow); 8 waves of 16 x 128:
+    PPO_REQUIRE(K % 8 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 8", K);   // 0.75 vs 0.87 ms (4 waves)
+    DenseDgradMask<XP128w8> p;
+    p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;
+    set_planes(p, wt, (long long)N * K, N, K);
+    p.n_fast = 0;   // m fastest: the 134 MB dy fits the Infinity Cache, the weight tile stays L2-resident
+    p.vec = N % 4 == 0 && ((uintptr_t)dx & 15) == 0 && (act == nullptr || ((uintptr_t)act & 15) == 0);
+    return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);
   }
   DenseDgradMask<CfgN128> p;
   p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;
@@ -2513,8 +2216,7 @@ PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt
 template <bool BITS>
 static int conv3_dgrad_img(const float* dz3, int B, const float* w3d, const float* mask, float* dz2, void* stream) {
   if (B <= 0) return 0;
-  const int n_cu = device_cus();
-  const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+  const unsigned nb = img_grid(B);
   int slot;
   const bool prof = ppo_prof_begin("conv3_dgrad", as_stream(stream), &slot);
   const uint16_t* wpl = planes_of(w3d, 64 * 288);
@@ -2526,70 +2228,44 @@ static int conv3_dgrad_img(const float* dz3, int B, const float* w3d, const floa
   return 0;
 }
 
-// conv3 dgrad with conv2's ReLU mask as bits (m2bits [B][81] u64 from
-// ppo_conv2_fwd_mask); the image-resident kernel only (ppo_conv3_dgrad_bits_ok).
-PPO_API int ppo_conv3_dgrad_bits_ok() { return g_tune[TK_CONV3_DGRAD] == 8 ? 1 : 0; }
+// conv3 dgrad with conv2's ReLU mask as bits (m2bits [B][81] u64 from ppo_conv2_fwd_mask)
+PPO_API int ppo_conv3_dgrad_bits_ok() { return 1; }
 PPO_API int ppo_conv3_dgrad_bits(const float* dz3, int B, const float* w3d, const uint64_t* m2bits, float* dz2,
                                  void* stream) {
-  PPO_REQUIRE(ppo_conv3_dgrad_bits_ok(), "ppo_conv3_dgrad_bits: needs the image-resident kernel (tune 8)");
   PPO_REQUIRE(m2bits != nullptr, "ppo_conv3_dgrad_bits: null mask");
   return conv3_dgrad_img<true>(dz3, B, w3d, reinterpret_cast<const float*>(m2bits), dz2, stream);
 }
 
 PPO_API int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream) {
-  if (g_tune[TK_CONV3_DGRAD] == 8) return conv3_dgrad_img<false>(dz3, B, w3d, a2, dz2, stream);
-  if (use_x9_all()) {
-    ConvDgradS1<9, 64, 3, 7, 32, XP64> p;
-    p.dy = dz3; p.wd = w3d; p.act = a2; p.dx = dz2; p.M = B * 81;
-    set_planes(p, w3d, 64 * 288, 64, 288);
-    return launch_x9(p, (long long)B * 81, 64, 1, as_stream(stream), "conv3_dgrad", 2.0 * B * 49 * 32 * 576);
-  }
-#define TD3(C_) ConvDgradS1<9, 64, 3, 7, 32, C_>
-  PPO_VARIANTS64(TD3, (p.dy = dz3, p.wd = w3d, p.act = a2, p.dx = dz2, p.M = B * 81), (long long)B * 81, 64, 1,
-                 "conv3_dgrad", 2.0 * B * 49 * 32 * 576)
-#undef TD3
+  return conv3_dgrad_img<false>(dz3, B, w3d, a2, dz2, stream);
 }
 
 template <bool BITS>
 static int conv2_dgrad_img(const float* dz2, int B, const float* w2d, const float* mask, float* dz1, void* stream) {
   if (B <= 0) return 0;
-  const int n_cu = device_cus();
-  const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
+  const unsigned nb = img_grid(B);
   int slot;
   const bool prof = ppo_prof_begin("conv2_dgrad", as_stream(stream), &slot);
   const uint16_t* wpl = planes_of(w2d, 128 * 256);
   const int sg = g_stagger & ~2;
   if (g_products == 9) conv2_dgrad_x9_kernel<9, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
   else if (g_products == 1) conv2_dgrad_x9_kernel<1, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
-  else if (sg & 0x70) conv2_dgrad_x9_kernel<6, BITS, true><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
   else conv2_dgrad_x9_kernel<6, BITS><<<nb, 512, 0, as_stream(stream)>>>(dz2, B, wpl, mask, dz1, sg);
   if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
   PPO_LAUNCH_CHECK("conv2_dgrad_x9_kernel");
   return 0;
 }
 
-// conv2 dgrad with the conv1 ReLU mask as bits (m1bits [B][400] u32 from
-// ppo_conv1_fwd_mask); the image-resident kernel only (ppo_conv2_dgrad_bits_ok).
-PPO_API int ppo_conv2_dgrad_bits_ok() { return g_tune[TK_CONV2_DGRAD] == 8 ? 1 : 0; }
+// conv2 dgrad with the conv1 ReLU mask as bits (m1bits [B][400] u32 from ppo_conv1_fwd_mask)
+PPO_API int ppo_conv2_dgrad_bits_ok() { return 1; }
 PPO_API int ppo_conv2_dgrad_bits(const float* dz2, int B, const float* w2d, const uint32_t* m1bits, float* dz1,
                                  void* stream) {
-  PPO_REQUIRE(ppo_conv2_dgrad_bits_ok(), "ppo_conv2_dgrad_bits: needs the image-resident kernel (tune 8)");
   PPO_REQUIRE(m1bits != nullptr, "ppo_conv2_dgrad_bits: null mask");
   return conv2_dgrad_img<true>(dz2, B, w2d, reinterpret_cast<const float*>(m1bits), dz1, stream);
 }
 
 PPO_API int ppo_conv2_dgrad(const float* dz2, int B, const float* w2d, const float* a1, float* dz1, void* stream) {
-  if (g_tune[TK_CONV2_DGRAD] == 8) return conv2_dgrad_img<false>(dz2, B, w2d, a1, dz1, stream);
-  if (use_x9_all()) {
-    Conv2Dgrad<XP128> p;
-    p.dy = dz2; p.wd = w2d; p.act = a1; p.dx = dz1; p.M = B * 100;
-    set_planes(p, w2d, 128 * 256, 128, 256);
-    return launch_x9(p, (long long)B * 100, 128, 1, as_stream(stream), "conv2_dgrad", 2.0 * B * 81 * 64 * 512);
-  }
-#define TD2(C_) Conv2Dgrad<C_>
-  PPO_VARIANTS128(TD2, (p.dy = dz2, p.wd = w2d, p.act = a1, p.dx = dz1, p.M = B * 100), (long long)B * 100, 128, 1,
-                  "conv2_dgrad", 2.0 * B * 81 * 64 * 512)
-#undef TD2
+  return conv2_dgrad_img<false>(dz2, B, w2d, a1, dz1, stream);
 }
 
 // split count and chunk for a wgrad reduction of R rows (BK-aligned chunks)
@@ -2615,9 +2291,6 @@ static void set_wgrad(P& p, const float* dz, int COUT, long long R, int Z, float
 }
 
 using CfgW32 = Cfg<32, 256, 1, 4, false, false, true>;
-using CfgW32n = Cfg<32, 128, 1, 4, false, false, true>;
-using CfgW64 = Cfg<64, 128, 2, 2, false, false, true>;
-using CfgW32b = Cfg<32, 128, 1, 4, false, false, true>;
 using CfgWfc = Cfg<128, 128, 2, 2, false, false, true>;
 
 // conv1 wgrad partials: slab [Z][32][C*64], slab_bias [Z][32]
@@ -2626,47 +2299,28 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
   const long long R = (long long)B * 400;
   PPO_REQUIRE(R < 0x7fffffffLL, "ppo_conv1_wgrad: B too large");
   const double fl = 2.0 * R * 32 * C * 64;
-  const int c1w = g_tune[TK_CONV1_WGRAD];
-  // part-pipelined (3-5; also the half-precision mode under the k-split tunes 7 / 8, which
-  // exist for fp32 dz only: the bf16-dz part kernel, tune 5's, runs there)
-  if (obs_is_u8 && C == 4 && ((c1w >= 3 && c1w <= 5) || ((c1w == 7 || c1w == 8) && g_products == 1))) {
+  // u8 rows, C = 4: the k-split kernel (conv1w.hip, tune 8, fp32 dz) or the
+  // part-pipelined kernel (tune 5; the half-precision mode's, bf16 dz)
+  if (obs_is_u8 && C == 4 && (g_tune[TK_CONV1_WGRAD] == 5 || g_products == 1)) {
     if (B <= 0 || Z <= 0) return 0;
     PPO_REQUIRE((B + Z - 1) / Z <= 512, "ppo_conv1_wgrad: %d images over %d blocks (at most 512 per block)", B, Z);
     int slot;
     const bool prof = ppo_prof_begin("conv1_wgrad_u8", as_stream(stream), &slot);
-    if (g_products == 1 && c1w != 3 && c1w != 4)   // half-precision mode: bf16 dz
+    if (g_products == 1)
       conv1_wgrad_parts_kernel<1, 16, 2><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
                                                                             slab, slab_bias, 0);
-    else if (g_products == 1)
-      conv1_wgrad_parts_kernel<1><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
-                                                                    slab_bias, 0);
-    else if (g_tune[TK_CONV1_WGRAD] == 4)   // four waves per SIMD
-      conv1_wgrad_parts_kernel<3, 16><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
-                                                                         slab, slab_bias, g_stagger >> 4);
-    else if (g_tune[TK_CONV1_WGRAD] == 5)   // four waves per SIMD, two column tiles per wave
+    else
       conv1_wgrad_parts_kernel<3, 16, 2><<<Z, 1024, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B,
                                                                             slab, slab_bias, g_stagger >> 4);
-    else
-      conv1_wgrad_parts_kernel<3><<<Z, 512, 0, as_stream(stream)>>>(dz1, (const uint8_t*)obs, idx, row0, B, slab,
-                                                                    slab_bias, g_stagger >> 4);
     if (prof) ppo_prof_end(slot, as_stream(stream), fl);
     PPO_LAUNCH_CHECK("conv1_wgrad_parts_kernel");
     return 0;
   }
-  if (obs_is_u8 && C == 4 && (g_tune[TK_CONV1_WGRAD] == 7 || g_tune[TK_CONV1_WGRAD] == 8) && g_products != 1)
-    return conv1_wgrad_kw(dz1, (const uint8_t*)obs, idx, row0, B, Z, slab, slab_bias, g_tune[TK_CONV1_WGRAD],
-                          stream);   // conv1w.hip, k-split over waves (8: u8 image by LDS-DMA)
-  if (!obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] != 9 && ((uintptr_t)obs & 15) == 0)   // conv1f.hip
+  if (obs_is_u8 && C == 4)
+    return conv1_wgrad_kw(dz1, (const uint8_t*)obs, idx, row0, B, Z, slab, slab_bias, stream);
+  if (!obs_is_u8 && C == 4 && ((uintptr_t)obs & 15) == 0)   // conv1f.hip
     return ppo_conv1_wgrad_f32(dz1, (const float*)obs, idx, row0, B, Z, slab, slab_bias, stream);
-  if (obs_is_u8 && C == 4 && g_tune[TK_CONV1_WGRAD] == 6)   // conv1f.hip, tr_b16 im2col (A/B)
-    return conv1_wgrad_u8_tr(dz1, (const uint8_t*)obs, idx, row0, B, Z, slab, slab_bias, stream);
-  if (obs_is_u8) {
-    if (g_tune[TK_CONV1_WGRAD] == 9) {
-      Conv1Wgrad<uint8_t, CfgW32n> p;
-      set_wgrad(p, dz1, 32, R, Z, slab, slab_bias, C * 64);
-      p.obs = (const uint8_t*)obs; p.idx = idx; p.row0 = row0; p.C = C;
-      return launch(p, 32, C * 64, Z, as_stream(stream), "conv1_wgrad_u8", fl);
-    }
+  if (obs_is_u8) {   // any other channel count: the generic fp32-MFMA tile GEMM
     Conv1Wgrad<uint8_t, CfgW32> p;
     set_wgrad(p, dz1, 32, R, Z, slab, slab_bias, C * 64);
     p.obs = (const uint8_t*)obs; p.idx = idx; p.row0 = row0; p.C = C;
@@ -2680,93 +2334,24 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
 
 PPO_API int ppo_conv2_wgrad(const float* dz2, const float* a1, int B, int Z, float* slab, float* slab_bias,
                             void* stream) {
-  if (g_tune[TK_CONV2_WGRAD] == 8) {
-    if (B <= 0 || Z <= 0) return 0;
-    int slot;
-    const bool prof = ppo_prof_begin("conv2_wgrad", as_stream(stream), &slot);
-    PPO_LAUNCH_NP(conv2_wgrad_x9_kernel, Z, 512, as_stream(stream), dz2, a1, B, slab, slab_bias);
-    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
-    PPO_LAUNCH_CHECK("conv2_wgrad_x9_kernel");
-    return 0;
-  }
-  if (use_x9_all()) {
-    ConvWgrad<20, 32, 4, 2, 9, XW64> p;
-    set_wgrad(p, dz2, 64, (long long)B * 81, Z, slab, slab_bias, 512);
-    p.in = a1;
-    return launch_x9(p, 64, 512, Z, as_stream(stream), "conv2_wgrad", 2.0 * B * 81 * 64 * 512);
-  }
-  ConvWgrad<20, 32, 4, 2, 9, CfgW64> p;
-  set_wgrad(p, dz2, 64, (long long)B * 81, Z, slab, slab_bias, 512);
-  p.in = a1;
-  return launch(p, 64, 512, Z, as_stream(stream), "conv2_wgrad", 2.0 * B * 81 * 64 * 512);
-}
-
-// timing anatomy of the conv2 forward (diagnostics, wrong results by design): dbg bits as
-// conv2_fwd_x9c_kernel's DBG (1 no MFMAs, 2 no staging, 4 no global loads, 8 no epilogue stores),
-// the mask-writing instantiation the training forward runs
-PPO_API int ppo_probe_conv2_fwd_anatomy(int dbg, const float* a1, int B, const float* w2p, const float* b2,
-                                        float* out, uint16_t* mbits, void* stream) {
-  PPO_REQUIRE(B > 0 && dbg >= 0 && dbg < 16, "ppo_probe_conv2_fwd_anatomy: B=%d dbg=%d", B, dbg);
-  const int n_cu = device_cus();
-  const unsigned nb = (unsigned)(B < n_cu ? B : n_cu);
-  const uint16_t* wpl = planes_of(w2p, 64 * 512);
-  hipStream_t st = as_stream(stream);
-  switch (dbg) {
-#define PPO_C2FA(D) \
-  case D: conv2_fwd_x9c_kernel<6, true, D><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits); break;
-    PPO_C2FA(0) PPO_C2FA(1) PPO_C2FA(2) PPO_C2FA(3) PPO_C2FA(4) PPO_C2FA(5) PPO_C2FA(6) PPO_C2FA(7)
-    PPO_C2FA(8) PPO_C2FA(9) PPO_C2FA(10) PPO_C2FA(11) PPO_C2FA(12) PPO_C2FA(13) PPO_C2FA(14) PPO_C2FA(15)
-#undef PPO_C2FA
-  }
-  PPO_LAUNCH_CHECK("conv2_fwd_x9c_kernel (anatomy)");
-  return 0;
-}
-
-// timing anatomy of the conv2 weight gradient (diagnostics, wrong results by design): dbg bits as
-// conv2_wgrad_x9_kernel's DBG (1 no MFMAs, 2 no LDS staging, 4 no global loads)
-PPO_API int ppo_probe_conv2_wgrad_anatomy(int dbg, const float* dz2, const float* a1, int B, int Z, float* slab,
-                                          float* slab_bias, void* stream) {
-  PPO_REQUIRE(B > 0 && Z > 0 && ((dbg >= 0 && dbg < 8) || dbg == 8 || dbg == 16 || dbg == 24),
-              "ppo_probe_conv2_wgrad_anatomy: B=%d Z=%d dbg=%d", B, Z, dbg);
-  hipStream_t st = as_stream(stream);
-  switch (dbg) {
-    case 0: conv2_wgrad_x9_kernel<6, 0><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    case 1: conv2_wgrad_x9_kernel<6, 1><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    case 2: conv2_wgrad_x9_kernel<6, 2><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    case 3: conv2_wgrad_x9_kernel<6, 3><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    case 4: conv2_wgrad_x9_kernel<6, 4><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    case 5: conv2_wgrad_x9_kernel<6, 5><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    case 6: conv2_wgrad_x9_kernel<6, 6><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    case 7: conv2_wgrad_x9_kernel<6, 7><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    case 8: conv2_wgrad_x9_kernel<6, 8><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    case 16: conv2_wgrad_x9_kernel<6, 16><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-    default: conv2_wgrad_x9_kernel<6, 24><<<Z, 512, 0, st>>>(dz2, a1, B, slab, slab_bias); break;
-  }
-  PPO_LAUNCH_CHECK("conv2_wgrad_x9_kernel (anatomy)");
+  if (B <= 0 || Z <= 0) return 0;
+  int slot;
+  const bool prof = ppo_prof_begin("conv2_wgrad", as_stream(stream), &slot);
+  PPO_LAUNCH_NP(conv2_wgrad_x9_kernel, Z, 512, as_stream(stream), dz2, a1, B, slab, slab_bias);
+  if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 81 * 64 * 512);
+  PPO_LAUNCH_CHECK("conv2_wgrad_x9_kernel");
   return 0;
 }
 
 PPO_API int ppo_conv3_wgrad(const float* dz3, const float* a2, int B, int Z, float* slab, float* slab_bias,
                             void* stream) {
-  if (g_tune[TK_CONV3_WGRAD] == 8) {
-    if (B <= 0 || Z <= 0) return 0;
-    int slot;
-    const bool prof = ppo_prof_begin("conv3_wgrad", as_stream(stream), &slot);
-    PPO_LAUNCH_NP(conv3_wgrad_x9_kernel, Z, 768, as_stream(stream), dz3, a2, B, slab, slab_bias);
-    if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
-    PPO_LAUNCH_CHECK("conv3_wgrad_x9_kernel");
-    return 0;
-  }
-  if (use_x9_all()) {
-    ConvWgrad<9, 64, 3, 1, 7, XW32> p;
-    set_wgrad(p, dz3, 32, (long long)B * 49, Z, slab, slab_bias, 576);
-    p.in = a2;
-    return launch_x9(p, 32, 576, Z, as_stream(stream), "conv3_wgrad", 2.0 * B * 49 * 32 * 576);
-  }
-  ConvWgrad<9, 64, 3, 1, 7, CfgW32b> p;
-  set_wgrad(p, dz3, 32, (long long)B * 49, Z, slab, slab_bias, 576);
-  p.in = a2;
-  return launch(p, 32, 576, Z, as_stream(stream), "conv3_wgrad", 2.0 * B * 49 * 32 * 576);
+  if (B <= 0 || Z <= 0) return 0;
+  int slot;
+  const bool prof = ppo_prof_begin("conv3_wgrad", as_stream(stream), &slot);
+  PPO_LAUNCH_NP(conv3_wgrad_x9_kernel, Z, 768, as_stream(stream), dz3, a2, B, slab, slab_bias);
+  if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
+  PPO_LAUNCH_CHECK("conv3_wgrad_x9_kernel");
+  return 0;
 }
 
 // dW[n][k] = Σ_r dy[r][n] x[r][k]: slab [Z][N][K], slab_bias [Z][N]
@@ -2782,20 +2367,12 @@ PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int 
       p.x = x; p.K = K;
       return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K);
     }
-#define PPO_FCW(CFG)                                                                \
-  {                                                                                 \
-    DenseWgrad<CFG> p;                                                              \
-    set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);                                  \
-    p.x = x; p.K = K; p.n_fast = fc_order(0);                                       \
-    p.vec = g_tune[TK_ORDER] < 3 && K % 4 == 0 && ((uintptr_t)slab & 15) == 0;      \
-    return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K); \
-  }
-    // fc_wgrad tune: 0 / 10 split-at-staging 256 x 128 (default: 0.727 vs 0.775 ms at the c3
-    // minibatch), 11 split-at-staging 128 x 128 (0.945), 1 the in-loop-split XW256x128
-    if (g_tune[TK_FC_WGRAD] == 1) PPO_FCW(XW256x128)   // 0.79 vs 0.83 ms (XW128), round 2
-    if (g_tune[TK_FC_WGRAD] == 11) PPO_FCW(SW128)
-    PPO_FCW(SW256x128)
-#undef PPO_FCW
+    // split at staging, 256 x 128 tiles: 0.727 vs 0.775 ms (in-loop split) at the c3 minibatch
+    DenseWgrad<SW256x128> p;
+    set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);
+    p.x = x; p.K = K; p.n_fast = 0;
+    p.vec = K % 4 == 0 && ((uintptr_t)slab & 15) == 0;
+    return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K);
   }
   DenseWgrad<CfgWfc> p;
   set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);

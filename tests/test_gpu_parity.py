@@ -854,11 +854,9 @@ def _packed(gpu, H, seed):
     return w, packed, [packed.data_ptr() + 4 * int(o) for o in offs]
 
 
-@pytest.mark.parametrize("variant", [3, 8])
-def test_conv2_dgrad_variants_vs_torch(gpu, variant):
+def test_conv2_dgrad_vs_torch(gpu):
     """conv2 dgrad (phase-merged GEMM, 4x4 stride 2 transposed conv 9x9 -> 20x20
-    with the conv1 ReLU mask), every kernel variant — the fp32 tile GEMM (3) and
-    the image-resident exact split-bf16 kernel (8) — vs torch float64:
+    with the conv1 ReLU mask) on the image-resident exact split-bf16 kernel vs torch float64:
     max |err| <= 1e-5 * max |ref| (fp32 arithmetic, summation order differs).
     B = 300 images > the persistent grid, so blocks walk several images."""
     Hh = _hip()
@@ -869,13 +867,8 @@ def test_conv2_dgrad_variants_vs_torch(gpu, variant):
     a1 = torch.randn(B, 20, 20, 32, generator=g)
     dz1 = torch.full((B, 20, 20, 32), float("nan"), device=gpu)
     dz2_d, a1_d = dz2.cuda(), a1.cuda()
-    old_tune = Hh.call("ppo_tune_get", b"conv2_dgrad")
-    Hh.call("ppo_tune_set", b"conv2_dgrad", variant)
-    try:
-        Hh.call("ppo_conv2_dgrad", dz2_d.data_ptr(), B, pk[5], a1_d.data_ptr(), dz1.data_ptr(), _s())
-        torch.cuda.synchronize()
-    finally:
-        Hh.call("ppo_tune_set", b"conv2_dgrad", old_tune)
+    Hh.call("ppo_conv2_dgrad", dz2_d.data_ptr(), B, pk[5], a1_d.data_ptr(), dz1.data_ptr(), _s())
+    torch.cuda.synchronize()
     ref = F.conv_transpose2d(dz2.double().permute(0, 3, 1, 2), w["w2"].double(), stride=2).permute(0, 2, 3, 1)
     ref = torch.where(a1 > 0, ref, torch.zeros((), dtype=torch.float64))
     err = (dz1.cpu().double() - ref).abs().max().item()
@@ -926,10 +919,8 @@ def test_conv1_mask_bits_and_conv2_dgrad_bits(gpu, conv1_variant):
     assert torch.equal(d_ref, d_bits)
 
 
-@pytest.mark.parametrize("conv2_variant", [0, 12])
-def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu, conv2_variant):
-    """ppo_conv2_fwd_mask (fused ballot epilogue: variant 12; conv + relu_bits
-    kernel: variant 0) writes bit c of word p = (a2[p][c] > 0) of its own fp32
+def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu):
+    """ppo_conv2_fwd_mask (fused ballot epilogue) writes bit c of word p = (a2[p][c] > 0) of its own fp32
     output, with a2 identical to ppo_conv2_fwd's; conv3 dgrad fed those bits
     (ppo_conv3_dgrad_bits) equals the fp32-mask kernel bit for bit.  B = 300."""
     Hh = _hip()
@@ -941,14 +932,9 @@ def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu, conv2_variant):
     a2 = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
     a2m = torch.full_like(a2, float("nan"))
     bits = torch.zeros(B * 81, dtype=torch.int64, device=gpu)
-    old = Hh.call("ppo_tune_get", b"conv2_fwd")
-    Hh.call("ppo_tune_set", b"conv2_fwd", conv2_variant)
-    try:
-        Hh.call("ppo_conv2_fwd", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2.data_ptr(), _s())
-        Hh.call("ppo_conv2_fwd_mask", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2m.data_ptr(), bits.data_ptr(), _s())
-        torch.cuda.synchronize()
-    finally:
-        Hh.call("ppo_tune_set", b"conv2_fwd", old)
+    Hh.call("ppo_conv2_fwd", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2.data_ptr(), _s())
+    Hh.call("ppo_conv2_fwd_mask", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2m.data_ptr(), bits.data_ptr(), _s())
+    torch.cuda.synchronize()
     assert torch.equal(a2, a2m)
     live = (a2 > 0).reshape(B * 81, 64).cpu()
     got = bits.cpu()
@@ -966,11 +952,11 @@ def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu, conv2_variant):
     assert torch.equal(d_ref, d_bits)
 
 
-@pytest.mark.parametrize("variant", [0, 12])
-def test_conv2_fwd_variants_vs_torch(gpu, variant):
-    """conv2 forward (4x4 stride 2, 20x20x32 -> 9x9x64, bias + ReLU): the split-bf16
-    tile GEMM (0), the image-resident kernel (12: two stages, staging inside the
-    k-steps) vs torch float64:
+@pytest.mark.parametrize("products", [6, 9])
+def test_conv2_fwd_vs_torch(gpu, products):
+    """conv2 forward (4x4 stride 2, 20x20x32 -> 9x9x64, bias + ReLU): the
+    image-resident kernel (two stages, staging inside the k-steps) with six and
+    nine part products vs torch float64:
     max |err| <= 1e-5 * max |ref|.  B = 300 > the persistent grid."""
     Hh = _hip()
     B = 300
@@ -980,24 +966,23 @@ def test_conv2_fwd_variants_vs_torch(gpu, variant):
     b2 = torch.randn(64, generator=g) * 0.1
     a1_d, b2_d = a1.cuda(), b2.cuda()
     out = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
-    old = Hh.call("ppo_tune_get", b"conv2_fwd")
-    Hh.call("ppo_tune_set", b"conv2_fwd", variant)
+    old = Hh.call("ppo_tune_get", b"products")
+    Hh.call("ppo_tune_set", b"products", products)
     try:
         Hh.call("ppo_conv2_fwd", a1_d.data_ptr(), B, pk[0], b2_d.data_ptr(), out.data_ptr(), _s())
         torch.cuda.synchronize()
     finally:
-        Hh.call("ppo_tune_set", b"conv2_fwd", old)
+        Hh.call("ppo_tune_set", b"products", old)
     ref = F.conv2d(a1.double().permute(0, 3, 1, 2), w["w2"].double(), b2.double(), stride=2)
     ref = torch.relu(ref).permute(0, 2, 3, 1)
     err = (out.cpu().double() - ref).abs().max().item()
     assert err <= 1e-5 * ref.abs().max().item(), err
 
 
-@pytest.mark.parametrize("variant", [0, 8])
-def test_conv2_wgrad_variants_vs_torch(gpu, variant):
+def test_conv2_wgrad_vs_torch(gpu):
     """conv2 weight + bias gradient (split-K partials + ppo_wgrad_reduce into the
-    torch layout): the fp32 tile GEMM (0) and the image-resident split-bf16 kernel
-    (8) vs torch float64: max |err| <= 1e-5 * max |ref| per tensor.  B = 300."""
+    torch layout) on the image-resident split-bf16 kernel vs torch float64:
+    max |err| <= 1e-5 * max |ref| per tensor.  B = 300."""
     Hh = _hip()
     B = 300
     g = torch.Generator().manual_seed(31)
@@ -1009,15 +994,10 @@ def test_conv2_wgrad_variants_vs_torch(gpu, variant):
     slab_b = torch.empty(Z * 64, device=gpu)
     gw = torch.empty(64 * 512, device=gpu)
     gb = torch.empty(64, device=gpu)
-    old_tune = Hh.call("ppo_tune_get", b"conv2_wgrad")
-    Hh.call("ppo_tune_set", b"conv2_wgrad", variant)
-    try:
-        Hh.call("ppo_conv2_wgrad", dz2_d.data_ptr(), a1_d.data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), _s())
-        Hh.call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, 64, 512, 1, 4, 32, gw.data_ptr(),
-                gb.data_ptr(), 1.0, 0, _s())
-        torch.cuda.synchronize()
-    finally:
-        Hh.call("ppo_tune_set", b"conv2_wgrad", old_tune)
+    Hh.call("ppo_conv2_wgrad", dz2_d.data_ptr(), a1_d.data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), _s())
+    Hh.call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, 64, 512, 1, 4, 32, gw.data_ptr(),
+            gb.data_ptr(), 1.0, 0, _s())
+    torch.cuda.synchronize()
     x, dy = a1.double().permute(0, 3, 1, 2), dz2.double().permute(0, 3, 1, 2)
     ref_w = torch.nn.grad.conv2d_weight(x, (64, 32, 4, 4), dy, stride=2)
     ref_b = dy.sum((0, 2, 3))
@@ -1061,10 +1041,9 @@ def test_two_rank_update_one_gpu():
     assert outs[0]["losses"] == outs[1]["losses"]
 
 
-@pytest.mark.parametrize("variant", [1, 8])
-def test_conv3_dgrad_variants_vs_torch(gpu, variant):
-    """conv3 dgrad (3x3 stride 1, 7x7x32 -> 9x9x64, a2 ReLU mask): the fp32 tile
-    GEMM (1) and the image-resident split-bf16 kernel (8) vs torch float64:
+def test_conv3_dgrad_vs_torch(gpu):
+    """conv3 dgrad (3x3 stride 1, 7x7x32 -> 9x9x64, a2 ReLU mask) on the
+    image-resident split-bf16 kernel vs torch float64:
     max |err| <= 1e-5 * max |ref|.  B = 300 > the persistent grid."""
     Hh = _hip()
     B = 300
@@ -1074,23 +1053,17 @@ def test_conv3_dgrad_variants_vs_torch(gpu, variant):
     a2 = torch.randn(B, 9, 9, 64, generator=g)
     dz3_d, a2_d = dz3.cuda(), a2.cuda()
     dz2 = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
-    old_tune = Hh.call("ppo_tune_get", b"conv3_dgrad")
-    Hh.call("ppo_tune_set", b"conv3_dgrad", variant)
-    try:
-        Hh.call("ppo_conv3_dgrad", dz3_d.data_ptr(), B, pk[4], a2_d.data_ptr(), dz2.data_ptr(), _s())
-        torch.cuda.synchronize()
-    finally:
-        Hh.call("ppo_tune_set", b"conv3_dgrad", old_tune)
+    Hh.call("ppo_conv3_dgrad", dz3_d.data_ptr(), B, pk[4], a2_d.data_ptr(), dz2.data_ptr(), _s())
+    torch.cuda.synchronize()
     ref = F.conv_transpose2d(dz3.double().permute(0, 3, 1, 2), w["w3"].double()).permute(0, 2, 3, 1)
     ref = torch.where(a2 > 0, ref, torch.zeros((), dtype=torch.float64))
     err = (dz2.cpu().double() - ref).abs().max().item()
     assert err <= 1e-5 * ref.abs().max().item(), err
 
 
-@pytest.mark.parametrize("variant", [3, 8])
-def test_conv3_fwd_variants_vs_torch(gpu, variant):
-    """conv3 forward (3x3 stride 1, 9x9x64 -> 7x7x32, bias + ReLU): the split-bf16
-    tile GEMM (3) and the image-resident kernel (8) vs torch float64:
+def test_conv3_fwd_vs_torch(gpu):
+    """conv3 forward (3x3 stride 1, 9x9x64 -> 7x7x32, bias + ReLU) on the
+    image-resident kernel vs torch float64:
     max |err| <= 1e-5 * max |ref|.  B = 300 > the persistent grid."""
     Hh = _hip()
     B = 300
@@ -1100,20 +1073,14 @@ def test_conv3_fwd_variants_vs_torch(gpu, variant):
     b3 = torch.randn(32, generator=g) * 0.1
     a2_d, b3_d = a2.cuda(), b3.cuda()
     out = torch.full((B, 7, 7, 32), float("nan"), device=gpu)
-    old_tune = Hh.call("ppo_tune_get", b"conv3_fwd")
-    Hh.call("ppo_tune_set", b"conv3_fwd", variant)
-    try:
-        Hh.call("ppo_conv3_fwd", a2_d.data_ptr(), B, pk[1], b3_d.data_ptr(), out.data_ptr(), _s())
-        torch.cuda.synchronize()
-    finally:
-        Hh.call("ppo_tune_set", b"conv3_fwd", old_tune)
+    Hh.call("ppo_conv3_fwd", a2_d.data_ptr(), B, pk[1], b3_d.data_ptr(), out.data_ptr(), _s())
+    torch.cuda.synchronize()
     ref = torch.relu(F.conv2d(a2.double().permute(0, 3, 1, 2), w["w3"].double(), b3.double())).permute(0, 2, 3, 1)
     err = (out.cpu().double() - ref).abs().max().item()
     assert err <= 1e-5 * ref.abs().max().item(), err
 
 
-@pytest.mark.parametrize("variant", [12])
-def test_conv2_fwd_two_stage_bit_identical(gpu, variant):
+def test_conv2_fwd_two_stage_bit_identical(gpu):
     """conv2 forward (two compact LDS stages, staging inside the k-steps,
     partials handed over in the vacated stage): the rollout instantiation and
     the training one that also writes the ReLU mask bits give bit-identical
@@ -1122,25 +1089,20 @@ def test_conv2_fwd_two_stage_bit_identical(gpu, variant):
     Hh = _hip()
     _, packed, pk = _packed(gpu, 64, 71)
     g = torch.Generator().manual_seed(72)
-    old = Hh.call("ppo_tune_get", b"conv2_fwd")
-    try:
-        for B in (300, 7):
-            a1 = torch.relu(torch.randn(B, 20, 20, 32, generator=g)).cuda()
-            b2 = (torch.randn(64, generator=g) * 0.1).cuda()
-            Hh.call("ppo_tune_set", b"conv2_fwd", variant)
-            o = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
-            bits = torch.zeros(B * 81, dtype=torch.int64, device=gpu)
-            Hh.call("ppo_conv2_fwd_mask", a1.data_ptr(), B, pk[0], b2.data_ptr(), o.data_ptr(), bits.data_ptr(), _s())
-            o2 = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
-            Hh.call("ppo_conv2_fwd", a1.data_ptr(), B, pk[0], b2.data_ptr(), o2.data_ptr(), _s())
-            torch.cuda.synchronize()
-            assert not torch.isnan(o).any()
-            assert torch.equal(o, o2)
-            pos = (o.reshape(B * 81, 64) > 0).cpu().to(torch.int64)
-            want = (pos << torch.arange(64, dtype=torch.int64)).sum(1)
-            assert torch.equal(bits.cpu(), want)
-    finally:
-        Hh.call("ppo_tune_set", b"conv2_fwd", old)
+    for B in (300, 7):
+        a1 = torch.relu(torch.randn(B, 20, 20, 32, generator=g)).cuda()
+        b2 = (torch.randn(64, generator=g) * 0.1).cuda()
+        o = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
+        bits = torch.zeros(B * 81, dtype=torch.int64, device=gpu)
+        Hh.call("ppo_conv2_fwd_mask", a1.data_ptr(), B, pk[0], b2.data_ptr(), o.data_ptr(), bits.data_ptr(), _s())
+        o2 = torch.full((B, 9, 9, 64), float("nan"), device=gpu)
+        Hh.call("ppo_conv2_fwd", a1.data_ptr(), B, pk[0], b2.data_ptr(), o2.data_ptr(), _s())
+        torch.cuda.synchronize()
+        assert not torch.isnan(o).any()
+        assert torch.equal(o, o2)
+        pos = (o.reshape(B * 81, 64) > 0).cpu().to(torch.int64)
+        want = (pos << torch.arange(64, dtype=torch.int64)).sum(1)
+        assert torch.equal(bits.cpu(), want)
 
 
 def test_stagger_bit_identical(gpu):
@@ -1184,11 +1146,10 @@ def test_stagger_bit_identical(gpu):
             assert torch.equal(r, x)
 
 
-@pytest.mark.parametrize("variant", [0, 8])
-def test_conv3_wgrad_variants_vs_torch(gpu, variant):
+def test_conv3_wgrad_vs_torch(gpu):
     """conv3 weight + bias gradient (partials + ppo_wgrad_reduce into the torch
-    layout): the fp32 tile GEMM (0) and the image-resident split-bf16 kernel (8)
-    vs torch float64: max |err| <= 1e-5 * max |ref| per tensor.  B = 300."""
+    layout) on the image-resident split-bf16 kernel vs torch float64:
+    max |err| <= 1e-5 * max |ref| per tensor.  B = 300."""
     Hh = _hip()
     B = 300
     g = torch.Generator().manual_seed(61)
@@ -1200,15 +1161,10 @@ def test_conv3_wgrad_variants_vs_torch(gpu, variant):
     slab_b = torch.empty(Z * 32, device=gpu)
     gw = torch.empty(32 * 576, device=gpu)
     gb = torch.empty(32, device=gpu)
-    old_tune = Hh.call("ppo_tune_get", b"conv3_wgrad")
-    Hh.call("ppo_tune_set", b"conv3_wgrad", variant)
-    try:
-        Hh.call("ppo_conv3_wgrad", dz3_d.data_ptr(), a2_d.data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), _s())
-        Hh.call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, 32, 576, 1, 3, 64, gw.data_ptr(),
-                gb.data_ptr(), 1.0, 0, _s())
-        torch.cuda.synchronize()
-    finally:
-        Hh.call("ppo_tune_set", b"conv3_wgrad", old_tune)
+    Hh.call("ppo_conv3_wgrad", dz3_d.data_ptr(), a2_d.data_ptr(), B, Z, slab.data_ptr(), slab_b.data_ptr(), _s())
+    Hh.call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), Z, 32, 576, 1, 3, 64, gw.data_ptr(),
+            gb.data_ptr(), 1.0, 0, _s())
+    torch.cuda.synchronize()
     x, dy = a2.double().permute(0, 3, 1, 2), dz3.double().permute(0, 3, 1, 2)
     ref_w = torch.nn.grad.conv2d_weight(x, (32, 64, 3, 3), dy)
     ref_b = dy.sum((0, 2, 3))
@@ -1489,16 +1445,13 @@ def test_gru_persistent_bptt_timeout_sets_error(gpu):
     assert err.item() == 0 and torch.isfinite(dgi).all() and (dgi[: n] != 0).any()
 
 
-@pytest.mark.parametrize("variant", [3, 4, 5, 6, 7, 8, 9])
-def test_conv1_wgrad_variants_vs_torch(gpu, variant):
+@pytest.mark.parametrize("variant,Z", [(5, 0), (8, 0), (8, 256)])
+def test_conv1_wgrad_variants_vs_torch(gpu, variant, Z):
     """conv1 weight + bias gradient from u8 observations gathered by index (the
-    minibatch path): the part-pipelined bf16x3 kernel with 8 (3) and 16
-    waves (4; 5 two tiles per wave), the k-split kernel of conv1w.hip (7: B = 300
-    and Z = 256 leave blocks with one and two images) and the fp32 tile GEMM (9)
-    vs torch float64
-    on (u8 / 255):
-    max |err| <= 1e-5 * max |ref|.
-    B = 300 images, rows gathered out of order."""
+    minibatch path): the part-pipelined bf16x3 kernel (5, 16 waves, two tiles per
+    wave) and the k-split kernel of conv1w.hip (8; Z = 256 leaves blocks with one
+    and two of the B = 300 images) vs torch float64 on (u8 / 255):
+    max |err| <= 1e-5 * max |ref|.  Rows gathered out of order."""
     Hh = _hip()
     B, rows = 300, 420
     g = torch.Generator().manual_seed(81)
@@ -1506,7 +1459,7 @@ def test_conv1_wgrad_variants_vs_torch(gpu, variant):
     idx = torch.randperm(rows, generator=g)[:B].contiguous()
     dz1 = torch.randn(B, 20, 20, 32, generator=g)
     obs_d, idx_d, dz1_d = obs.cuda(), idx.cuda(), dz1.cuda()
-    Z = Hh.call("ppo_wgrad_splits", B * 400, 1, 2048, 16)
+    Z = Z or Hh.call("ppo_wgrad_splits", B * 400, 1, 2048, 16)
     slab = torch.empty(Z * 32 * 256, device=gpu)
     slab_b = torch.empty(Z * 32, device=gpu)
     gw = torch.empty(32 * 256, device=gpu)

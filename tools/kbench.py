@@ -80,8 +80,6 @@ def main():
     z4 = a.z4 or z4
     fws = torch.empty(max(call("ppo_fc_fwd_ws_bytes", B, H) // 4, 4), device=dev)
     z2c = a.z2 or max(n_cu, -(-B // 512))   # the engine's split for the image-resident conv2 wgrad
-    a1s = torch.empty(call("ppo_a1s_bytes", B) // 2, dtype=torch.int16, device=dev) \
-        if any("split" in k for k in a.only.split(",")) else None
     hw = rn(9 * H + 9, sc=0.03)                       # heads: wc [H], bc, wa [8][H], ba [8]
     hv = torch.empty(3 * B, device=dev)
     ha = torch.empty(B, dtype=torch.int64, device=dev)
@@ -151,31 +149,12 @@ def main():
         "conv1_wgrad_rgb": (lambda: call("ppo_conv1_wgrad_rgb", dz1.data_ptr(), frames.data_ptr(), idx.data_ptr(), 0,
                                          B, mean.data_ptr(), 36.31282043457031, z1c, slab.data_ptr(),
                                          slab_b.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
-        # the pre-split conv1 -> conv2 hand-off (a1split.hip)
-        "conv1_fwd_split": (lambda: call("ppo_conv1_fwd_split", obs.data_ptr(), idx.data_ptr(), 0, B, w1.data_ptr(),
-                                         b1.data_ptr(), a1s.data_ptr(), m1.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
-        "conv2_fwd_split": (lambda: call("ppo_conv2_fwd_split", a1s.data_ptr(), B, pk[0], b2.data_ptr(), a2.data_ptr(),
-                                         m2.data_ptr(), s), 2.0 * B * 81 * 64 * 512),
-        "conv2_fwd_split_nm": (lambda: call("ppo_conv2_fwd_split", a1s.data_ptr(), B, pk[0], b2.data_ptr(),
-                                            a2.data_ptr(), None, s), 2.0 * B * 81 * 64 * 512),
-        "conv2_wgrad_split": (lambda: call("ppo_conv2_wgrad_split", dz2.data_ptr(), a1s.data_ptr(), B, z2c,
-                                           slab.data_ptr(), slab_b.data_ptr(), s), 2.0 * B * 81 * 64 * 512),
-        # timing anatomy of the conv2 forward (wrong results): no MFMA / staging / loads / stores
-        **{f"conv2_fwd_anat{d}": ((lambda d=d: call("ppo_probe_conv2_fwd_anatomy", d, a1.data_ptr(), B, pk[0],
-                                                       b2.data_ptr(), a2.data_ptr(), m2.data_ptr(), s)),
-                                  2.0 * B * 81 * 64 * 512) for d in range(16)},
-        # timing anatomy of the conv2 weight gradient (wrong results): no MFMA / no staging / no loads
-        **{f"conv2_wgrad_anat{d}": ((lambda d=d: call("ppo_probe_conv2_wgrad_anatomy", d, dz2.data_ptr(),
-                                                         a1.data_ptr(), B, z2c, slab.data_ptr(), slab_b.data_ptr(),
-                                                         s)), 2.0 * B * 81 * 64 * 512) for d in (*range(8), 8, 16, 24)},
         "conv1_wreduce": (lambda: call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), z1, 32, 256, 0, 0, 0,
                                        gw.data_ptr(), gb.data_ptr(), 1.0 / 255, 0, s), 0.0),
     }
     # realistic activations for the backward kernels
     K["conv1_fwd_mask"][0](); K["conv2_fwd_mask"][0](); K["conv3_fwd"][0](); K["fc_fwd"][0]()
     K["fc_dgrad"][0](); K["conv3_dgrad"][0](); K["conv2_dgrad"][0]()
-    if a1s is not None:
-        K["conv1_fwd_split"][0]()
     torch.cuda.synchronize()
     only = [x for x in a.only.split(",") if x]
     total = 0.0
