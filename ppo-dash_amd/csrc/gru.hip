@@ -218,8 +218,13 @@ using CfgGruB = Cfg<64, 64, 2, 2, true, true>;
 // once per launch (no LDS staging, no k-loop barrier), one
 // v_mfma_f32_16x16x4_f32 (exact fp32) per 16x16 tile per k-step, and the four
 // K-quarter partials meet in LDS for the fused epilogue.  512 rows x 256 units
-// -> 256 blocks.  K order: lane group g of wave q owns the KW consecutive k
-// starting at q*4*KW + g*KW, the same k for the A and B operands.
+// -> 256 blocks.  K order: wave q owns the 4*KW consecutive k from q*4*KW, dealt
+// to its lane groups in 16-B chunks — MFMA s of lane group g takes
+// k = q*4*KW + 16*(s/4) + 4*g + s%4, the same k for the A and B operands — so one
+// 16-B load instruction of the four lane groups reads 64 contiguous bytes of a
+// row (one request; with KW-long runs per lane group it touched four 64-B
+// segments per instruction, and the sc1 hand-off loads, which skip L1, re-fetched
+// each segment four times).
 // MFMA maps (16x16x4 f32): A[l&15][k=l>>4], B[k=l>>4][l&15], D col=l&15, row=4(l>>4)+r.
 
 // forward: gh = h_in · W_hhᵀ for the (r, z, n) rows of the block's 16 units, then
@@ -238,22 +243,22 @@ __device__ __forceinline__ void gru_fwd_tile(int m0, int j0, const float* __rest
                                              f32x4 (&P)[4][6][64]) {
   constexpr int KW = H / 16;   // k per lane group and wave (4 groups x 4 waves x KW = H)
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
-  const int k0 = q * 4 * KW + g * KW;
+  const int kg = q * 4 * KW + 4 * g;   // + 4 s: the lane group's 16-B chunk of MFMAs s .. s + 3
   float a[2][KW];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     const int m = m0 + 16 * rt + c;
     const bool ok = m < M;
     const float mk = ok && masks ? masks[mask_idx ? mask_idx[m] : m] : 1.0f;
-    const float* src = hprev + (size_t)(ok ? m : 0) * H + k0;
+    const float* src = hprev + (size_t)(ok ? m : 0) * H + kg;
 #pragma unroll
     for (int s = 0; s < KW; s += 4) {
       f32x4 v;
       if constexpr (PUB)
         v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                          make_rsrc(hprev, (uint32_t)M * H * 4), ((ok ? m : 0) * H + k0 + s) * 4, 0, 16));
+                                          make_rsrc(hprev, (uint32_t)M * H * 4), ((ok ? m : 0) * H + kg + 4 * s) * 4, 0, 16));
       else
-        v = *reinterpret_cast<const f32x4*>(src + s);
+        v = *reinterpret_cast<const f32x4*>(src + 4 * s);
       v = ok ? v * mk : zero4();
       a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
     }
@@ -331,13 +336,13 @@ template <int H>
 __device__ __forceinline__ void gru_load_whh(const float* __restrict__ whh, int j0, float (&b)[3][H / 16]) {
   constexpr int KW = H / 16;
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
-  const int k0 = q * 4 * KW + g * KW;
+  const int kg = q * 4 * KW + 4 * g;   // gru_fwd_tile's K order
 #pragma unroll
   for (int gt = 0; gt < 3; ++gt) {
-    const float* src = whh + ((size_t)gt * H + j0 + c) * H + k0;
+    const float* src = whh + ((size_t)gt * H + j0 + c) * H + kg;
 #pragma unroll
     for (int s = 0; s < KW; s += 4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(src + s);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * s);
       b[gt][s] = v[0]; b[gt][s + 1] = v[1]; b[gt][s + 2] = v[2]; b[gt][s + 3] = v[3];
     }
   }
@@ -393,7 +398,7 @@ __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict_
   __shared__ int s_abort;
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
   const int j0 = blockIdx.y * 16, m0 = blockIdx.x * 32, grp = blockIdx.x, need = H / 16;
-  const int k0 = q * 4 * KW + g * KW;
+  const int kg = q * 4 * KW + 4 * g;   // gru_fwd_tile's K order
   if (threadIdx.x == 0) s_abort = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_abort) return;   // an earlier launch on these words timed out: its outputs (and ours) are invalid
@@ -477,10 +482,10 @@ __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict_
       for (int s = 0; s < KW; s += 4) {
         f32x4 v;
         if (t == 0)
-          v = *reinterpret_cast<const f32x4*>(h0 + (size_t)ra[rt] * H + k0 + s);
+          v = *reinterpret_cast<const f32x4*>(h0 + (size_t)ra[rt] * H + kg + 4 * s);
         else
           v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            rh, (int)((o - (size_t)n * H) + (size_t)ra[rt] * H + k0 + s) * 4, 0, 16));
+                                            rh, (int)((o - (size_t)n * H) + (size_t)ra[rt] * H + kg + 4 * s) * 4, 0, 16));
         v = oka[rt] ? v * mA[rt] : zero4();
         a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
       }
@@ -585,7 +590,7 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
   __shared__ f32x4 P[4][2][64];
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
-  const int k0 = q * 4 * KW + g * KW;
+  const int kg = q * 4 * KW + 4 * g;   // + half * 4 * KH + 4 s (gru_fwd_tile's chunked K order)
   // epilogue operands prefetched (in flight during the MFMAs)
   float pd[2], pm[2], pc[2][6];
 #pragma unroll
@@ -603,7 +608,7 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
 #pragma unroll
   for (int half = 0; half < NH; ++half) {
     float a[2][KH], b[KH];
-    const int kb = k0 + half * KH;
+    const int kb = kg + half * 4 * KH;
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
       const int m = m0 + 16 * rt + c;
@@ -611,14 +616,14 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
       const float* src = dgh + (size_t)(ok ? m : 0) * 3 * H + kb;
 #pragma unroll
       for (int s = 0; s < KH; s += 4) {
-        const f32x4 v = ok ? *reinterpret_cast<const f32x4*>(src + s) : zero4();
+        const f32x4 v = ok ? *reinterpret_cast<const f32x4*>(src + 4 * s) : zero4();
         a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
       }
     }
     const float* bs = whhT + (size_t)(j0 + c) * 3 * H + kb;
 #pragma unroll
     for (int s = 0; s < KH; s += 4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(bs + s);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(bs + 4 * s);
       b[s] = v[0]; b[s + 1] = v[1]; b[s + 2] = v[2]; b[s + 3] = v[3];
     }
 #pragma unroll
@@ -668,18 +673,20 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
   __shared__ int s_abort;
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
   const int grp = blockIdx.x, m0 = grp * 32, j0 = blockIdx.y * 16, need = H / 16;
-  const int k0 = q * 4 * KW + g * KW;
+  const int kg = q * 4 * KW + 4 * g;   // gru_step_bwd16_kernel's K order
   if (tid == 0) s_abort = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_abort) return;
-  float b[KW];   // W_hhᵀ row j0 + c, k0 .. k0 + KW - 1
+  float b[KW];   // W_hhᵀ row j0 + c: b[half * KH + s] at k = kg + half * 4 KH + 4 s (+ 0..3)
   {
-    const float* bs = whhT + (size_t)(j0 + c) * 3 * H + k0;
+    const float* bs = whhT + (size_t)(j0 + c) * 3 * H + kg;
 #pragma unroll
-    for (int s = 0; s < KW; s += 4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(bs + s);
-      b[s] = v[0]; b[s + 1] = v[1]; b[s + 2] = v[2]; b[s + 3] = v[3];
-    }
+    for (int half = 0; half < NH; ++half)
+#pragma unroll
+      for (int s = 0; s < KH; s += 4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(bs + half * 4 * KH + 4 * s);
+        b[half * KH + s] = v[0]; b[half * KH + s + 1] = v[1]; b[half * KH + s + 2] = v[2]; b[half * KH + s + 3] = v[3];
+      }
   }
   // L2 agreement: when every unit block of the row group runs on one XCD, dgh is
   // handed over through that XCD's L2: the producers store it plain (the line stays
@@ -800,7 +807,7 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
 #pragma unroll
     for (int half = 0; half < NH; ++half) {
       float a[2][KH];
-      const int kb = k0 + half * KH;
+      const int kb = kg + half * 4 * KH;
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
         const int m = m0 + 16 * rt + c;
@@ -808,7 +815,7 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
 #pragma unroll
         for (int s = 0; s < KH; s += 4) {
           f32x4 v = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((ok ? m : 0) * 3 * H + kb + s) * 4, 0, CP_LD));
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((ok ? m : 0) * 3 * H + kb + 4 * s) * 4, 0, CP_LD));
           v = ok ? v : zero4();
           a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
         }
