@@ -110,6 +110,17 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // elsewhere the two are interchangeable.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// One 1-KB LDS-DMA piece: lane i's 16 B from gsrc land at LDS byte lds_dst + 16 i
+// (inline asm: invisible to the compiler's waitcnt pass, so every user retires it
+// with its own vmcnt count, stated at the use)
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
 // Range-checked buffer stores: a store whose byte offset is out of the
 // resource's range (e.g. -1) is dropped by the hardware — predication without an
 // exec-mask branch.  dword3 0x00020000: raw 32-bit buffer on gfx9 (gfx950).

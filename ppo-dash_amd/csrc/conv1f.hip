@@ -53,7 +53,7 @@ constexpr int NPART = 5, PROWS = 20;
 // channels c and c + 1 of one k-step hit disjoint bank halves
 constexpr int CSTR = PROWS * IMG + 48, PLANE = 4 * CSTR;   // bf16 elements per plane of a part (6,912)
 constexpr int PSTR = 36;   // LDS row stride (floats) of the channel partials: 4 px apart -> 16 banks apart
-enum { SRC_F32 = 0, SRC_RGB = 1, SRC_U8 = 2 };   // U8: the 4-channel u8 rows (weight gradient only)
+enum { SRC_F32 = 0, SRC_RGB = 1 };
 
 // fl32(fl64((u - m) / s)) bit-exactly (see header): q = d·(1/s); the 29 bits a
 // rounding to fp32 drops decide; within 4 of the midpoint pattern, take d / s
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(512) void conv1_fwd_x6_kernel(const void* __restric
 }
 
 
-// Forward, full-K form (default; conv1_fwd tune 4 selects the K-split kernel
+// Forward, full-K form (fp32 rows; the RGB decode takes the K-split kernel
 // above): 10 waves, wave w = (column tile w & 1, row tile w >> 1) of the part
 // computes its 16 x 16 output tile over all 256 k (8 k-steps, one kernel row
 // each) with all 8 x 3 weight fragments resident (96 VGPRs), so no partial sums
@@ -652,8 +652,7 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
   // dbg (timing anatomy only, wrong results): 1 skips the MFMAs, 2 the staging,
   // 4 the global loads, 16 the stagger
   const bool no_mma = dbg & 1, no_put = dbg & 2, no_ld = dbg & 4;
-  constexpr int NPL = NP == 1 ? 1 : 3;                  // dz planes
-  constexpr int NPX = SRC == SRC_U8 ? 1 : NPL;          // image planes (u8 pixels are exact in bf16)
+  constexpr int NPL = NP == 1 ? 1 : 3;                  // dz and image planes
   __shared__ __attribute__((aligned(16))) uint16_t S[2][3][SPL];   // 3 planes even at NPL 1: the k-group scratch
   __shared__ __attribute__((aligned(16))) uint16_t D[2][NPL][DZPL];
   __shared__ __attribute__((aligned(16))) uint8_t R8[SRC == SRC_RGB ? RGBB + 16 : 16];
@@ -679,7 +678,6 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
 
   // ---------------- raw data in registers, one part ahead
   f32x4 xr[2];    // SRC_F32: the part's rows, 1,680 float4
-  uint32_t ur[2]; // SRC_U8: the part's rows, 1,680 4-pixel words
   float dv[8];    // dz item: 8 pixels of one channel
   auto fetch = [&](int it) __attribute__((always_inline)) {
     if (it >= nit || no_ld) return;
@@ -692,17 +690,6 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
         if (f < 1680) {
           const int c = f / 420, rem = f - 420 * c, yl = rem / 21, q = rem - 21 * yl;
           xr[j] = *reinterpret_cast<const f32x4*>(base + c * IMG2 + yl * IMG + 4 * q);
-        }
-      }
-    }
-    if constexpr (SRC == SRC_U8) {
-      const uint8_t* base = reinterpret_cast<const uint8_t*>(obs) + (long long)rowtab[k] * (4LL * IMG2) + p * 16 * IMG;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int f = tid + 1024 * j;
-        if (f < 1680) {
-          const int c = f / 420, rem = f - 420 * c, yl = rem / 21, q = rem - 21 * yl;
-          ur[j] = *reinterpret_cast<const uint32_t*>(base + c * IMG2 + yl * IMG + 4 * q);
         }
       }
     }
@@ -752,18 +739,6 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
           for (int pl = 0; pl < NPL; ++pl) *reinterpret_cast<uint2*>(&S[st][pl][off]) = o[pl];
         }
       }
-    } else if constexpr (SRC == SRC_U8) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int f = tid + 1024 * j;
-        if (f < 1680) {   // 4 pixels -> 4 exact bf16 (the high halves of the fp32 integers)
-          const int c = f / 420, rem = f - 420 * c, yl = rem / 21, q = rem - 21 * yl;
-          const f32x4 v = to_f32x4(ur[j]);
-          const uint2 o = {__builtin_amdgcn_perm(__float_as_uint(v[1]), __float_as_uint(v[0]), 0x07060302u),
-                           __builtin_amdgcn_perm(__float_as_uint(v[3]), __float_as_uint(v[2]), 0x07060302u)};
-          *reinterpret_cast<uint2*>(&S[st][0][c * SCH + yl * SRS + 4 * q]) = o;
-        }
-      }
     } else {
       rgb_item<NPL>(tid, it % NPART, R8, mean != nullptr, mr, stdv, rstd, &S[st][0][0], SCH, SPL, SRS);
     }
@@ -810,7 +785,7 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
       for (int t = 0; t < 2; ++t) {   // kernel-row half t: ky = 4 t + (column >> 3)
         bf16x8 b[3];
 #pragma unroll
-        for (int pl = 0; pl < NPX; ++pl) {
+        for (int pl = 0; pl < NPL; ++pl) {
           s16x4 v[2];
 #pragma unroll
           for (int rd = 0; rd < 2; ++rd)
@@ -818,12 +793,7 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_x6_kernel(const float* __res
                 (__attribute__((address_space(3))) s16x4*)(&S[st][pl][ro[rd] + 4 * t * SRS]));
           b[pl] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v[0], v[1], 0, 1, 2, 3, 4, 5, 6, 7));
         }
-        if constexpr (SRC == SRC_U8) {   // dz (l, m, h) x the exact pixels, smallest first
-#pragma unroll
-          for (int pl = NPL - 1; pl >= 0; --pl) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pl], b[0], acc[t], 0, 0, 0);
-        } else {
-          acc[t] = mma32_set<NP>(a, b, acc[t]);
-        }
+        acc[t] = mma32_set<NP>(a, b, acc[t]);
       }
     }
   };
@@ -935,10 +905,8 @@ static int conv1_fwd_x6_launch(int src, const void* obs, const int64_t* idx, lon
   const int dbg = ppo_tune_get("stagger") >> 4;   // timing anatomy (kbench --tune stagger=16*dbg)
   // kernel form: fp32 rows take the full-K 10-wave kernel (3.3 vs 3.9 ms per 65,536-image
   // minibatch); RGB frames the K-split 8-wave one (5.8-5.9 vs 6.5 ms: the full-K form's
-  // 96 weight VGPRs plus the decode's means spill there).  conv1_fwd tune 4 / 5 forces
-  // the K-split / full-K form (A/B)
-  const int tv = ppo_tune_get("conv1_fwd");
-  const bool ksplit = tv == 4 || (tv != 5 && src == SRC_RGB);
+  // 96 weight VGPRs plus the decode's means spill there)
+  const bool ksplit = src == SRC_RGB;
 #define L1(S, M, N)                                                                                           \
   if (ksplit) conv1_fwd_x6_kernel<S, M, N><<<nb, 512, 0, st>>>(obs, idx, row0, B, mean, stdv, rs, w1, b1, out, mbits, dbg); \
   else conv1_fwd_x6w_kernel<S, M, N><<<nb, 640, 0, st>>>(obs, idx, row0, B, mean, stdv, rs, w1, b1, out, mbits, dbg)
@@ -989,8 +957,7 @@ static int conv1_wgrad_x6_launch(int src, const float* dz1, const void* obs, con
   const int np = ppo_tune_get("products");
   hipStream_t st = as_stream(stream);
   int slot;
-  const bool prof = ppo_prof_begin(src == SRC_F32 ? "conv1_wgrad_f32" : src == SRC_RGB ? "conv1_wgrad_rgb"
-                                                                                    : "conv1_wgrad_u8", st, &slot);
+  const bool prof = ppo_prof_begin(src == SRC_F32 ? "conv1_wgrad_f32" : "conv1_wgrad_rgb", st, &slot);
   const double rs = 1.0 / stdv;
   const int dbg = ppo_tune_get("stagger") >> 4;
 #define W1(S, N) \

@@ -35,15 +35,6 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// One 1-KB LDS-DMA piece (inline asm: invisible to the compiler's waitcnt pass,
-// retired by the explicit / in-order vmcnt waits described at the use).
-__device__ __forceinline__ void glds16_c1(const void* gsrc, uint32_t lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
 
 // The same algorithm with the u8 image staged by LDS-DMA (ppo_tune_set("conv1_wgrad", 8)):
 // the raw image (28,224 B) lands in a 28-KB LDS buffer beside the two E stages
@@ -79,7 +70,7 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw2_kernel(const float* _
     for (int i = 0; i < 4; ++i) {
       const int pc = min(wave + 8 * i, 27);
       const int off = min(pc * 1024 + lane * 16, IMGB - 16);
-      glds16_c1(img + off, __builtin_amdgcn_readfirstlane(raw_lds + pc * 1024));
+      glds16(img + off, __builtin_amdgcn_readfirstlane(raw_lds + pc * 1024));
     }
   };
   auto put = [&](int st) {   // RAW -> E[st]: u8 -> bf16 (exact), de-interleaved by x mod 4

@@ -228,14 +228,6 @@ __global__ __launch_bounds__(512) void conv1_fwd_rgbaff_kernel(const uint8_t* __
 // summed over c with k_c and transposed) and the direct pass the bias partials;
 // rgbaff_wfinal subtracts the means' share from slab 0.  Slab format and bias as
 // every conv1 wgrad (the engine's ppo_wgrad_reduce sums the Z slabs, scale 1).
-__device__ __forceinline__ void glds16_ra(const void* gsrc, uint32_t lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
-
 template <bool TRANS>
 __global__ __launch_bounds__(512) void conv1_wgrad_rgbaff_kernel(const float* __restrict__ dz1,
                                                                  const uint8_t* __restrict__ frames,
@@ -259,7 +251,7 @@ __global__ __launch_bounds__(512) void conv1_wgrad_rgbaff_kernel(const float* __
     for (int i = 0; i < 3; ++i) {
       const int pc = min(wave + 8 * i, NPC - 1);
       const int off = min(pc * 1024 + lane * 16, RA_FB - 16);
-      glds16_ra(img + off, __builtin_amdgcn_readfirstlane(raw_lds + pc * 1024));
+      glds16(img + off, __builtin_amdgcn_readfirstlane(raw_lds + pc * 1024));
     }
   };
   // RAW (HWC bytes) -> E[st][c][y][dx][X] = plane value at (y, 4X + dx), bf16 (exact);
