@@ -22,11 +22,75 @@
 #include <mutex>
 #include <type_traits>
 
-#include "igemm.h"
+#include "igemm_x9.h"
 
 namespace {
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// W_hh products of the register-tiled step kernels on the matrix cores.  Where a
+// wave's K run fills whole 32-k steps (BF: the forward for H = 128, 256, 512, the
+// BPTT's K halves for H = 128, 256, 512) both operands are split exactly into
+// three bf16 parts and the six part products of the convolutions' fp32 emulation
+// (DESIGN.md §3, mma9<.., 6>) run on v_mfma_f32_16x16x32_bf16: 6 x 16 cycles per
+// 32 k instead of 8 x 32 on v_mfma_f32_16x16x4_f32 (2.7x the rate).  A 32-k step
+// takes the lane's own consecutive 16-B chunks 2 kk, 2 kk + 1 (the lane group's k
+// of the chunked K order below), for the A and B operands alike, so the sum runs
+// over the same k.  Otherwise (H = 64) the exact fp32 MFMAs remain.
+template <int KW, bool BF>
+struct GruRow {   // one B row of KW k in the chunked K order
+  float f[BF ? 1 : KW];
+  Frag3 p[BF ? KW / 8 : 1];
+};
+template <int KW, bool BF>
+__device__ __forceinline__ void gru_row_set(const float (&v)[KW], GruRow<KW, BF>& r) {
+  if constexpr (BF) {
+#pragma unroll
+    for (int kk = 0; kk < KW / 8; ++kk)
+      split8(f32x4{v[8 * kk], v[8 * kk + 1], v[8 * kk + 2], v[8 * kk + 3]},
+             f32x4{v[8 * kk + 4], v[8 * kk + 5], v[8 * kk + 6], v[8 * kk + 7]}, r.p[kk], false);
+  } else {
+#pragma unroll
+    for (int s = 0; s < KW; ++s) r.f[s] = v[s];
+  }
+}
+// acc[rt][g] += a[rt][0 .. KA) · w[g] over its k OFF .. OFF + KA (rt: the block's two
+// 16-row tiles); the accumulation order is fixed by (KA, OFF, NG) alone
+template <int KA, int OFF, int NG, int KW, bool BF>
+__device__ __forceinline__ void gru_mma(const float (&a)[2][KA], const GruRow<KW, BF> (&w)[NG], f32x4 (&acc)[2][NG]) {
+  if constexpr (BF) {
+    static_assert(KA % 8 == 0 && OFF % 8 == 0, "whole 32-k steps");
+#pragma unroll
+    for (int kk = 0; kk < KA / 8; ++kk)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        Frag3 fa;
+#ifdef GRU_NOSPLIT   // timing anatomy only (wrong results): A's planes without the split VALU
+        {
+          uint32_t w[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            w[i] = __builtin_amdgcn_perm(__float_as_uint(a[rt][8 * kk + 2 * i + 1]), __float_as_uint(a[rt][8 * kk + 2 * i]),
+                                         0x07060302u);
+          fa.h = fa.m = fa.l = __builtin_bit_cast(bf16x8, uint4{w[0], w[1], w[2], w[3]});
+        }
+#else
+        split8(f32x4{a[rt][8 * kk], a[rt][8 * kk + 1], a[rt][8 * kk + 2], a[rt][8 * kk + 3]},
+               f32x4{a[rt][8 * kk + 4], a[rt][8 * kk + 5], a[rt][8 * kk + 6], a[rt][8 * kk + 7]}, fa, false);
+#endif
+#pragma unroll
+        for (int g = 0; g < NG; ++g) acc[rt][g] = mma9<false, false, 6>(fa, w[g].p[OFF / 8 + kk], acc[rt][g]);
+      }
+  } else {
+#pragma unroll
+    for (int s = 0; s < KA; ++s)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+          acc[rt][g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], w[g].f[OFF + s], acc[rt][g], 0, 0, 0);
+  }
+}
 
 // gh tile with the fused GRU cell.  B rows n = jt*96 + g*32 + jj <-> W_hh row g*H + jt*32 + jj.
 template <class C_>
@@ -236,7 +300,7 @@ using CfgGruB = Cfg<64, 64, 2, 2, true, true>;
 template <int H, bool PUB = false>
 __device__ __forceinline__ void gru_fwd_tile(int m0, int j0, const float* __restrict__ hprev,
                                              const float* __restrict__ masks, const int64_t* __restrict__ mask_idx,
-                                             const float (&b)[3][H / 16], const float* __restrict__ bhh,
+                                             const GruRow<H / 16, (H / 16) % 8 == 0> (&b)[3], const float* __restrict__ bhh,
                                              const float* __restrict__ gi, int M, float* __restrict__ hout,
                                              float* __restrict__ sr, float* __restrict__ sz, float* __restrict__ sn,
                                              float* __restrict__ sghn, float* __restrict__ shin,
@@ -287,13 +351,7 @@ __device__ __forceinline__ void gru_fwd_tile(int m0, int j0, const float* __rest
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
     for (int gt = 0; gt < 3; ++gt) acc[rt][gt] = zero4();
-#pragma unroll
-  for (int s = 0; s < KW; ++s)
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int gt = 0; gt < 3; ++gt)
-        acc[rt][gt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], b[gt][s], acc[rt][gt], 0, 0, 0);
+  gru_mma<KW, 0>(a, b, acc);
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -333,18 +391,21 @@ __device__ __forceinline__ void gru_fwd_tile(int m0, int j0, const float* __rest
 }
 
 template <int H>
-__device__ __forceinline__ void gru_load_whh(const float* __restrict__ whh, int j0, float (&b)[3][H / 16]) {
+__device__ __forceinline__ void gru_load_whh(const float* __restrict__ whh, int j0,
+                                             GruRow<H / 16, (H / 16) % 8 == 0> (&b)[3]) {
   constexpr int KW = H / 16;
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
   const int kg = q * 4 * KW + 4 * g;   // gru_fwd_tile's K order
 #pragma unroll
   for (int gt = 0; gt < 3; ++gt) {
     const float* src = whh + ((size_t)gt * H + j0 + c) * H + kg;
+    float v[KW];
 #pragma unroll
     for (int s = 0; s < KW; s += 4) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(src + 4 * s);
-      b[gt][s] = v[0]; b[gt][s + 1] = v[1]; b[gt][s + 2] = v[2]; b[gt][s + 3] = v[3];
+      const f32x4 x = *reinterpret_cast<const f32x4*>(src + 4 * s);
+      v[s] = x[0]; v[s + 1] = x[1]; v[s + 2] = x[2]; v[s + 3] = x[3];
     }
+    gru_row_set(v, b[gt]);
   }
 }
 
@@ -358,7 +419,7 @@ __global__ __launch_bounds__(256) void gru_step16_kernel(const float* __restrict
                                                          float* __restrict__ sn, float* __restrict__ sghn,
                                                          float* __restrict__ shin) {
   __shared__ f32x4 P[4][6][64];
-  float b[3][H / 16];
+  GruRow<H / 16, (H / 16) % 8 == 0> b[3];
   gru_load_whh<H>(whh, blockIdx.y * 16, b);
   gru_fwd_tile<H>(blockIdx.x * 32, blockIdx.y * 16, hprev, masks, mask_idx, b, bhh, gi, M, hout, sr, sz, sn, sghn,
                   shin, P);
@@ -402,7 +463,7 @@ __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict_
   if (threadIdx.x == 0) s_abort = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_abort) return;   // an earlier launch on these words timed out: its outputs (and ours) are invalid
-  float b[3][H / 16];
+  GruRow<KW, KW % 8 == 0> b[3];
   gru_load_whh<H>(whh, j0, b);
   const bool sv = sr != nullptr;
   const auto rh = make_rsrc(hout, (uint32_t)((size_t)T * n * H * 4 < 0xffffffffu ? (size_t)T * n * H * 4 : 0xffffffffu));
@@ -501,13 +562,7 @@ __global__ __launch_bounds__(256) void gru_seq16_kernel(const float* __restrict_
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int gt = 0; gt < 3; ++gt) acc[rt][gt] = zero4();
-#pragma unroll
-    for (int s = 0; s < KW; ++s)
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int gt = 0; gt < 3; ++gt)
-          acc[rt][gt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], b[gt][s], acc[rt][gt], 0, 0, 0);
+    gru_mma<KW, 0>(a, b, acc);   // gru_fwd_tile's products and order
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -586,7 +641,8 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
                                                              float* __restrict__ carry, int M,
                                                              const CellPrev cp) {
   constexpr int KW = 3 * H / 16;
-  constexpr int NH = KW % 8 == 0 ? 2 : 1, KH = KW / NH;   // K halves keep the operand registers small
+  constexpr int NH = KW % 16 == 0 ? 2 : 1, KH = KW / NH;   // K halves keep the operand registers small
+  constexpr bool BF = KH % 8 == 0;                         // split-bf16 products (gru_mma)
   __shared__ f32x4 P[4][2][64];
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.x * 32, j0 = blockIdx.y * 16;
@@ -604,7 +660,7 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
       pc[e][3] = cp.n[o]; pc[e][4] = cp.ghn[o]; pc[e][5] = cp.hin[o];
     }
   }
-  f32x4 acc[2] = {zero4(), zero4()};
+  f32x4 acc[2][1] = {{zero4()}, {zero4()}};
 #pragma unroll
   for (int half = 0; half < NH; ++half) {
     float a[2][KH], b[KH];
@@ -626,13 +682,12 @@ __global__ __launch_bounds__(256) void gru_step_bwd16_kernel(const float* __rest
       const f32x4 v = *reinterpret_cast<const f32x4*>(bs + 4 * s);
       b[s] = v[0]; b[s + 1] = v[1]; b[s + 2] = v[2]; b[s + 3] = v[3];
     }
-#pragma unroll
-    for (int s = 0; s < KH; ++s)
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], b[s], acc[rt], 0, 0, 0);
+    GruRow<KH, BF> w[1];
+    gru_row_set(b, w[0]);
+    gru_mma<KH, 0>(a, w, acc);
   }
-  P[q][0][lane] = acc[0];
-  P[q][1][lane] = acc[1];
+  P[q][0][lane] = acc[0][0];
+  P[q][1][lane] = acc[1][0];
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
@@ -668,7 +723,8 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
     float* __restrict__ dgi, float* __restrict__ dgh, float* __restrict__ dhz, float* __restrict__ carry,
     int* __restrict__ cnt, int* __restrict__ err, int spin_max, int l2_mode) {
   constexpr int KW = 3 * H / 16;
-  constexpr int NH = KW % 8 == 0 ? 2 : 1, KH = KW / NH;
+  constexpr int NH = KW % 16 == 0 ? 2 : 1, KH = KW / NH;
+  constexpr bool BF = KH % 8 == 0;
   __shared__ f32x4 P[4][2][64];
   __shared__ int s_abort;
   const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6, c = lane & 15, g = lane >> 4;
@@ -677,8 +733,9 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
   if (tid == 0) s_abort = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_abort) return;
-  float b[KW];   // W_hhᵀ row j0 + c: b[half * KH + s] at k = kg + half * 4 KH + 4 s (+ 0..3)
+  GruRow<KW, BF> w[1];   // W_hhᵀ row j0 + c: value half * KH + s at k = kg + half * 4 KH + 4 s (+ 0..3)
   {
+    float b[KW];
     const float* bs = whhT + (size_t)(j0 + c) * 3 * H + kg;
 #pragma unroll
     for (int half = 0; half < NH; ++half)
@@ -687,6 +744,7 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
         const f32x4 v = *reinterpret_cast<const f32x4*>(bs + half * 4 * KH + 4 * s);
         b[half * KH + s] = v[0]; b[half * KH + s + 1] = v[1]; b[half * KH + s + 2] = v[2]; b[half * KH + s + 3] = v[3];
       }
+    gru_row_set(b, w[0]);
   }
   // L2 agreement: when every unit block of the row group runs on one XCD, dgh is
   // handed over through that XCD's L2: the producers store it plain (the line stays
@@ -803,7 +861,7 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
     }
     const size_t o = (size_t)t * n * H, op = o - (size_t)n * H;
     const auto rs = make_rsrc(dgh + 3 * o, gbytes);
-    f32x4 acc[2] = {zero4(), zero4()};
+    f32x4 acc[2][1] = {{zero4()}, {zero4()}};
 #pragma unroll
     for (int half = 0; half < NH; ++half) {
       float a[2][KH];
@@ -820,14 +878,11 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
           a[rt][s] = v[0]; a[rt][s + 1] = v[1]; a[rt][s + 2] = v[2]; a[rt][s + 3] = v[3];
         }
       }
-#pragma unroll
-      for (int s = 0; s < KH; ++s)
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-          acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][s], b[half * KH + s], acc[rt], 0, 0, 0);
+      if (half == 0) gru_mma<KH, 0>(a, w, acc);   // the step kernel's products and order
+      else gru_mma<KH, KH>(a, w, acc);
     }
-    P[q][0][lane] = acc[0];
-    P[q][1][lane] = acc[1];
+    P[q][0][lane] = acc[0][0];
+    P[q][1][lane] = acc[1][0];
     __syncthreads();
     float* dgh_p = dgh + 3 * op;
     const auto rsp = make_rsrc(dgh_p, gbytes);
