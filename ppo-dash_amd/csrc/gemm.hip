@@ -82,11 +82,11 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
                                                                const float* __restrict__ bias,
                                                                float* __restrict__ out,
                                                                uint16_t* __restrict__ mbits) {
-  constexpr int NPX = C * IMG2, CH = NPX / 16, K = C * 64, KS = K / 32, PER = (CH + 511) / 512, NT = 7;
+  constexpr int NPX = C * IMG2, CH = NPX / 16, K = C * 64, KS = K / 32, PER = (CH + 511) / 512;
   static_assert(NPX % 16 == 0, "16-pixel chunks");
   __shared__ __attribute__((aligned(16))) uint16_t img[2][NPX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ct = wave & 1, rq = wave >> 1, ntile = rq == 0 ? 7 : 6;
+  const int ct = wave & 1, rq = wave >> 1;
   const int i16 = lane & 15, g = lane >> 4;
   const int col = ct * 16 + i16;
   const float bv = bias[col];
@@ -144,56 +144,62 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
   for (; b < B; b += G) {
     if (b + G < B) put(cur ^ 1);          // read two iterations ago; the last barrier retired it
     if (b + 2 * G < B) fetch(b + 2 * G);
-    const uint16_t* I = img[cur];
-    f32x4 acc[NT];
+    // the wave's row tiles rq + 4t: 7 for rq 0, 6 otherwise (25 per image), as a
+    // compile-time count, so no MFMA is issued for a tile the wave does not own
+    // (with a run-time bound the compiler issued them all and selected: 1,344
+    // instead of 1,200 MFMAs per image)
+    auto tiles = [&](auto ntc) __attribute__((always_inline)) {
+      constexpr int NTL = decltype(ntc)::value;
+      const uint16_t* I = img[cur];
+      f32x4 acc[NTL];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = zero4();
-    int pix[NT];   // pixel offset of this lane's output row, per row tile
+      for (int t = 0; t < NTL; ++t) acc[t] = zero4();
+      int pix[NTL];   // pixel offset of this lane's output row, per row tile
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int row = (rq + 4 * t) * 16 + i16, oy = row / 20, ox = row - oy * 20;
-      pix[t] = oy * (4 * IMG) + ox * 4;
-    }
+      for (int t = 0; t < NTL; ++t) {
+        const int row = (rq + 4 * t) * 16 + i16, oy = row / 20, ox = row - oy * 20;
+        pix[t] = oy * (4 * IMG) + ox * 4;
+      }
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int k0 = 32 * s + 8 * g;
-      const uint16_t* Is = I + (k0 >> 6) * IMG2 + ((k0 >> 3) & 7) * IMG;
-      bf16x8 a[NT];
+      for (int s = 0; s < KS; ++s) {
+        const int k0 = 32 * s + 8 * g;
+        const uint16_t* Is = I + (k0 >> 6) * IMG2 + ((k0 >> 3) & 7) * IMG;
+        bf16x8 a[NTL];
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        if (t < ntile) {
+        for (int t = 0; t < NTL; ++t) {
           const uint2* p2 = reinterpret_cast<const uint2*>(Is + pix[t]);   // 8-B aligned: 4ox bf16
           const uint2 lo = p2[0], hi = p2[1];
-          const uint4 v = uint4{lo.x, lo.y, hi.x, hi.y};
-          a[t] = __builtin_bit_cast(bf16x8, v);
+          a[t] = __builtin_bit_cast(bf16x8, uint4{lo.x, lo.y, hi.x, hi.y});
         }
 #pragma unroll
-      for (int part = 0; part < NPW; ++part)
+        for (int part = 0; part < NPW; ++part)
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-          if (t < ntile) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t], wf[part][s], acc[t], 0, 0, 0);
-    }
-    float* o = out + (size_t)b * (400 * 32) + col;
+          for (int t = 0; t < NTL; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t], wf[part][s], acc[t], 0, 0, 0);
+      }
+      float* o = out + (size_t)b * (400 * 32) + col;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-      if (t < ntile) {
-        const int rt = rq + 4 * t;
-        uint64_t bal[4];
+      for (int t = 0; t < NTL; ++t) {
+          const int rt = rq + 4 * t;
+          uint64_t bal[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = fmaxf(acc[t][r] * (1.0f / 255.0f) + bv, 0.f);
-          o[(rt * 16 + 4 * g + r) * 32] = v;
-          if constexpr (MASK) bal[r] = __builtin_amdgcn_ballot_w64(v > 0.f);
-        }
-        if constexpr (MASK) {   // ReLU mask bits: lane (g, i16) of ballot r -> pixel 16 rt + 4g + r,
-          // channel 16 ct + i16; lane j < 16 stores pixel 16 rt + j's 16 bits (one store per tile)
-          if (lane < 16) {
-            const int r = lane & 3, gg = lane >> 2;
-            const uint64_t bsel = r == 0 ? bal[0] : r == 1 ? bal[1] : r == 2 ? bal[2] : bal[3];
-            mbits[((size_t)b * 400 + rt * 16 + lane) * 2 + ct] = (uint16_t)(bsel >> (16 * gg));
+          for (int r = 0; r < 4; ++r) {
+            const float v = fmaxf(acc[t][r] * (1.0f / 255.0f) + bv, 0.f);
+            o[(rt * 16 + 4 * g + r) * 32] = v;
+            if constexpr (MASK) bal[r] = __builtin_amdgcn_ballot_w64(v > 0.f);
+          }
+          if constexpr (MASK) {   // ReLU mask bits: lane (g, i16) of ballot r -> pixel 16 rt + 4g + r,
+            // channel 16 ct + i16; lane j < 16 stores pixel 16 rt + j's 16 bits (one store per tile)
+            if (lane < 16) {
+              const int r = lane & 3, gg = lane >> 2;
+              const uint64_t bsel = r == 0 ? bal[0] : r == 1 ? bal[1] : r == 2 ? bal[2] : bal[3];
+              mbits[((size_t)b * 400 + rt * 16 + lane) * 2 + ct] = (uint16_t)(bsel >> (16 * gg));
+            }
           }
         }
-      }
+    };
+    if (rq == 0) tiles(std::integral_constant<int, 7>{});
+    else tiles(std::integral_constant<int, 6>{});
     __syncthreads();   // every wave is done with img[cur]; img[cur ^ 1] is complete
     cur ^= 1;
   }
