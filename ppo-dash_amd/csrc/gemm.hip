@@ -1864,6 +1864,7 @@ using V32_0 = Cfg<256, 32, 4, 1, true, true>;           // 4 waves x 64 rows, 46
 // exact-split bf16 core (igemm_x9.h)
 using X64 = CfgX<128, 64, 2, 2, true, true>;          // N = 64: waves of 64x32
 using X128 = CfgX<128, 128, 2, 2, true, true>;        // N >= 128: waves of 64x64
+using X64s = CfgX<64, 64, 2, 2, true, true>;          // few 128 x 128 tiles (rollout rows): waves of 32x32
 using XW64 = CfgX<64, 128, 2, 2, false, false, true>;   // wgrad, 64 output channels
 using XP128 = CfgX<128, 128, 4, 1, true, true, false, false, false, true>;  // B from planes, waves 32x128
 using XP128w8 = CfgX<128, 128, 8, 1, true, true, false, false, false, true>;      // 8 waves of 16x128
@@ -2147,12 +2148,21 @@ PPO_API int ppo_linear_fwd_ex(const float* x, const int64_t* idx, int M, int K, 
       p.idx = idx;
       return launch_x9(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);
     }
-    DenseReluFwd<X128> p;
-    p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = act;
-    p.idx = idx;
-    p.vec = N % 4 == 0 && (ldo ? ldo : N) % 4 == 0 && ((uintptr_t)out & 15) == 0 &&
-            (b == nullptr || ((uintptr_t)b & 15) == 0);
-    return launch_x9(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);
+#define PPO_LEX(CFG)                                                                                       \
+  {                                                                                                        \
+    DenseReluFwd<CFG> p;                                                                                   \
+    p.x = x; p.w = w; p.bias = b; p.out = out; p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldo = ldo; p.relu = act; \
+    p.idx = idx;                                                                                           \
+    p.vec = N % 4 == 0 && (ldo ? ldo : N) % 4 == 0 && ((uintptr_t)out & 15) == 0 &&                        \
+            (b == nullptr || ((uintptr_t)b & 15) == 0);                                                    \
+    return launch_x9(p, M, N, 1, as_stream(stream), "linear_fwd_ex", 2.0 * M * N * K);                     \
+  }
+    // rollout-sized M (the GRU input projection at 4,096 rows: 192 tiles of 128 x 128 for
+    // 256 CUs) takes 64 x 64 tiles
+    // 0.024 vs 0.028-0.031 ms at 4,096 x 272 x 768 (profiles/r05_m_gi.log)
+    if (((M + 127LL) / 128) * ((N + 127) / 128) < 2LL * device_cus()) PPO_LEX(X64s)
+    PPO_LEX(X128)
+#undef PPO_LEX
   }
   if (N % 128 == 0) {
     DenseReluFwd<CfgN128> p;

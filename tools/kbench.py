@@ -80,6 +80,9 @@ def main():
     z4 = a.z4 or z4
     fws = torch.empty(max(call("ppo_fc_fwd_ws_bytes", B, H) // 4, 4), device=dev)
     z2c = a.z2 or max(n_cu, -(-B // 512))   # the engine's split for the image-resident conv2 wgrad
+    gru = any(k.startswith("gru_") for k in a.only.split(","))
+    gx, gwih, gbih = (rn(B * 272, sc=1.0), rn(768 * 272), rn(768)) if gru else (None, None, None)
+    ggi = torch.empty(B * 768, device=dev) if gru else None
     hw = rn(9 * H + 9, sc=0.03)                       # heads: wc [H], bc, wa [8][H], ba [8]
     hv = torch.empty(3 * B, device=dev)
     ha = torch.empty(B, dtype=torch.int64, device=dev)
@@ -149,6 +152,9 @@ def main():
         "conv1_wgrad_rgb": (lambda: call("ppo_conv1_wgrad_rgb", dz1.data_ptr(), frames.data_ptr(), idx.data_ptr(), 0,
                                          B, mean.data_ptr(), 36.31282043457031, z1c, slab.data_ptr(),
                                          slab_b.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
+        # the recurrent trunk's GRU input projection gi = x_pad · W_ihᵀ + b (c5: K = 272, N = 768)
+        "gru_gi": (lambda: call("ppo_linear_fwd_ex", gx.data_ptr(), None, B, 272, 272, gwih.data_ptr(),
+                                gbih.data_ptr(), 768, ggi.data_ptr(), 768, 0, s), 2.0 * B * 272 * 768),
         "conv1_wreduce": (lambda: call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), z1, 32, 256, 0, 0, 0,
                                        gw.data_ptr(), gb.data_ptr(), 1.0 / 255, 0, s), 0.0),
     }
