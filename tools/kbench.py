@@ -82,7 +82,9 @@ def main():
     z2c = a.z2 or max(n_cu, -(-B // 512))   # the engine's split for the image-resident conv2 wgrad
     gru = any(k.startswith("gru_") for k in a.only.split(","))
     gx, gwih, gbih = (rn(B * 272, sc=1.0), rn(768 * 272), rn(768)) if gru else (None, None, None)
-    ggi = torch.empty(B * 768, device=dev) if gru else None
+    ggi = rn(B * 768, sc=1.0) if gru else None
+    ghp, gho = (rn(B * 256, sc=0.5), torch.empty(B * 256, device=dev)) if gru else (None, None)
+    gwhh, gbhh = (rn(768 * 256), rn(768)) if gru else (None, None)
     hw = rn(9 * H + 9, sc=0.03)                       # heads: wc [H], bc, wa [8][H], ba [8]
     hv = torch.empty(3 * B, device=dev)
     ha = torch.empty(B, dtype=torch.int64, device=dev)
@@ -155,6 +157,10 @@ def main():
         # the recurrent trunk's GRU input projection gi = x_pad · W_ihᵀ + b (c5: K = 272, N = 768)
         "gru_gi": (lambda: call("ppo_linear_fwd_ex", gx.data_ptr(), None, B, 272, 272, gwih.data_ptr(),
                                 gbih.data_ptr(), 768, ggi.data_ptr(), 768, 0, s), 2.0 * B * 272 * 768),
+        # the rollout's GRU step (c5: H = 256)
+        "gru_step": (lambda: call("ppo_gru_step_fwd", ghp.data_ptr(), None, None, gwhh.data_ptr(), gbhh.data_ptr(),
+                                  ggi.data_ptr(), B, 256, gho.data_ptr(), None, None, None, None, None, s),
+                     2.0 * B * 768 * 256),
         "conv1_wreduce": (lambda: call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), z1, 32, 256, 0, 0, 0,
                                        gw.data_ptr(), gb.data_ptr(), 1.0 / 255, 0, s), 0.0),
     }
