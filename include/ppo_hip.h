@@ -156,6 +156,14 @@ int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const float* b2
                        void* stream);
 /* model.py:179 Conv2d(64,32,3,s1)+ReLU */
 int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream);
+/* conv1 -> conv2 -> conv3 forward of u8 4-channel observation rows (model.py:177-179) in
+ * one persistent launch: a1 / a2 / a3 bit-identical to ppo_conv1_fwd, ppo_conv2_fwd and
+ * ppo_conv3_fwd; m1 / m2 both NULL or both given (the ReLU mask bits of
+ * ppo_conv1_fwd_mask / ppo_conv2_fwd_mask).  Replaces the trunk's three launches
+ * (model.py:177-179 as one call). */
+int ppo_trunk_fwd(const uint8_t* obs, const int64_t* idx, long long row0, int B, const float* w1, const float* b1,
+                  float* a1, uint32_t* m1, const float* w2p, const float* b2, float* a2, uint64_t* m2,
+                  const float* w3p, const float* b3, float* a3, void* stream);
 /* model.py:180 Linear(1568,H)+ReLU (generic Linear+ReLU) */
 /* model.py:181 CNNBase fc + ReLU from the packed W4p segment (ppo_pack_weights; its bf16 planes follow it):
  * out[m * ldo + n] = relu(x[m] · W4p[n] + b[n]), x [M][1568] (p, c) order */

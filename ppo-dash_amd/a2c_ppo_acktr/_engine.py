@@ -18,11 +18,16 @@ Per PPO minibatch (every box is a libppo_hip.so kernel):
 """
 import contextlib
 
+import os
+
 import torch
 
 from . import _dist
 from ._hip import call, ptr, stream
 
+# ppo_trunk_fwd (conv1 -> conv2 -> conv3 in one launch) for u8 rows; PPO_FUSED_TRUNK=0
+# runs the three launches (same-box A/B, tools/ab_bench.sh)
+FUSED_TRUNK = os.environ.get("PPO_FUSED_TRUNK", "1") != "0"
 FEAT = 32 * 7 * 7  # conv3 output, flattened
 
 
@@ -236,19 +241,26 @@ class CNNEngine:
         if out is None:
             out, ldo = ws.get("h", B * self.H, device=dev), self.H
         s = stream()
-        if ws is self.ws["train"]:
-            # training forward: conv1 and conv2 also write their ReLU masks as bits,
-            # read by the conv2 / conv3 dgrads instead of the fp32 activations
-            m1 = ws.get("m1bits", B * 400, dtype=torch.int32, device=dev)
-            m2 = ws.get("m2bits", B * 81, dtype=torch.int64, device=dev)
-            self._conv1(obs, idx, B, a1, m1[:B * 400], s)
-            call("ppo_conv2_fwd_mask", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), m2.data_ptr(),
-                 s)
-            self._mask_rows = B
+        train = ws is self.ws["train"]
+        # training forward: conv1 and conv2 also write their ReLU masks as bits,
+        # read by the conv2 / conv3 dgrads instead of the fp32 activations
+        m1 = ws.get("m1bits", B * 400, dtype=torch.int32, device=dev) if train else None
+        m2 = ws.get("m2bits", B * 81, dtype=torch.int64, device=dev) if train else None
+        if obs.dtype == torch.uint8 and self.C == 4 and not self._is_rgb(obs) and FUSED_TRUNK:
+            # u8 rows: conv1 -> conv2 -> conv3 in one persistent launch (ppo_trunk_fwd)
+            call("ppo_trunk_fwd", obs.data_ptr(), ptr(idx, torch.int64, "idx"), 0, B, self.pv(self.W1),
+                 self.pv(self.B1), a1.data_ptr(), ptr(m1), self.pk(0), self.pv(self.B2), a2.data_ptr(), ptr(m2),
+                 self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
         else:
-            self._conv1(obs, idx, B, a1, None, s)
-            call("ppo_conv2_fwd", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), s)
-        call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
+            self._conv1(obs, idx, B, a1, m1[:B * 400] if train else None, s)
+            if train:
+                call("ppo_conv2_fwd_mask", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(),
+                     m2.data_ptr(), s)
+            else:
+                call("ppo_conv2_fwd", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), s)
+            call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
+        if train:
+            self._mask_rows = B
         nb = call("ppo_fc_fwd_ws_bytes", B, self.H)   # rollout-sized B: split-K into a workspace slab
         if nb:
             fws = ws.get("fc_ws", nb // 4, device=dev)

@@ -53,6 +53,7 @@ SIGNATURES = {
     "ppo_conv2_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv2_fwd_mask": [c_p, c_int, c_p, c_p, c_p, c_p, c_p],
     "ppo_conv3_fwd": [c_p, c_int, c_p, c_p, c_p, c_p],
+    "ppo_trunk_fwd": [c_p, c_p, c_ll, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     "ppo_linear_relu_fwd": [c_p, c_int, c_int, c_p, c_p, c_int, c_p, c_p],
     "ppo_fc_fwd": [c_p, c_int, c_p, c_p, c_int, c_p, c_int, c_p],
     "ppo_fc_fwd_ws_bytes": [c_int, c_int],

@@ -75,16 +75,16 @@ struct Conv1Fwd : C_ {
 // g = lane >> 4 supplies k = 32s + 8g + j, j = 0..7 — one kx row of the patch,
 // 8 adjacent pixels, so an A fragment is one 16-byte LDS read.
 // NPW: weight parts summed (3: exact fp32 weights; 1: half-precision mode, bf16 weights)
+// The body takes its LDS (img: two image stages) so that the fused rollout trunk
+// (trunk_fwd_kernel) can run it as its first phase in a shared buffer.
 template <int C, bool MASK, int NPW = 3>   // MASK: also write the ReLU mask bits (training forward)
-__global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __restrict__ obs,
-                                                               const int64_t* __restrict__ idx, long long row0,
-                                                               int B, const float* __restrict__ w,
-                                                               const float* __restrict__ bias,
-                                                               float* __restrict__ out,
-                                                               uint16_t* __restrict__ mbits) {
+__device__ __forceinline__ void conv1_fwd_bf16x3_body(const uint8_t* __restrict__ obs,
+                                                      const int64_t* __restrict__ idx, long long row0, int B,
+                                                      const float* __restrict__ w, const float* __restrict__ bias,
+                                                      float* __restrict__ out, uint16_t* __restrict__ mbits,
+                                                      uint16_t (*__restrict__ img)[C * IMG2]) {
   constexpr int NPX = C * IMG2, CH = NPX / 16, K = C * 64, KS = K / 32, PER = (CH + 511) / 512;
   static_assert(NPX % 16 == 0, "16-pixel chunks");
-  __shared__ __attribute__((aligned(16))) uint16_t img[2][NPX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ct = wave & 1, rq = wave >> 1;
   const int i16 = lane & 15, g = lane >> 4;
@@ -203,6 +203,17 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
     __syncthreads();   // every wave is done with img[cur]; img[cur ^ 1] is complete
     cur ^= 1;
   }
+}
+
+template <int C, bool MASK, int NPW = 3>
+__global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __restrict__ obs,
+                                                               const int64_t* __restrict__ idx, long long row0,
+                                                               int B, const float* __restrict__ w,
+                                                               const float* __restrict__ bias,
+                                                               float* __restrict__ out,
+                                                               uint16_t* __restrict__ mbits) {
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][C * IMG2];
+  conv1_fwd_bf16x3_body<C, MASK, NPW>(obs, idx, row0, B, w, bias, out, mbits, img);
 }
 
 // conv1 weight gradient on the bf16 matrix cores, exact, part-pipelined
@@ -542,17 +553,19 @@ __global__ __launch_bounds__(256) void relu_bits_kernel(const float* __restrict_
 // DBG (timing anatomy of a diagnostic build only — the library instantiates DBG = 0;
 // wrong results): 1 skips the MFMAs, 2 the staging (split + ds_write), 4 the global
 // loads, 8 the epilogue stores (profiles/r04_c2f_anatomy_kbench.log)
+constexpr int C2F_STG = 3 * 4 * 400, C2F_MT = 6;   // conv2 forward: bf16x8 units per stage, row tiles
+constexpr int C2F_LDS = 2 * C2F_STG * 16 + 2 * C2F_MT * 16 * 4;   // stages + vtab + otab (154,368 B)
 template <int NP, bool MASK = false, int DBG = 0>
-__global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restrict__ a1, int B,
-                                                           const uint16_t* __restrict__ wpl,
-                                                           const float* __restrict__ bias,
-                                                           float* __restrict__ out,
-                                                           uint16_t* __restrict__ mbits) {
-  constexpr int U = 400, PLN = 4 * U, STG = 3 * PLN, MT = 6, KS = 8, WN = 64 * 512;
+__device__ __forceinline__ void conv2_fwd_x9c_body(const float* __restrict__ a1, int B,
+                                                   const uint16_t* __restrict__ wpl, const float* __restrict__ bias,
+                                                   float* __restrict__ out, uint16_t* __restrict__ mbits,
+                                                   uint8_t* __restrict__ lds) {
+  constexpr int U = 400, PLN = 4 * U, STG = 3 * PLN, MT = C2F_MT, KS = 8, WN = 64 * 512;
   constexpr int UNITS = 4 * U, UPER = (UNITS + 511) / 512;   // 4 units per thread (the 4th: wave 0)
-  __shared__ __attribute__((aligned(16))) bf16x8 S[2 * STG];
-  __shared__ int vtab[MT][16];
-  __shared__ int otab[MT][16];
+  static_assert(STG == C2F_STG, "stage size");
+  bf16x8* const S = reinterpret_cast<bf16x8*>(lds);
+  int (*const vtab)[16] = reinterpret_cast<int (*)[16]>(lds + 2 * STG * 16);
+  int (*const otab)[16] = reinterpret_cast<int (*)[16]>(lds + 2 * STG * 16 + MT * 16 * 4);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
   const int nt = wave & 3, kh = wave >> 2, co = 16 * nt + i16;
   if (tid < 16) {
@@ -718,6 +731,16 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
     }
     cur ^= 1;
   }
+}
+
+template <int NP, bool MASK = false, int DBG = 0>
+__global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restrict__ a1, int B,
+                                                           const uint16_t* __restrict__ wpl,
+                                                           const float* __restrict__ bias,
+                                                           float* __restrict__ out,
+                                                           uint16_t* __restrict__ mbits) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[C2F_LDS];
+  conv2_fwd_x9c_body<NP, MASK, DBG>(a1, B, wpl, bias, out, mbits, lds);
 }
 
 // conv2 weight gradient, image-resident on the bf16 matrix cores (exact split,
@@ -1110,14 +1133,16 @@ __global__ __launch_bounds__(512) void conv3_dgrad_x9_kernel(const float* __rest
 // the next image staged before the compute.  Wave w: co tile w & 1, K half
 // (w >> 1) & 1 (taps 0-4.5 / 4.5-8: 9 k-steps, weights in 108 VGPRs), row tiles
 // 2 (w >> 2) .. +1; K half 1 hands its partial sums over through LDS.
+constexpr int C3F_PL = 84 * 64;   // conv3 forward: bf16 per plane
+constexpr int C3F_LDS = 2 * 3 * C3F_PL * 2 + 2 * 2 * 2 * 2 * 64 * 16;   // stages + K-half partials (80,896 B)
 template <int NP>
-__global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restrict__ a2, int B,
-                                                          const uint16_t* __restrict__ wpl,
-                                                          const float* __restrict__ bias,
-                                                          float* __restrict__ out, int stagger) {
+__device__ __forceinline__ void conv3_fwd_x9_body(const float* __restrict__ a2, int B,
+                                                  const uint16_t* __restrict__ wpl, const float* __restrict__ bias,
+                                                  float* __restrict__ out, uint8_t* __restrict__ lds) {
   constexpr int NPX = 84, PL = NPX * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, UPER = (UNITS + 511) / 512;
-  __shared__ __attribute__((aligned(16))) uint16_t S[2][3 * PL];
-  __shared__ __attribute__((aligned(16))) f32x4 R[2][2][2][2][64];   // [stage][co tile][row half][tile][lane]
+  static_assert(PL == C3F_PL, "plane size");
+  uint16_t (*const S)[3 * PL] = reinterpret_cast<uint16_t (*)[3 * PL]>(lds);
+  f32x4 (*const R)[2][2][2][64] = reinterpret_cast<f32x4 (*)[2][2][2][64]>(lds + 2 * 3 * PL * 2);   // [stage][co tile][row half][tile][lane]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
   const int nt = wave & 1, kh = (wave >> 1) & 1, mh = wave >> 2, co = 16 * nt + i16;
   bf16x8 bw[KS][3];
@@ -1167,7 +1192,6 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
     fetch(b + G < B ? b + G : b);
   }
   __syncthreads();
-  (void)stagger;
   for (; b < B; b += G) {
     // the stage write unconditional (past the end: a copy of this image into the
     // idle stage), the image after next fetched one unit per k-step 1, 3 inside the
@@ -1217,6 +1241,50 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
     }
     cur ^= 1;
   }
+}
+
+template <int NP>
+__global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restrict__ a2, int B,
+                                                          const uint16_t* __restrict__ wpl,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out, int stagger) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[C3F_LDS];
+  (void)stagger;
+  conv3_fwd_x9_body<NP>(a2, B, wpl, bias, out, lds);
+}
+
+// The rollout's CNN trunk in one launch: conv1 -> conv2 -> conv3 forward as three
+// phases of one persistent grid (one block per CU).  Every phase maps image b to
+// block b mod G, so a block consumes only its own outputs of the phase before:
+// no grid-wide synchronisation, only each wave's stores retired (vmcnt) and a
+// block barrier between phases, then an agent-scope acquire (L1 invalidate).
+// This removes the two kernel boundaries inside the trunk — 10.3-10.4 us each
+// between these persistent kernels at the rollout's 4,096 images (c5 kernel trace,
+// profiles/r05_l_c5_kernel_stats.csv) — and each phase is the unchanged kernel body
+// (bit-identical outputs to the three launches).  The phases share one LDS buffer
+// (the largest phase, conv2: 154,368 B).
+constexpr int TRUNK_LDS = C2F_LDS > C3F_LDS ? (C2F_LDS > 2 * 4 * IMG2 * 2 ? C2F_LDS : 2 * 4 * IMG2 * 2)
+                                            : (C3F_LDS > 2 * 4 * IMG2 * 2 ? C3F_LDS : 2 * 4 * IMG2 * 2);
+__device__ __forceinline__ void trunk_phase_sync() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's output stores are in L2
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // no stale L1 line under the next phase's loads
+}
+template <int NP, bool MASK>
+__global__ __launch_bounds__(512) void trunk_fwd_kernel(const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx,
+                                                       long long row0, int B, const float* __restrict__ w1,
+                                                       const float* __restrict__ b1, float* __restrict__ a1,
+                                                       uint16_t* __restrict__ m1, const uint16_t* __restrict__ w2pl,
+                                                       const float* __restrict__ b2, float* __restrict__ a2,
+                                                       uint16_t* __restrict__ m2, const uint16_t* __restrict__ w3pl,
+                                                       const float* __restrict__ b3, float* __restrict__ a3) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[TRUNK_LDS];
+  conv1_fwd_bf16x3_body<4, MASK, NP == 1 ? 1 : 3>(obs, idx, row0, B, w1, b1, a1, m1,
+                                                   reinterpret_cast<uint16_t (*)[4 * IMG2]>(lds));
+  trunk_phase_sync();
+  conv2_fwd_x9c_body<NP, MASK>(a1, B, w2pl, b2, a2, m2, lds);
+  trunk_phase_sync();
+  conv3_fwd_x9_body<NP>(a2, B, w3pl, b3, a3, lds);
 }
 
 // conv3 weight gradient, image-resident on the bf16 matrix cores (exact split,
@@ -2012,6 +2080,43 @@ PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float*
                 g_stagger);
   if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
   PPO_LAUNCH_CHECK("conv3_fwd_x9_kernel");
+  return 0;
+}
+
+// conv1 -> conv2 -> conv3 forward (model.py:177-179) of u8 4-channel observation rows in
+// one launch (trunk_fwd_kernel): a1, a2, a3 as ppo_conv1_fwd / ppo_conv2_fwd /
+// ppo_conv3_fwd write them (bit-identical); m1 / m2 both NULL or both given (the
+// ReLU mask bits of ppo_conv1_fwd_mask / ppo_conv2_fwd_mask).  Small batches (<=
+// small_b) and conv1_fwd tune 9 take the three separate calls.
+PPO_API int ppo_trunk_fwd(const uint8_t* obs, const int64_t* idx, long long row0, int B, const float* w1,
+                          const float* b1, float* a1, uint32_t* m1, const float* w2p, const float* b2, float* a2,
+                          uint64_t* m2, const float* w3p, const float* b3, float* a3, void* stream) {
+  PPO_REQUIRE(B >= 0 && obs != nullptr && (m1 == nullptr) == (m2 == nullptr),
+              "ppo_trunk_fwd: B=%d, obs and both-or-neither masks required", B);
+  if (B == 0) return 0;
+  // the masked (training) form runs the three launches: fused, its registers spill
+  // (2 VGPRs at 256), and the training forward has 2 boundaries per minibatch only
+  if (B <= g_small_b || g_tune[TK_CONV1_FWD] != 0 || m1 != nullptr) {
+    int rc = conv1_fwd_impl(obs, 1, idx, row0, 4, B, w1, b1, a1, reinterpret_cast<uint16_t*>(m1), stream);
+    if (rc == 0) rc = conv2_fwd_impl(a1, B, w2p, b2, a2, reinterpret_cast<uint16_t*>(m2), stream);
+    if (rc == 0) rc = ppo_conv3_fwd(a2, B, w3p, b3, a3, stream);
+    return rc;
+  }
+  const unsigned nb = img_grid(B);
+  hipStream_t st = as_stream(stream);
+  int slot;
+  const bool prof = ppo_prof_begin("trunk_fwd", st, &slot);
+  const uint16_t* w2pl = planes_of(w2p, 64 * 512);
+  const uint16_t* w3pl = planes_of(w3p, 32 * 576);
+#define PPO_TRUNK(NP_) \
+  trunk_fwd_kernel<NP_, false><<<nb, 512, 0, st>>>(obs, idx, row0, B, w1, b1, a1, nullptr, w2pl, b2, a2, nullptr, \
+                                                    w3pl, b3, a3)
+  if (g_products == 9) PPO_TRUNK(9);
+  else if (g_products == 1) PPO_TRUNK(1);
+  else PPO_TRUNK(6);
+#undef PPO_TRUNK
+  if (prof) ppo_prof_end(slot, st, 2.0 * B * (400.0 * 32 * 256 + 81.0 * 64 * 512 + 49.0 * 32 * 576));
+  PPO_LAUNCH_CHECK("trunk_fwd_kernel");
   return 0;
 }
 

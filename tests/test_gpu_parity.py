@@ -952,6 +952,57 @@ def test_conv2_mask_bits_and_conv3_dgrad_bits(gpu):
     assert torch.equal(d_ref, d_bits)
 
 
+@pytest.mark.parametrize("B", [5, 300, 4096])
+@pytest.mark.parametrize("products", [6, 1, 9])
+def test_trunk_fwd_equals_three_launches(gpu, B, products):
+    """ppo_trunk_fwd (conv1 -> conv2 -> conv3 as three phases of one persistent
+    launch, the rollout's trunk) writes a1, a2, a3 bit-identical to ppo_conv1_fwd,
+    ppo_conv2_fwd and ppo_conv3_fwd, rows gathered out of order: B < the grid
+    (blocks without images), blocks walking 2 images, and the rollout's 4,096 (16
+    per block); every product count.  The masked form (both mask buffers) equals
+    ppo_conv1_fwd_mask / ppo_conv2_fwd_mask."""
+    Hh = _hip()
+    _, packed, pk = _packed(gpu, 64, 51)
+    g = torch.Generator().manual_seed(52 + B)
+    rows = B + 64
+    obs = torch.randint(0, 256, (rows, 4, 84, 84), dtype=torch.uint8, generator=g).cuda()
+    idx = torch.randperm(rows, generator=g)[:B].contiguous().cuda()
+    w1 = (torch.randn(32, 4, 8, 8, generator=g) * 0.05).cuda()
+    b1, b2, b3 = [(torch.randn(n, generator=g) * 0.1).cuda() for n in (32, 64, 32)]
+    def bufs():
+        return [torch.full((B * n,), float("nan"), device=gpu) for n in (400 * 32, 81 * 64, 49 * 32)]
+    old = Hh.call("ppo_tune_get", b"products")
+    try:
+        Hh.call("ppo_tune_set", b"products", products)
+        r1, r2, r3 = bufs()
+        Hh.call("ppo_conv1_fwd", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, w1.data_ptr(), b1.data_ptr(),
+                r1.data_ptr(), _s())
+        Hh.call("ppo_conv2_fwd", r1.data_ptr(), B, pk[0], b2.data_ptr(), r2.data_ptr(), _s())
+        Hh.call("ppo_conv3_fwd", r2.data_ptr(), B, pk[1], b3.data_ptr(), r3.data_ptr(), _s())
+        t1, t2, t3 = bufs()
+        Hh.call("ppo_trunk_fwd", obs.data_ptr(), idx.data_ptr(), 0, B, w1.data_ptr(), b1.data_ptr(), t1.data_ptr(),
+                None, pk[0], b2.data_ptr(), t2.data_ptr(), None, pk[1], b3.data_ptr(), t3.data_ptr(), _s())
+        m1 = torch.zeros(B * 400, dtype=torch.int32, device=gpu)
+        m2 = torch.zeros(B * 81, dtype=torch.int64, device=gpu)
+        q1 = torch.zeros_like(m1)
+        q2 = torch.zeros_like(m2)
+        u1, u2, u3 = bufs()
+        Hh.call("ppo_trunk_fwd", obs.data_ptr(), idx.data_ptr(), 0, B, w1.data_ptr(), b1.data_ptr(), u1.data_ptr(),
+                m1.data_ptr(), pk[0], b2.data_ptr(), u2.data_ptr(), m2.data_ptr(), pk[1], b3.data_ptr(),
+                u3.data_ptr(), _s())
+        v1, v2 = bufs()[:2]
+        Hh.call("ppo_conv1_fwd_mask", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, w1.data_ptr(), b1.data_ptr(),
+                v1.data_ptr(), q1.data_ptr(), _s())
+        Hh.call("ppo_conv2_fwd_mask", v1.data_ptr(), B, pk[0], b2.data_ptr(), v2.data_ptr(), q2.data_ptr(), _s())
+        torch.cuda.synchronize()
+    finally:
+        Hh.call("ppo_tune_set", b"products", old)
+    for a, b in ((r1, t1), (r2, t2), (r3, t3), (r1, u1), (r2, u2), (r3, u3)):
+        assert torch.equal(a, b)
+    assert torch.equal(m1, q1) and torch.equal(m2, q2)
+    assert 0.2 < (r3 > 0).float().mean().item() < 0.8
+
+
 @pytest.mark.parametrize("products", [6, 9])
 def test_conv2_fwd_vs_torch(gpu, products):
     """conv2 forward (4x4 stride 2, 20x20x32 -> 9x9x64, bias + ReLU): the
