@@ -1292,12 +1292,14 @@ def test_split_products_fp32_accuracy(gpu):
         assert e6 <= 2 * e9 + 1e-9 and e6 <= 4 * ecpu + 1e-9 and e6 < 1e-6, (name, e6, e9, ecpu)
 
 
-@pytest.mark.parametrize("M,H", [(37, 64), (512, 256), (100, 128)])
+@pytest.mark.parametrize("M,H", [(37, 64), (512, 256), (100, 128), (4096, 256), (4001, 512)])
 def test_gru_step_kernels_vs_float64(gpu, M, H):
     """The register-tiled GRU step kernels (default) and the tile-GEMM steps
     (ppo_gru_variant_set(1)) vs a float64 restatement of the cell
     (model.py:112-115 with h_in = h·mask): forward outputs, every saved gate, and
-    the backward carry (dh_in + dh'·z)·m, within 2e-5 of max|ref|."""
+    the backward carry (dh_in + dh'·z)·m, within 2e-5 of max|ref|.  M = 4096 / 4000
+    (the rollout's rows): the forward step's blocks loop over several row groups
+    (at most two blocks per CU), a one-row last group at 4001."""
     Hh = _hip()
     g = torch.Generator().manual_seed(M + H)
     hprev = torch.randn(M, H, generator=g)
