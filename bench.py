@@ -93,10 +93,11 @@ def profiled(products):
         "linear_wgrad": mf(", fc / GRU weight gradients, split-K slabs"),
         "linear_fwd_ex": mf(", GRU input projection / MLP layers"),
         "linear_dgrad_ex": mf(", GRU input dgrad / MLP layers"),
-        "gru_seq_fwd": ("mfma", PEAK_FP32_MFMA_TFLOPS, "flop",
-                        "v_mfma_f32_16x16x4_f32 register-tiled GRU step kernels (cell fused), T launches"),
-        "gru_seq_bwd": ("mfma", PEAK_FP32_MFMA_TFLOPS, "flop",
-                        "v_mfma_f32_16x16x4_f32 BPTT step kernels fused with the gate backward"),
+        # the GRU's W_hh products: split-bf16 x6 for H >= 128 (c5: H = 256); fp32 MFMA at H = 64
+        "gru_seq_fwd": mf(", W_hh products of the persistent GRU forward (cell fused)"),
+        "gru_seq_bwd": mf(", W_hh products of the persistent BPTT (gate backward fused)"),
+        # the rollout's conv1 -> conv2 -> conv3 in one launch (conv1's share at x3 counted at x6: conservative)
+        "trunk_fwd": mf(", rollout trunk conv1 -> conv2 -> conv3 as one persistent launch"),
         "heads_train": hbm("Categorical + PPO loss + analytic backward fused, one wave per row"),
         "heads_act": hbm("value / logits / Categorical sample fused"),
         "heads_reduce": hbm("head-gradient partial sums"),
