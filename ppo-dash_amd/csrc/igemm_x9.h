@@ -147,9 +147,16 @@ __device__ __forceinline__ int x9_off(int row, int k) {   // f32 element offset,
   constexpr unsigned H8 = 0x32765410u;   // nibbles: H8[i] = (H8 >> 4i) & 15
   return row * 32 + 4 * ((k >> 2) ^ ((H8 >> (4 * ((row >> 1) & 7))) & 7));
 }
+// pl_off also swaps rows 2j, 2j + 1 in every second group of 16 rows (row bit 0 ^=
+// bit 4): the split-at-staging kernel's non-KC units write rows 4t + q of 8
+// consecutive t from 8 lanes at one chunk, which without it all sit in the same
+// 64-B quarter of the 256-B bank row (2-way conflicts: 31 % of the fc weight
+// gradient's LDS cycles, profiles/r05_s_fc_sq.json); with it those 8 writes, the 2-row
+// x 4-chunk KC writes and the ds_read_b128 fragment groups are all conflict-free
+// (exhaustive check over the tile, tools/swizzle_check.py).
 __device__ __forceinline__ int pl_off(int row, int q) {   // bf16 element offset
   constexpr unsigned H4 = 0x1320u;
-  return row * 32 + 8 * (q ^ ((H4 >> (4 * ((row >> 2) & 3))) & 3));
+  return (row ^ ((row >> 4) & 1)) * 32 + 8 * (q ^ ((H4 >> (4 * ((row >> 2) & 3))) & 3));
 }
 
 // Block -> (m0, n0, z) tile.  n_fast 0: m = xcd_remap(blockIdx.x) (each XCD a
