@@ -163,3 +163,17 @@ def test_bf16x3_split_is_exact():
             assert np.array_equal(back, v.astype(np.float64)), scale
         else:   # lo falls into the subnormal range: off by at most its spacing, 2^-133
             assert np.abs(back - v).max() <= 2.0 ** -133, scale
+
+
+def test_gemm_plane_swizzle_conflict_free():
+    """igemm_x9.h pl_off: the ds_read_b128 fragment groups, the split-at-staging
+    non-KC writes and the KC writes are all free of LDS bank conflicts (exhaustive
+    over a 256-row tile, tools/swizzle_check.py restates the function)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "ppo-dash_amd", "csrc", "igemm_x9.h")).read()
+    assert "(row ^ ((row >> 4) & 1)) * 32 + 8 * (q ^ ((H4 >> (4 * ((row >> 2) & 3))) & 3))" in src
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "swizzle_check.py")], capture_output=True,
+                         text=True, check=True).stdout
+    assert "reads 1 non-KC writes 1 KC writes 1" in out
