@@ -2488,7 +2488,15 @@ PPO_API int ppo_linear_wgrad(const float* dy, const float* x, int R, int N, int 
       p.x = x; p.K = K;
       return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K);
     }
-    // split at staging, 256 x 128 tiles: 0.727 vs 0.775 ms (in-loop split) at the c3 minibatch
+    // split at staging, 256 x 128 tiles: 0.727 vs 0.775 ms (in-loop split) at the c3 minibatch;
+    // branch-free buffer loads where the operands fit 31-bit offsets
+    if ((long long)R * (N > K ? N : K) * 4 < 0x7fffffffLL) {
+      DenseWgradB<SW256x128> p;
+      set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);
+      p.x = x; p.K = K; p.n_fast = 0;
+      p.vec = K % 4 == 0 && ((uintptr_t)slab & 15) == 0;
+      return launch_x9(p, N, K, Z, as_stream(stream), "linear_wgrad", 2.0 * R * N * K);
+    }
     DenseWgrad<SW256x128> p;
     set_wgrad(p, dy, N, R, Z, slab, slab_bias, K);
     p.x = x; p.K = K; p.n_fast = 0;

@@ -440,6 +440,32 @@ struct DenseWgrad : WgradBase<C_> {
   }
 };
 
+// Linear wgrad with branch-free buffer loads (the split-at-staging fc / GRU weight
+// gradients): operand row r, column c at byte offset c·4 + r·ld·4 of one buffer
+// resource over the whole operand; rows past R read 0 from beyond the resource's
+// range and a column past the width starts out of range (0x80000000), so no load
+// needs an exec-mask branch or a 64-bit address (DenseWgrad's 16 loads per k-step
+// compiled to a branch and a 64-bit multiply each).  Offsets are 32-bit: the
+// launcher checks R·width·4 < 2^31.
+template <class C_>
+struct DenseWgradB : WgradBase<C_> {
+  const float* x; int K;
+  struct ACtx { uint32_t off; };
+  struct BCtx { uint32_t off; };
+  __device__ ACtx a_ctx(int co, int) const { return {co < this->COUT ? 4u * (uint32_t)co : 0x80000000u}; }
+  __device__ f32x4 a_load(const ACtx& c, int r) const {
+    const auto rs = make_rsrc(this->dz, (uint32_t)(this->R * this->COUT) * 4u);
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         rs, c.off + __umul24((uint32_t)r, 4u * (uint32_t)this->COUT), 0, 0));
+  }
+  __device__ BCtx b_ctx(int n, int) const { return {n < K ? 4u * (uint32_t)n : 0x80000000u}; }
+  __device__ f32x4 b_load(const BCtx& c, int r) const {
+    const auto rs = make_rsrc(x, (uint32_t)(this->R * K) * 4u);
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         rs, c.off + __umul24((uint32_t)r, 4u * (uint32_t)K), 0, 0));
+  }
+};
+
 // Deterministic column sums: out[c] = scale * Σ_z src[z*ld + c], c < cols.
 // A block covers 32 consecutive columns with 8 z-groups (each summing
 // z ≡ g mod 8 in a fixed order, 4 loads in flight), then combines the groups
