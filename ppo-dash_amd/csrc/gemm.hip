@@ -2142,7 +2142,7 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
             (b == nullptr || ((uintptr_t)b & 15) == 0);                                              \
     return launch_x9(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);                      \
   }
-    if (wide) PPO_FC(XP128)
+    if (wide) PPO_FC(XP128)   // 0.546-0.551 ms; 8 waves of 16 x 128 0.563-0.565 (r05_v_fc_fwd_tiles_kbench.log)
     PPO_FC(XP128x64w8)
 #undef PPO_FC
   }
