@@ -2132,9 +2132,10 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
     // fills a quarter of the chip with 128 x 128 tiles: 8 waves of 16 x 64 there
     // (0.060 vs 0.070 ms for 128 x 64)
     const bool wide = ((M + 127LL) / 128) * ((H + 127) / 128) >= 2LL * device_cus();
-#define PPO_FC(CFG)                                                                                  \
+    const bool abuf = 4LL * M * K < 0x80000000LL;   // DenseReluFwdB's 32-bit offsets
+#define PPO_FC(T, CFG)                                                                               \
   {                                                                                                  \
-    DenseReluFwd<CFG> p;                                                                             \
+    T<CFG> p;                                                                                        \
     p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1; \
     set_planes(p, w4p, (long long)H * K, H, K);                                                      \
     p.n_fast = 1;                                                                                    \
@@ -2142,8 +2143,10 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
             (b == nullptr || ((uintptr_t)b & 15) == 0);                                              \
     return launch_x9(p, M, H, 1, as_stream(stream), "fc_fwd", 2.0 * M * H * K);                      \
   }
-    if (wide) PPO_FC(XP128)   // 0.546-0.551 ms; 8 waves of 16 x 128 0.563-0.565 (r05_v_fc_fwd_tiles_kbench.log)
-    PPO_FC(XP128x64w8)
+    if (wide && abuf) PPO_FC(DenseReluFwdB, XP128)   // 0.546-0.551 ms; 8 waves of 16 x 128 0.563-0.565 (r05_v_fc_fwd_tiles_kbench.log)
+    if (wide) PPO_FC(DenseReluFwd, XP128)
+    if (abuf) PPO_FC(DenseReluFwdB, XP128x64w8)
+    PPO_FC(DenseReluFwd, XP128x64w8)
 #undef PPO_FC
   }
   DenseReluFwd<CfgN128> p;
@@ -2322,12 +2325,18 @@ PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt
   PPO_REQUIRE(K % 4 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 4", K);
   if (use_x9()) {   // wt = the packed W4T segment [1568][H] (planes follow); 8 waves of 16 x 128:
     PPO_REQUIRE(K % 8 == 0, "ppo_linear_dgrad_mask: K=%d must be a multiple of 8", K);   // 0.75 vs 0.87 ms (4 waves)
-    DenseDgradMask<XP128w8> p;
-    p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;
-    set_planes(p, wt, (long long)N * K, N, K);
-    p.n_fast = 0;   // m fastest: the 134 MB dy fits the Infinity Cache, the weight tile stays L2-resident
-    p.vec = N % 4 == 0 && ((uintptr_t)dx & 15) == 0 && (act == nullptr || ((uintptr_t)act & 15) == 0);
-    return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);
+#define PPO_DGM(T)                                                                                          \
+  {                                                                                                         \
+    T<XP128w8> p;                                                                                           \
+    p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;                                \
+    set_planes(p, wt, (long long)N * K, N, K);                                                              \
+    p.n_fast = 0;   /* m fastest: the 134 MB dy fits the Infinity Cache, the weight tile stays L2-resident */ \
+    p.vec = N % 4 == 0 && ((uintptr_t)dx & 15) == 0 && (act == nullptr || ((uintptr_t)act & 15) == 0);     \
+    return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);                  \
+  }
+    if (4LL * M * K < 0x80000000LL) PPO_DGM(DenseDgradMaskB)   // 32-bit buffer offsets
+    PPO_DGM(DenseDgradMask)
+#undef PPO_DGM
   }
   DenseDgradMask<CfgN128> p;
   p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;

@@ -401,6 +401,36 @@ struct DenseDgradMask : C_ {
   }
 };
 
+// A operand (row m, k) by branch-free buffer loads (see DenseWgradB): byte offset
+// m·ld·4 + k·4 in one resource over rows [0, M); a row past M starts out of range
+// (0x80000000) and k ≥ K is sent there by a select, so each load is one v_cndmask
+// instead of an exec-mask branch and a 64-bit address.  The launcher checks
+// M·ld·4 < 2^31 (and that there is no row gather).
+struct ABufCtx { uint32_t off; };
+__device__ __forceinline__ f32x4 abuf_load(const float* base, uint32_t bytes, const ABufCtx& c, int k, int K) {
+  const uint32_t off = k < K ? c.off + 4u * (uint32_t)k : 0x80000000u;
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(make_rsrc(base, bytes), off, 0, 0));
+}
+
+template <class C_>
+struct DenseReluFwdB : DenseReluFwd<C_> {
+  using ACtx = ABufCtx;
+  __device__ uint32_t ld() const { return (uint32_t)(this->lda ? this->lda : this->K); }
+  __device__ ACtx a_ctx(int m, int) const { return {m < this->M ? 4u * (uint32_t)m * ld() : 0x80000000u}; }
+  __device__ f32x4 a_load(const ACtx& c, int k) const {
+    return abuf_load(this->x, 4u * (uint32_t)this->M * ld(), c, k, this->K);
+  }
+};
+
+template <class C_>
+struct DenseDgradMaskB : DenseDgradMask<C_> {
+  using ACtx = ABufCtx;
+  __device__ ACtx a_ctx(int m, int) const { return {m < this->M ? 4u * (uint32_t)m * (uint32_t)this->K : 0x80000000u}; }
+  __device__ f32x4 a_load(const ACtx& c, int k) const {
+    return abuf_load(this->dy, 4u * (uint32_t)this->M * (uint32_t)this->K, c, k, this->K);
+  }
+};
+
 template <class C_>
 struct WgradBase : C_ {
   const float* dz; int COUT; long long R; int chunk;  // chunk: multiple of 16 (and of BK)

@@ -207,6 +207,17 @@ __device__ __forceinline__ void vec_epilogue(const P& p, float* smem, const f32x
     }
 }
 
+// one 16-B chunk of B plane pl, row n, from k: a branch-free buffer load (a row past
+// bnr or k past bld is sent out of the 3-plane resource's range and reads 0);
+// launch_x9 checks 6·bps < 2^31
+template <class P>
+__device__ __forceinline__ uint4 bpl_load(const P& p, int n, int pl, int kk) {
+  const uint32_t off = (n < p.bnr && kk < p.bld)
+                           ? 2u * ((uint32_t)pl * (uint32_t)p.bps + (uint32_t)n * (uint32_t)p.bld + (uint32_t)kk)
+                           : 0x80000000u;
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(make_rsrc(p.bpl, 6u * (uint32_t)p.bps), off, 0, 0));
+}
+
 template <class P, int NP>
 __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
   constexpr int BM = P::BM, BN = P::BN, NT = P::NT, WM = P::WM, WN = P::WN, BK = 32;
@@ -238,7 +249,7 @@ __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
 #pragma unroll
   for (int i = 0; i < NUA; ++i) {
     const int u = tid + i * NT;
-    aon[i] = u < UA;
+    aon[i] = (i + 1) * NT <= UA || u < UA;   // a full row of units: known true, no exec mask
     if constexpr (P::A_KC) {
       arow[i] = u / (BK / 4);
       ak[i] = 4 * (u % (BK / 4));
@@ -251,7 +262,7 @@ __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
 #pragma unroll
   for (int i = 0; i < NUB; ++i) {
     const int u = tid + i * NT;
-    bon[i] = u < UB;
+    bon[i] = (i + 1) * NT <= UB || u < UB;
     if constexpr (BPL) {   // brow = plane row, bk = plane * 4 + 16-B chunk
       brow[i] = (u % (BN * 4)) / 4;
       bk[i] = (u / (BN * 4)) * 4 + u % 4;
@@ -272,8 +283,7 @@ __global__ __launch_bounds__(P::NT) void igemm_x9_kernel(const P p) {
   auto bload = [&](int i, int k) {
     if constexpr (BPL) {   // k = k0 + bk[i]: plane bk >> 2, chunk bk & 3
       const int n = n0 + brow[i], pl = (k - (k & ~(BK - 1))) >> 2, kk = (k & ~(BK - 1)) + 8 * (k & 3);
-      if (n >= p.bnr || kk >= p.bld) return uint4{0u, 0u, 0u, 0u};
-      return *reinterpret_cast<const uint4*>(p.bpl + pl * p.bps + (long long)n * p.bld + kk);
+      return bpl_load(p, n, pl, kk);
     } else if constexpr (P::B_TILE) {
       return p.b_load_t(bctx[i], p.tile(k & ~(BK - 1)), k);
     } else {
@@ -489,7 +499,7 @@ __global__ __launch_bounds__(P::NT) void igemm_x9s_kernel(const P p) {
 #pragma unroll
   for (int i = 0; i < NUA; ++i) {
     const int u = tid + i * NT;
-    aon[i] = u < UA;
+    aon[i] = (i + 1) * NT <= UA || u < UA;   // a full row of units: known true, no exec mask
     if constexpr (AKC) {
       arow[i] = u >> 2;
       ak[i] = 8 * (u & 3);
@@ -502,7 +512,7 @@ __global__ __launch_bounds__(P::NT) void igemm_x9s_kernel(const P p) {
 #pragma unroll
   for (int i = 0; i < NUB; ++i) {
     const int u = (tid + BOFF) % NT + i * NT;
-    bon[i] = u < UB;
+    bon[i] = (i + 1) * NT <= UB || u < UB;
     if constexpr (BPL) {   // brow = plane row, bk = plane * 4 + 16-B chunk
       brow[i] = (u % (BN * 4)) / 4;
       bk[i] = (u / (BN * 4)) * 4 + u % 4;
@@ -523,8 +533,7 @@ __global__ __launch_bounds__(P::NT) void igemm_x9s_kernel(const P p) {
   auto bload = [&](int i, int k) {
     if constexpr (BPL) {   // k = k0 + bk[i]: plane bk >> 2, chunk bk & 3
       const int n = n0 + brow[i], pl = (k - (k & ~(BK - 1))) >> 2, kk = (k & ~(BK - 1)) + 8 * (k & 3);
-      if (n >= p.bnr || kk >= p.bld) return uint4{0u, 0u, 0u, 0u};
-      return *reinterpret_cast<const uint4*>(p.bpl + pl * p.bps + (long long)n * p.bld + kk);
+      return bpl_load(p, n, pl, kk);
     } else {
       return p.b_load(bctx[i], k);
     }
@@ -678,6 +687,12 @@ int launch_x9(const P& p, long long M, int N, int Z, hipStream_t st, const char*
   if (gx > 0x7fffffffLL) {
     ppo_set_error("%s: grid too large (M=%lld)", name, M);
     return PPO_ESHAPE;
+  }
+  if constexpr (P::B_PLANES) {
+    if (6LL * p.bps >= 0x80000000LL) {   // bpl_load's 32-bit offsets
+      ppo_set_error("%s: B planes too large (%lld elements)", name, p.bps);
+      return PPO_ESHAPE;
+    }
   }
   dim3 grid((unsigned)gx, (unsigned)((N + P::BN - 1) / P::BN), (unsigned)Z);
   int slot;

@@ -77,9 +77,10 @@ def test_fc_fwd_vs_float64(gpu, x9, products, B, H):
 
 @pytest.mark.parametrize("x9", [1, 0])
 @pytest.mark.parametrize("products", [6, 9, 1])
-@pytest.mark.parametrize("B,H", [(300, 512), (77, 64)])
+@pytest.mark.parametrize("B,H", [(300, 512), (77, 64), (200, 40)])
 def test_fc_dgrad_mask_vs_float64(gpu, x9, products, B, H):
-    """dx = [a3 > 0] * (dh W): N = 1568 = 6 full 256-row weight blocks + 32 rows."""
+    """dx = [a3 > 0] * (dh W): N = 1568 = 6 full 256-row weight blocks + 32 rows;
+    H = 40 ends the reduction inside a 32-wide k-step."""
     H_ = _hip()
     w4, packed, pk = _packed(gpu, H, 5 + H)
     g = torch.Generator().manual_seed(B + 1)
