@@ -34,6 +34,7 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
 
 
 // The same algorithm with the u8 image staged by LDS-DMA (ppo_tune_set("conv1_wgrad", 8)):
@@ -225,7 +226,322 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw2_kernel(const float* _
   }
 }
 
+// The same product with ONE wave per SIMD (round 5, ppo_tune_set("conv1_wgrad", 9)).
+// kw2's anatomy shows a chain of latencies per wave — one tile of
+// B read-ahead, the dz split in front of each k-step, a conversion phase between
+// two barriers — that its 256-VGPR budget leaves no room to pipeline.  Here 4
+// waves with 512 registers each (accumulators in AGPRs):
+//   * wave w: k-steps w + 4 i (i < 6) of every image and tiles 2 w, 2 w + 1 of
+//     k-step 24: 150 MFMAs per wave per image;
+//   * B fragments read RA tiles ahead through a ring (one flat sequence of the 50
+//     tiles of the image); the dz split of step i + 1 (and of the next image's step
+//     0) computed during step i; dz of the next image loaded one image ahead, one
+//     8-value slot per step;
+//   * the next image converted into the other E stage during this image's steps,
+//     one or two 16-B items per step, from registers loaded one image ahead
+//     (plain buffer loads: no raw LDS buffer, no DMA): one barrier per image.
+// A timing variant of kw2's algorithm; the slab and its sums are kw2's (a
+// different summation order: not bit-identical to tune 8).
+#ifndef KW3_FENCE
+#define KW3_FENCE 1
+#endif
+constexpr int KW3_RA = 3;   // B read-ahead in tiles (lgkmcnt holds 15: 4 reads per tile)
+// NW = 4: one wave per SIMD, all 8 column tiles per wave (tune 9); NW = 8: two waves
+// per SIMD, wave w = 2 kg + ch owning column tiles 4 ch .. 4 ch + 3 of the k-steps of
+// group kg (the pair kg splits the same dz; tune 10)
+template <int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4))) void conv1_wgrad_kw3_kernel(
+    const float* __restrict__ dz1, const uint8_t* __restrict__ obs, const int64_t* __restrict__ idx, long long row0,
+    int B, float* __restrict__ slab, float* __restrict__ slab_bias) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int C = 4, IMG = 84, IMGB = C * IMG * IMG;
+  constexpr int XW = 24, ROWE = 4 * XW, EST = C * IMG * ROWE;
+  constexpr int NT = NW * 64, NITEM = C * IMG * 6, IPT = 2048 / NT, NS = 6;
+  constexpr int TW = 32 / NW, NTAIL = 8 / NW, NP = TW * NS + NTAIL, RA = KW3_RA, RING = RA + 1;
+  __shared__ __attribute__((aligned(16))) uint16_t E[2 * EST + 80];   // + the empty put slots' target
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR): the tail's tile choice is a scalar branch
+  const int kg = NW == 8 ? w >> 1 : w, t0 = NW == 8 ? 4 * (w & 1) : 0;
+  const bool counts = NW == 4 || (w & 1) == 0;   // the bias sum: one wave of each k-step group
+  const int G = gridDim.x;
+  const int kx = l32 & 7, sh = 2 * (kx >> 2);
+  const int lbase = ((l32 >> 3) * 4 + (kx & 3)) * XW;
+  // put items: thread item j = tid + NT j (2,016 of 2,048 slots are real)
+  int isrc[IPT], idst[IPT];
+#pragma unroll
+  for (int j = 0; j < IPT; ++j) {
+    const int it = tid + NT * j, r = it / 6, g6 = it - 6 * r;
+    isrc[j] = r * IMG + 16 * g6;   // >= IMGB for the empty slots: their loads read 0
+    idst[j] = it < NITEM ? r * ROWE + 4 * g6 : -1;
+  }
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  u32x4v raw[IPT];
+  auto raw_load1 = [&](const __amdgpu_buffer_rsrc_t& rs, int j) {
+    if (j < IPT - 1) {
+      raw[j] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(rs, isrc[j], 0, 0));
+    } else {   // the slot holding the image's last 4 bytes: dword loads (each range-checked)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) raw[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, isrc[j] + 4 * k, 0, 0);
+    }
+  };
+  auto put_dx = [&](int j, int st, int dx) {   // one x-phase of item j: u8 -> bf16 (exact), de-interleaved by x mod 4
+    const int d = idst[j] >= 0 ? st * EST + idst[j] : 2 * EST;
+    float f[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = (float)((raw[j][k] >> (8 * dx)) & 255u);
+    const uint2 q = {__builtin_amdgcn_perm(__float_as_uint(f[1]), __float_as_uint(f[0]), 0x07060302u),
+                     __builtin_amdgcn_perm(__float_as_uint(f[3]), __float_as_uint(f[2]), 0x07060302u)};
+    *reinterpret_cast<uint2*>(E + d + dx * XW) = q;
+  };
+  // dz of (image b, k-step s): 8 pixels 16 s + 8 h + j of channel l32
+  auto dz_load1 = [&](int b, int s, f32x8& d, int j) {
+    const auto rs = make_rsrc(dz1 + (size_t)b * 12800, 12800 * 4);
+    d[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((16 * s + 8 * h) * 32 + l32) * 4 + 128 * j, 0, 0));
+  };
+  float bacc = 0.f;
+  // one pair (values 2 pr, 2 pr + 1) of split8's three-way split (the same bits)
+  auto split_pair = [&](const f32x8& d, Frag3& f, int pr, bool count) {
+    const float v0 = d[2 * pr], v1 = d[2 * pr + 1];
+    const bf16x2 hh = __builtin_convertvector(f32x2{v0, v1}, bf16x2);
+    const float r0 = v0 - (float)hh[0], r1 = v1 - (float)hh[1];
+    const bf16x2 mm = __builtin_convertvector(f32x2{r0, r1}, bf16x2);
+    const bf16x2 ll = __builtin_convertvector(f32x2{r0 - (float)mm[0], r1 - (float)mm[1]}, bf16x2);
+    f.h[2 * pr] = hh[0]; f.h[2 * pr + 1] = hh[1];
+    f.m[2 * pr] = mm[0]; f.m[2 * pr + 1] = mm[1];
+    f.l[2 * pr] = ll[0]; f.l[2 * pr + 1] = ll[1];
+    if (count) bacc += v0 + v1;
+  };
+  auto qoff = [&](int q) { const int oy = q / 5; return 4 * oy * ROWE + 4 * (q - 5 * oy); };
+  // the tail (k-step 24) tile e of this wave: one of its own column tiles (NW = 4:
+  // 2 w + e; NW = 8: t0 + kg)
+  auto tail_tile = [&](int e) { return NW == 4 ? 2 * w + e : t0 + kg; };
+  // tile p of the image's flat sequence: k-step kg + 4 (p / TW), tile t0 + p % TW (p <
+  // TW NS); k-step 24, tile tail_tile(p - TW NS) (the tail)
+  uint32_t braw[RING][6];
+  // per-lane element offsets of the two quads of each step (lbase included): the
+  // tile part of a B address is then a compile-time constant (the ds_read offset)
+  int qb[NS + 1][2];
+#pragma unroll
+  for (int i = 0; i <= NS; ++i)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) qb[i][k] = lbase + qoff(4 * (i < NS ? kg + 4 * i : 24) + 2 * h + k);
+  auto bread = [&](const uint16_t* S, int p) {
+    const int i = p < TW * NS ? p / TW : NS, tt = p < TW * NS ? t0 + p % TW : tail_tile(p - TW * NS);
+    const int toff = ((tt >> 1) * IMG + 4 * (tt & 1)) * ROWE;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint16_t* pp = S + toff + qb[i][k];
+      const uint2 d01 = *reinterpret_cast<const uint2*>(pp);
+      braw[p % RING][3 * k] = d01.x;
+      braw[p % RING][3 * k + 1] = d01.y;
+      braw[p % RING][3 * k + 2] = *reinterpret_cast<const uint32_t*>(pp + 4);
+    }
+  };
+  f32x16 acc[TW];
+#pragma unroll
+  for (int t = 0; t < TW; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  auto mma3 = [&](int p, const Frag3& a, f32x16& c) {
+    const uint32_t* r = braw[p % RING];
+    const bf16x8 bq = __builtin_bit_cast(bf16x8, uint4{__builtin_amdgcn_alignbyte(r[1], r[0], sh),
+                                                       __builtin_amdgcn_alignbyte(r[2], r[1], sh),
+                                                       __builtin_amdgcn_alignbyte(r[4], r[3], sh),
+                                                       __builtin_amdgcn_alignbyte(r[5], r[4], sh)});
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, bq, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, bq, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, bq, c, 0, 0, 0);
+  };
+  // Prefetch schedule (each slot is live only between its load and its split, so
+  // the loop-carried registers stay few and the allocator does not split their live
+  // ranges — a copy of an in-flight load waits for it):
+  //   dz slot i (k-step kg + 4 i) is split during step i - 1 (slot 0: step 5 of the
+  //   previous image); slots 4, 5 are loaded in steps 0, 1 (this image), the next
+  //   image's slots 0-3 two per step in steps 2, 3 (two steps before the loop end, so
+  //   the back-edge copies find the data arrived); D24 is loaded in step 1 and split
+  //   in step 4;
+  //   put items (converting image b + G; NW = 4: 0 | 1 | 2, 3 | 4 | 5, 6 | 7 in
+  //   steps 0-5, NW = 8: 0 | 1 | - | 2 | 3 | -) are loaded four steps ahead: those
+  //   put in steps 4, 5 during steps 0, 1 (image b + G), the others during steps
+  //   2-5 (image b + 2G).
+  f32x8 D[NS], D24;   // 8-register tuples: the allocator keeps a slot in one place
+  Frag3 F[2], F24;
+  int b = blockIdx.x, cur = 0;
+  const auto clampb = [&](int x) { return x < B ? x : B - 1; };
+  auto put_step = [](int j) {
+    if constexpr (NW == 4) return j < 2 ? j : j < 4 ? 2 : j == 4 ? 3 : j < 7 ? 4 : 5;
+    else return j < 2 ? j : j + 1;
+  };
+  if (b < B) {
+    {
+      const auto rs0 = make_rsrc(obs + obs_row(idx, row0, b) * (long long)IMGB, IMGB);
+#pragma unroll
+      for (int j = 0; j < IPT; ++j) raw_load1(rs0, j);
+    }
+#pragma unroll
+    for (int i = 0; i < (NW == 4 ? 4 : 3); ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dz_load1(b, kg + 4 * i, D[i], j);
+    wait_vm0();
+#pragma unroll
+    for (int j = 0; j < IPT; ++j)
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) put_dx(j, 0, dx);
+    {
+      const auto rs1 = make_rsrc(obs + obs_row(idx, row0, clampb(b + G)) * (long long)IMGB, IMGB);
+#pragma unroll
+      for (int j = 0; j < IPT; ++j)
+        if (put_step(j) <= 3) raw_load1(rs1, j);
+    }
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) split_pair(D[0], F[0], pr, counts);
+    // nothing in flight at the loop entry: the waitcnt pass merges the entry and the
+    // back-edge states at the loop head, and prologue loads with few younger loads
+    // behind them would cap every iteration's waits (vmcnt(1) at step 0)
+    wait_vm0();
+    lds_barrier();
+#pragma unroll
+    for (int p = 0; p < RA; ++p) bread(E, p);
+  }
+  for (; b < B; b += G) {
+    const uint16_t* Sc = E + cur * EST;
+    const int bn = clampb(b + G);
+    const auto rs1 = make_rsrc(obs + obs_row(idx, row0, bn) * (long long)IMGB, IMGB);
+    const auto rs2 = make_rsrc(obs + obs_row(idx, row0, clampb(b + 2 * G)) * (long long)IMGB, IMGB);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      int ja = -1, jb = -1;   // the step's put items
+#pragma unroll
+      for (int j = 0; j < IPT; ++j)
+        if (put_step(j) == i) {
+          if (ja < 0) ja = j;
+          else jb = j;
+        }
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        const int p = TW * i + t;
+        if (p + RA < NP) bread(Sc, p + RA);
+#if KW3_FENCE
+        __builtin_amdgcn_sched_barrier(0);   // the read-ahead stays ahead of this tile's MFMAs
+#endif
+        mma3(p, F[i & 1], acc[t]);
+        // filler work, sliced evenly over the step's tiles (a tile's MFMAs and its
+        // slice share one scheduling region between the fences): pairs of the next
+        // step's split (and of the tail's in step 4), the dz slot loads, the x-phases
+        // of the step's put item(s), then the raw loads four steps ahead
+        if (t < 4) {
+          if (i + 1 < NS) split_pair(D[i + 1], F[(i + 1) & 1], t, counts);
+          else split_pair(D[0], F[0], t, counts && b + G < B);
+        }
+        if (i == 4 && t >= TW - 4) split_pair(D24, F24, t - (TW - 4), w == 0);
+#pragma unroll
+        for (int u = 0; u < 8 / TW; ++u) {
+          const int jl = (8 / TW) * t + u;   // load jl of the slot's 8
+          if constexpr (NW == 4) {
+            if (i < 2) dz_load1(b, kg + 4 * (4 + i), D[4 + i], jl);
+            if (i == 2 || i == 3) {
+              dz_load1(bn, kg + 4 * (2 * (i - 2)), D[2 * (i - 2)], jl);
+              dz_load1(bn, kg + 4 * (2 * (i - 2) + 1), D[2 * (i - 2) + 1], jl);
+            }
+            if (i == 1) dz_load1(b, 24, D24, jl);
+          } else {   // two waves per SIMD: shorter distances — slots 3, 4, 5 (this image)
+                     // in steps 0-2, the next image's 0 in step 3, 1 and 2 in step 4
+            if (i < 3) dz_load1(b, kg + 4 * (3 + i), D[3 + i], jl);
+            if (i == 3) dz_load1(bn, kg, D[0], jl);
+            if (i == 4) {
+              dz_load1(bn, kg + 4, D[1], jl);
+              dz_load1(bn, kg + 8, D[2], jl);
+            }
+            if (i == 2) dz_load1(b, 24, D24, jl);
+          }
+        }
+        if (ja >= 0) {
+          if (jb < 0) {
+            if (t < 4) put_dx(ja, cur ^ 1, t);
+          } else {
+            put_dx(t < 4 ? ja : jb, cur ^ 1, t & 3);
+          }
+        }
+        if (t == TW - 1) {
+#pragma unroll
+          for (int jj = 0; jj < IPT; ++jj) {
+            if (i < 2 && put_step(jj) == i + 4) raw_load1(rs1, jj);
+            if (i >= 2 && put_step(jj) == i - 2) raw_load1(rs2, jj);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < NTAIL; ++e) {   // the tail: tile tail_tile(e) of k-step 24
+      const int p = TW * NS + e;
+      if (p + RA < NP) bread(Sc, p + RA);
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+        if (t0 + t == tail_tile(e)) mma3(p, F24, acc[t]);
+    }
+    lds_barrier();   // E[cur ^ 1] complete, E[cur] consumed
+    cur ^= 1;
+    if (b + G < B) {
+#pragma unroll
+      for (int p = 0; p < RA; ++p) bread(E + cur * EST, p);
+    }
+  }
+  wait_vm0();
+  __syncthreads();
+  // the k-step groups' partial gradients summed in a fixed order (per column half)
+  float* X = reinterpret_cast<float*>(E);
+  const int slot = NW == 8 ? (w & 1) : 0;
+#pragma unroll
+  for (int half = 2; half >= 1; half >>= 1) {
+    if (kg >= half && kg < 2 * half) {
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) X[((((kg - half) * 2 + slot) * TW + t) * 16 + r) * 64 + lane] = acc[t][r];
+    }
+    __syncthreads();
+    if (kg < half) {
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] += X[(((kg * 2 + slot) * TW + t) * 16 + r) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  float* out = slab + (size_t)blockIdx.x * 32 * 256;
+  if (kg == 0) {
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = (r & 3) + 8 * (r >> 2) + 4 * h, n = 32 * (t0 + t) + l32;
+        out[co * 256 + n] = acc[t][r];
+      }
+  }
+  X[tid] = bacc;
+  __syncthreads();
+  if (tid < 32) {
+    float t = 0.f;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) t += X[v * 64 + tid] + X[v * 64 + 32 + tid];
+    slab_bias[(size_t)blockIdx.x * 32 + tid] = t;
+  }
+}
+
 }  // namespace
+
+int conv1_wgrad_kw3(const float* dz1, const uint8_t* obs, const int64_t* idx, long long row0, int B, int Z,
+                    float* slab, float* slab_bias, void* stream, int nw) {
+  if (B <= 0 || Z <= 0) return 0;
+  hipStream_t st = as_stream(stream);
+  int slot;
+  const bool prof = ppo_prof_begin("conv1_wgrad_u8", st, &slot);
+  if (nw == 8) conv1_wgrad_kw3_kernel<8><<<Z, 512, 0, st>>>(dz1, obs, idx, row0, B, slab, slab_bias);
+  else conv1_wgrad_kw3_kernel<4><<<Z, 256, 0, st>>>(dz1, obs, idx, row0, B, slab, slab_bias);
+  if (prof) ppo_prof_end(slot, st, 2.0 * B * 400 * 32 * 256);
+  PPO_LAUNCH_CHECK("conv1_wgrad_kw3_kernel");
+  return 0;
+}
 
 // conv1 weight gradient of u8 observations (C = 4) with the k-split kernel: slab [Z][32][256]
 // (integer-scaled: reduce with 1/255) and bias partials [Z][32]; called by ppo_conv1_wgrad (tune 8)

@@ -1877,7 +1877,7 @@ static int g_small_b = 4;
 static bool tune_ok(int k, int v) {
   switch (k) {
     case TK_CONV1_FWD: return v == 0 || v == 9;
-    case TK_CONV1_WGRAD: return v == 5 || v == 8;
+    case TK_CONV1_WGRAD: return v == 5 || v == 8 || v == 9 || v == 10;
     case TK_X9: return v >= 0 && v <= 2;
     case TK_FC_SPLITK: return v >= 0 && v <= 8;
     default: return v == 0 || v == 1;
@@ -1971,7 +1971,9 @@ static inline unsigned img_grid(int B) {
 static int conv1_fwd_impl(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
                           const float* w1, const float* b1, float* out, uint16_t* mbits, void* stream);
 int conv1_wgrad_kw(const float* dz1, const uint8_t* obs, const int64_t* idx, long long row0, int B, int Z,
-                   float* slab, float* slab_bias, void* stream);   // conv1w.hip
+                   float* slab, float* slab_bias, void* stream);
+int conv1_wgrad_kw3(const float* dz1, const uint8_t* obs, const int64_t* idx, long long row0, int B, int Z,
+                   float* slab, float* slab_bias, void* stream, int nw);   // conv1w.hip
 
 // conv1 forward: out [B][20][20][32] = relu(conv(obs rows, W1 torch layout) + b1)
 PPO_API int ppo_conv1_fwd(const void* obs, int obs_is_u8, const int64_t* idx, long long row0, int C, int B,
@@ -2447,7 +2449,10 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
     return 0;
   }
   if (obs_is_u8 && C == 4)
-    return conv1_wgrad_kw(dz1, (const uint8_t*)obs, idx, row0, B, Z, slab, slab_bias, stream);
+    return g_tune[TK_CONV1_WGRAD] >= 9
+               ? conv1_wgrad_kw3(dz1, (const uint8_t*)obs, idx, row0, B, Z, slab, slab_bias, stream,
+                                 g_tune[TK_CONV1_WGRAD] == 10 ? 8 : 4)
+               : conv1_wgrad_kw(dz1, (const uint8_t*)obs, idx, row0, B, Z, slab, slab_bias, stream);
   if (!obs_is_u8 && C == 4 && ((uintptr_t)obs & 15) == 0)   // conv1f.hip
     return ppo_conv1_wgrad_f32(dz1, (const float*)obs, idx, row0, B, Z, slab, slab_bias, stream);
   if (obs_is_u8) {   // any other channel count: the generic fp32-MFMA tile GEMM

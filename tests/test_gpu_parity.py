@@ -1498,12 +1498,13 @@ def test_gru_persistent_bptt_timeout_sets_error(gpu):
     assert err.item() == 0 and torch.isfinite(dgi).all() and (dgi[: n] != 0).any()
 
 
-@pytest.mark.parametrize("variant,Z", [(5, 0), (8, 0), (8, 256)])
+@pytest.mark.parametrize("variant,Z", [(5, 0), (8, 0), (8, 256), (9, 0), (9, 256), (9, 7), (10, 0), (10, 256), (10, 7)])
 def test_conv1_wgrad_variants_vs_torch(gpu, variant, Z):
     """conv1 weight + bias gradient from u8 observations gathered by index (the
     minibatch path): the part-pipelined bf16x3 kernel (5, 16 waves, two tiles per
-    wave) and the k-split kernel of conv1w.hip (8; Z = 256 leaves blocks with one
-    and two of the B = 300 images) vs torch float64 on (u8 / 255):
+    wave), the k-split kernels of conv1w.hip (8; 9 and 10 with one / two waves per SIMD; Z =
+    256 leaves blocks with one and two of the B = 300 images, Z = 7 walks 42-43
+    images per block) vs torch float64 on (u8 / 255):
     max |err| <= 1e-5 * max |ref|.  Rows gathered out of order."""
     Hh = _hip()
     B, rows = 300, 420
