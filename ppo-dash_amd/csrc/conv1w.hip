@@ -1,5 +1,6 @@
 // conv1 weight gradient on u8 observations, k-split over waves (round 4;
-// ppo_tune_set("conv1_wgrad", 8), the default):
+// ppo_tune_set("conv1_wgrad", 8); the default since round 5 is its one-wave-per-SIMD
+// form below, tune 9):
 //   dW1[co][(c, ky, kx)] = Σ_images Σ_px dz1[px][co] · u[c][4oy+ky][4ox+kx]
 // (the conv1 backward of CNNBase, T/a2c_ppo_acktr/model.py:177), exact: u8 pixels
 // are exact in bf16 and dz = hi + mid + lo (split_bf16x3), three
@@ -296,7 +297,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   // dz of (image b, k-step s): 8 pixels 16 s + 8 h + j of channel l32
   auto dz_load1 = [&](int b, int s, f32x8& d, int j) {
     const auto rs = make_rsrc(dz1 + (size_t)b * 12800, 12800 * 4);
-    d[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((16 * s + 8 * h) * 32 + l32) * 4 + 128 * j, 0, 0));
+    const int px = 16 * s + 4 * h + (j & 3) + 8 * (j >> 2);   // quads 4 s + h, 4 s + h + 2 (see qb)
+    d[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (px * 32 + l32) * 4, 0, 0));
   };
   float bacc = 0.f;
   // one pair (values 2 pr, 2 pr + 1) of split8's three-way split (the same bits)
@@ -319,12 +321,19 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   // TW NS); k-step 24, tile tail_tile(p - TW NS) (the tail)
   uint32_t braw[RING][6];
   // per-lane element offsets of the two quads of each step (lbase included): the
-  // tile part of a B address is then a compile-time constant (the ds_read offset)
+  // tile part of a B address is then a compile-time constant (the ds_read offset).
+  // Lane half h takes quads 4 s + h and 4 s + h + 2 of the k-step (pixels 16 s + 4 h
+  // .. +3, +8 .. +11; the A fragment's dz loads follow).  The 4-B tail reads are
+  // 2-way bank conflicts (ds_read_b32 banks by dword mod 32; the 16 (ky, x-phase)
+  // rows sit 12 dwords apart): 39 % of the LDS-active cycles
+  // (profiles/r05_y_kw3_sq.json).  Reading the tail as an aligned 8-B ds_read_b64
+  // (mod-64 banks: conflict-free) from an address the compiler cannot merge with the
+  // head read was slower, 1.75-1.78 vs 1.51-1.53 ms (an extra address add per read)
   int qb[NS + 1][2];
 #pragma unroll
   for (int i = 0; i <= NS; ++i)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) qb[i][k] = lbase + qoff(4 * (i < NS ? kg + 4 * i : 24) + 2 * h + k);
+    for (int k = 0; k < 2; ++k) qb[i][k] = lbase + qoff(4 * (i < NS ? kg + 4 * i : 24) + h + 2 * k);
   auto bread = [&](const uint16_t* S, int p) {
     const int i = p < TW * NS ? p / TW : NS, tt = p < TW * NS ? t0 + p % TW : tail_tile(p - TW * NS);
     const int toff = ((tt >> 1) * IMG + 4 * (tt & 1)) * ROWE;

@@ -1857,8 +1857,10 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // the superseded variants of rounds 1-4 live in git history, not in the library.
 //   conv1_fwd    0: image-resident bf16x3 kernel (u8, C = 4); 9: the generic tile GEMM
 //                (the path any other C takes), for A/B and its parity test
-//   conv1_wgrad  8: k-split kernel, u8 image by LDS-DMA (conv1w.hip, default);
-//                5: part-pipelined kernel (the half-precision mode's, bf16 dz)
+//   conv1_wgrad  9: k-split kernel with one wave per SIMD (conv1w.hip, default since
+//                round 5); 10: its two-waves-per-SIMD form; 8: the round-4 k-split
+//                kernel (8 waves, u8 image by LDS-DMA); 5: part-pipelined kernel (the
+//                half-precision mode's, bf16 dz)
 //   x9           1: fp32 GEMMs on the bf16 matrix cores (exact split, igemm_x9.h) where
 //                they measured faster; 0: fp32 MFMA (igemm.h); 2: the split core everywhere
 //   fc_splitk    K slices of the rollout-sized fc forward with a workspace (<= 1: unsplit)
@@ -1866,7 +1868,7 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 // ---------------------------------------------------------------------------
 enum { TK_CONV1_FWD, TK_CONV1_WGRAD, TK_X9, TK_FC_SPLITK, TK_RGB_AFF, TK_N };
 static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv1_wgrad", "x9", "fc_splitk", "rgb_aff"};
-static int g_tune[TK_N] = {0, 8, 1, 2, 1};
+static int g_tune[TK_N] = {0, 9, 1, 2, 1};
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
 static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measured best
@@ -2431,7 +2433,7 @@ PPO_API int ppo_conv1_wgrad(const float* dz1, const void* obs, int obs_is_u8, co
   const long long R = (long long)B * 400;
   PPO_REQUIRE(R < 0x7fffffffLL, "ppo_conv1_wgrad: B too large");
   const double fl = 2.0 * R * 32 * C * 64;
-  // u8 rows, C = 4: the k-split kernel (conv1w.hip, tune 8, fp32 dz) or the
+  // u8 rows, C = 4: the k-split kernels (conv1w.hip, tunes 8-10, fp32 dz) or the
   // part-pipelined kernel (tune 5; the half-precision mode's, bf16 dz)
   if (obs_is_u8 && C == 4 && (g_tune[TK_CONV1_WGRAD] == 5 || g_products == 1)) {
     if (B <= 0 || Z <= 0) return 0;

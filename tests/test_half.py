@@ -156,7 +156,7 @@ def test_half_precision_run_py_flow(gpu):
     assert all(np.isfinite(losses)) and (after - before).abs().max().item() > 0
 
 
-@pytest.mark.parametrize("conv1_wgrad", [5, 8])
+@pytest.mark.parametrize("conv1_wgrad", [5, 8, 9])
 def test_minibatch_gradient_deterministic(gpu, conv1_wgrad):
     """The fused minibatch backward is run-to-run deterministic (fixed-order
     reductions everywhere): two identical minibatches give bit-identical
