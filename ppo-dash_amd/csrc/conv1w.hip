@@ -246,7 +246,9 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw2_kernel(const float* _
 #ifndef KW3_FENCE
 #define KW3_FENCE 1
 #endif
-constexpr int KW3_RA = 3;   // B read-ahead in tiles (lgkmcnt holds 15: 4 reads per tile)
+#ifndef KW3_RA
+#define KW3_RA 3   // B read-ahead in tiles (lgkmcnt holds 15: 4 reads per tile)
+#endif
 // NW = 4: one wave per SIMD, all 8 column tiles per wave (tune 9); NW = 8: two waves
 // per SIMD, wave w = 2 kg + ch owning column tiles 4 ch .. 4 ch + 3 of the k-steps of
 // group kg (the pair kg splits the same dz; tune 10)
