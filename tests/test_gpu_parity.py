@@ -776,23 +776,26 @@ def test_cartpole_env_vs_oracle(gpu):
     assert ended > N   # plenty of terminations and TimeLimit truncations exercised
 
 
-def test_ppo_learns_cartpole(gpu):
+@pytest.mark.parametrize("N,Mb,iters", [(16, 4, 60), (8, 32, 60)])
+def test_ppo_learns_cartpole(gpu, N, Mb, iters):
     """c1 end to end (MLPBase hidden 64, GPU CartPole, GAE, PPO.update): the
-    mean finished-episode length must rise well above a random policy's ~22."""
+    mean finished-episode length must rise well above a random policy's ~22.
+    (8, 32) is c1's own shape (8 envs x 128 steps, 4 epochs, 32
+    minibatches of 32 samples)."""
     from a2c_ppo_acktr import model as M
     from a2c_ppo_acktr.algo import PPO
     from a2c_ppo_acktr.storage import RolloutStorage
     from a2c_ppo_acktr.synthetic import CartPoleVecEnv
     torch.manual_seed(0)
-    N, T = 16, 128
+    T = 128
     env = CartPoleVecEnv(N, seed=3, device=gpu)
     pol = M.Policy(env.obs_shape, env.action_space, base=M.MLPBase, base_kwargs={"recurrent": False})
     pol.to(gpu)
-    agent = PPO(pol, 0.2, 4, 4, 0.5, 0.0, lr=2.5e-3, eps=1e-5, max_grad_norm=0.5)
+    agent = PPO(pol, 0.2, 4, Mb, 0.5, 0.0, lr=2.5e-3, eps=1e-5, max_grad_norm=0.5)
     st = RolloutStorage(T, N, env.obs_shape, [0], env.action_space, 1, device=gpu)
     env.reset_into(st.obs[0])
     hist = []
-    for it in range(60):
+    for it in range(iters):
         tot = torch.zeros(2, device=gpu)
         for step in range(T):
             v, a, lp, h = pol.act(st.obs[step], st.vector_obs[step], st.recurrent_hidden_states[step],
