@@ -227,22 +227,22 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw2_kernel(const float* _
   }
 }
 
-// The same product with ONE wave per SIMD (round 5, ppo_tune_set("conv1_wgrad", 9)).
-// kw2's anatomy shows a chain of latencies per wave — one tile of
-// B read-ahead, the dz split in front of each k-step, a conversion phase between
-// two barriers — that its 256-VGPR budget leaves no room to pipeline.  Here 4
-// waves with 512 registers each (accumulators in AGPRs):
+// The same product with ONE wave per SIMD (round 5, ppo_tune_set("conv1_wgrad", 9),
+// the default).  kw2's anatomy shows a chain of latencies per wave —
+// one tile of B read-ahead, the dz split in front of each k-step, a conversion phase
+// between two barriers — that its 256-VGPR budget leaves no room to pipeline.  Here
+// 4 waves with 512 registers each (accumulators in AGPRs):
 //   * wave w: k-steps w + 4 i (i < 6) of every image and tiles 2 w, 2 w + 1 of
 //     k-step 24: 150 MFMAs per wave per image;
 //   * B fragments read RA tiles ahead through a ring (one flat sequence of the 50
 //     tiles of the image); the dz split of step i + 1 (and of the next image's step
-//     0) computed during step i; dz of the next image loaded one image ahead, one
-//     8-value slot per step;
+//     0) computed during step i; the dz slots and the next image's u8 bytes
+//     prefetched into registers a few steps ahead (schedule at the loop);
 //   * the next image converted into the other E stage during this image's steps,
-//     one or two 16-B items per step, from registers loaded one image ahead
-//     (plain buffer loads: no raw LDS buffer, no DMA): one barrier per image.
-// A timing variant of kw2's algorithm; the slab and its sums are kw2's (a
-// different summation order: not bit-identical to tune 8).
+//     one or two 16-B items per step (plain buffer loads: no raw LDS buffer, no
+//     DMA): one barrier per image.
+// The slab format and the sums are kw2's (a different summation order: not
+// bit-identical to tune 8).  kbench at Z = 256: 1.48-1.50 vs 1.585-1.59 ms.
 #ifndef KW3_FENCE
 #define KW3_FENCE 1
 #endif
