@@ -2164,7 +2164,7 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
 // [Z][M][H] and fc_splitk_reduce_kernel sums them in a fixed order, adds the bias
 // and applies ReLU.
 template <class C_>
-struct DenseFwdSplitK : DenseReluFwd<C_> {
+struct DenseFwdSplitK : DenseReluFwdB<C_> {   // branch-free operand loads (the launcher checks 4·M·K < 2^31)
   static constexpr bool VEC_STORE = false;   // partials go to the slab (store), never store4
   float* slab = nullptr;
   int chunk = 0;   // k per slice, a multiple of 32
@@ -2206,7 +2206,7 @@ PPO_API long long ppo_fc_fwd_ws_bytes(int M, int H) {
 PPO_API int ppo_fc_fwd_ws(const float* x, int M, const float* w4p, const float* b, int H, float* out, int ldo,
                           float* ws, long long ws_bytes, void* stream) {
   const long long need = ppo_fc_fwd_ws_bytes(M, H);
-  if (!use_x9() || need == 0 || ws == nullptr || ws_bytes < need || ldo % 4 != 0 || H % 4 != 0 ||
+  if (!use_x9() || need == 0 || ws == nullptr || ws_bytes < need || ldo % 4 != 0 || H % 4 != 0 || 4LL * M * 1568 >= 0x80000000LL ||
       ((uintptr_t)out & 15) != 0 || ((uintptr_t)ws & 15) != 0 || ((uintptr_t)b & 15) != 0)
     return ppo_fc_fwd(x, M, w4p, b, H, out, ldo, stream);
   const int K = 1568, Z = (int)(need / (4LL * M * H));
