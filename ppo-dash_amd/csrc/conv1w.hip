@@ -243,6 +243,9 @@ __global__ __launch_bounds__(NW * 64) void conv1_wgrad_kw2_kernel(const float* _
 //     DMA): one barrier per image.
 // The slab format and the sums are kw2's (a different summation order: not
 // bit-identical to tune 8).  kbench at Z = 256: 1.48-1.50 vs 1.585-1.59 ms.
+#ifndef KW3_BXT
+#define KW3_BXT 1
+#endif
 #ifndef KW3_FENCE
 #define KW3_FENCE 1
 #endif
@@ -267,8 +270,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   const int kg = NW == 8 ? w >> 1 : w, t0 = NW == 8 ? 4 * (w & 1) : 0;
   const bool counts = NW == 4 || (w & 1) == 0;   // the bias sum: one wave of each k-step group
   const int G = gridDim.x;
+  // column tiles: BXT (4 waves) — tile tt = (channel tt >> 1, x-phase half bx = tt & 1),
+  // lane l32 = (ky = l32 >> 2, dx = l32 & 3), so a tile's whole B fragment is either
+  // unshifted (bx = 0: one 8-B read per quad, no realignment) or shifted by one
+  // element (bx = 1: 8-B + 4-B read, two v_alignbyte by a constant); otherwise (the
+  // 8-wave form) tile tt = (channel, ky half), lane l32 = (ky & 3, kx) with a per-lane
+  // shift for kx >= 4
+  constexpr bool BXT = KW3_BXT && NW == 4;
   const int kx = l32 & 7, sh = 2 * (kx >> 2);
-  const int lbase = ((l32 >> 3) * 4 + (kx & 3)) * XW;
+  const int lbase = BXT ? l32 * XW : ((l32 >> 3) * 4 + (kx & 3)) * XW;
   // put items: thread item j = tid + NT j (2,016 of 2,048 slots are real)
   int isrc[IPT], idst[IPT];
 #pragma unroll
@@ -336,16 +346,18 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
   for (int i = 0; i <= NS; ++i)
 #pragma unroll
     for (int k = 0; k < 2; ++k) qb[i][k] = lbase + qoff(4 * (i < NS ? kg + 4 * i : 24) + h + 2 * k);
+  // the x-phase half of flat tile p (BXT; compile-time: t0 = 0 there)
+  auto bx_of = [&](int p) { return p < TW * NS ? (p % TW) & 1 : (p - TW * NS) & 1; };
   auto bread = [&](const uint16_t* S, int p) {
     const int i = p < TW * NS ? p / TW : NS, tt = p < TW * NS ? t0 + p % TW : tail_tile(p - TW * NS);
-    const int toff = ((tt >> 1) * IMG + 4 * (tt & 1)) * ROWE;
+    const int toff = BXT ? (tt >> 1) * IMG * ROWE : ((tt >> 1) * IMG + 4 * (tt & 1)) * ROWE;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const uint16_t* pp = S + toff + qb[i][k];
       const uint2 d01 = *reinterpret_cast<const uint2*>(pp);
       braw[p % RING][3 * k] = d01.x;
       braw[p % RING][3 * k + 1] = d01.y;
-      braw[p % RING][3 * k + 2] = *reinterpret_cast<const uint32_t*>(pp + 4);
+      if (!BXT || bx_of(p)) braw[p % RING][3 * k + 2] = *reinterpret_cast<const uint32_t*>(pp + 4);
     }
   };
   f32x16 acc[TW];
@@ -355,10 +367,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   auto mma3 = [&](int p, const Frag3& a, f32x16& c) {
     const uint32_t* r = braw[p % RING];
-    const bf16x8 bq = __builtin_bit_cast(bf16x8, uint4{__builtin_amdgcn_alignbyte(r[1], r[0], sh),
-                                                       __builtin_amdgcn_alignbyte(r[2], r[1], sh),
-                                                       __builtin_amdgcn_alignbyte(r[4], r[3], sh),
-                                                       __builtin_amdgcn_alignbyte(r[5], r[4], sh)});
+    bf16x8 bq;
+    if (BXT && !bx_of(p)) {
+      bq = __builtin_bit_cast(bf16x8, uint4{r[0], r[1], r[3], r[4]});
+    } else {
+      const int s2 = BXT ? 2 : sh;
+      bq = __builtin_bit_cast(bf16x8, uint4{__builtin_amdgcn_alignbyte(r[1], r[0], s2),
+                                            __builtin_amdgcn_alignbyte(r[2], r[1], s2),
+                                            __builtin_amdgcn_alignbyte(r[4], r[3], s2),
+                                            __builtin_amdgcn_alignbyte(r[5], r[4], s2)});
+    }
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, bq, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, bq, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, bq, c, 0, 0, 0);
@@ -525,7 +543,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW / 4,
     for (int t = 0; t < TW; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int co = (r & 3) + 8 * (r >> 2) + 4 * h, n = 32 * (t0 + t) + l32;
+        const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int n = BXT ? 64 * (t >> 1) + 8 * (l32 >> 2) + 4 * (t & 1) + (l32 & 3) : 32 * (t0 + t) + l32;
         out[co * 256 + n] = acc[t][r];
       }
   }
