@@ -539,7 +539,12 @@ __global__ __launch_bounds__(256) void relu_bits_kernel(const float* __restrict_
 //     output pixel (oy, ox) reads v + toff(ky, kx), v = 10 oy + ox.  Row i of row
 //     tile t is the t-th pixel (by v) with v ≡ i (mod 16) (≤ 6 per residue: 6
 //     tiles; a missing one is a dummy row reading pixel v = i): the 16 lanes of
-//     a ds_read_b128 group read 16 distinct residues, conflict-free.  Two stages
+//     a ds_read_b128 group read 16 distinct residues, conflict-free.  That leaves
+//     five real rows in the sixth tile (v = 80 .. 88: the sixth pixels of residues
+//     0, 2, 4, 6, 8).  MT = 5 (the standalone launches): residues 9, 11, 13, 15 have
+//     four pixels, so tile 4's rows 9, 11, 13, 15 take v = 82, 84, 86, 88 (a 2-way
+//     bank conflict in that tile's reads), and v = 80 (output (8, 0)) is left to
+//     conv2_fwd_lone_kernel, 16 images per tile; the fused trunk keeps MT = 6.  Two stages
 //     x 3 planes x 4 chunks x 400 x 16 B = 153,600 B.
 //   * The K-half partials (24,576 B) are handed over in the lo plane of the stage
 //     the image has just left: kh 1 writes them after barrier A, kh 0 reads them
@@ -555,12 +560,13 @@ __global__ __launch_bounds__(256) void relu_bits_kernel(const float* __restrict_
 // loads, 8 the epilogue stores (profiles/r04_c2f_anatomy_kbench.log)
 constexpr int C2F_STG = 3 * 4 * 400, C2F_MT = 6;   // conv2 forward: bf16x8 units per stage, row tiles
 constexpr int C2F_LDS = 2 * C2F_STG * 16 + 2 * C2F_MT * 16 * 4;   // stages + vtab + otab (154,368 B)
-template <int NP, bool MASK = false, int DBG = 0>
+template <int NP, bool MASK = false, int DBG = 0, int MT = C2F_MT>
 __device__ __forceinline__ void conv2_fwd_x9c_body(const float* __restrict__ a1, int B,
                                                    const uint16_t* __restrict__ wpl, const float* __restrict__ bias,
                                                    float* __restrict__ out, uint16_t* __restrict__ mbits,
                                                    uint8_t* __restrict__ lds) {
-  constexpr int U = 400, PLN = 4 * U, STG = 3 * PLN, MT = C2F_MT, KS = 8, WN = 64 * 512;
+  constexpr int U = 400, PLN = 4 * U, STG = 3 * PLN, KS = 8, WN = 64 * 512;
+  static_assert(MT == 5 || MT == 6, "row tiles: 6, or 5 with the lone pixel elsewhere");
   constexpr int UNITS = 4 * U, UPER = (UNITS + 511) / 512;   // 4 units per thread (the 4th: wave 0)
   static_assert(STG == C2F_STG, "stage size");
   bf16x8* const S = reinterpret_cast<bf16x8*>(lds);
@@ -571,11 +577,19 @@ __device__ __forceinline__ void conv2_fwd_x9c_body(const float* __restrict__ a1,
   if (tid < 16) {
     int t = 0;
     for (int v = tid; v <= 88; v += 16)
-      if (v % 10 != 9) {
+      if (v % 10 != 9 && t < MT) {
         vtab[t][tid] = v;
         otab[t][tid] = 9 * (v / 10) + v % 10;
         ++t;
       }
+    if (MT == 5 && t == 4) {   // residues 9, 11, 13, 15 (4 pixels each) take the sixth pixels
+      // of residues 2, 4, 6, 8 (v = 82 .. 88; a 2-way bank conflict in tile 4's reads);
+      // residue 0's (v = 80) is the lone pixel
+      const int v = 82 + (tid - 9);
+      vtab[4][tid] = v;
+      otab[4][tid] = 9 * (v / 10) + v % 10;
+      t = 5;
+    }
     for (; t < MT; ++t) {
       vtab[t][tid] = tid;
       otab[t][tid] = -1;
@@ -674,6 +688,7 @@ __device__ __forceinline__ void conv2_fwd_x9c_body(const float* __restrict__ a1,
         Frag3 a[3];
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
+          if (t0 + u >= MT) continue;
           const bf16x8* q = Sc + vrow[t0 + u] + toff;
           a[u].h = q[0];
           if constexpr (NP > 1) {
@@ -682,12 +697,13 @@ __device__ __forceinline__ void conv2_fwd_x9c_body(const float* __restrict__ a1,
           }
         }
 #define PPO_PART(X, Y) \
-  _Pragma("unroll") for (int u = 0; u < 3; ++u) acc[t0 + u] = mma(w.Y, a[u].X, acc[t0 + u]);
+  _Pragma("unroll") for (int u = 0; u < 3; ++u) if (t0 + u < MT) acc[t0 + u] = mma(w.Y, a[u].X, acc[t0 + u]);
         if constexpr ((DBG & 1) == 0) {
           PPO_PRODUCTS(NP, PPO_PART)
         } else {   // keep the fragment reads live
 #pragma unroll
-          for (int u = 0; u < 3; ++u) asm volatile("" ::"v"(a[u].h), "v"(a[u].m), "v"(a[u].l));
+          for (int u = 0; u < 3; ++u)
+            if (t0 + u < MT) asm volatile("" ::"v"(a[u].h), "v"(a[u].m), "v"(a[u].l));
         }
 #undef PPO_PART
       }
@@ -733,6 +749,9 @@ __device__ __forceinline__ void conv2_fwd_x9c_body(const float* __restrict__ a1,
   }
 }
 
+#ifndef C2F_LONE
+#define C2F_LONE 1   // standalone conv2 forward: five row tiles + conv2_fwd_lone_kernel
+#endif
 template <int NP, bool MASK = false, int DBG = 0>
 __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restrict__ a1, int B,
                                                            const uint16_t* __restrict__ wpl,
@@ -740,7 +759,75 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
                                                            float* __restrict__ out,
                                                            uint16_t* __restrict__ mbits) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[C2F_LDS];
-  conv2_fwd_x9c_body<NP, MASK, DBG>(a1, B, wpl, bias, out, mbits, lds);
+  conv2_fwd_x9c_body<NP, MASK, DBG, C2F_LONE ? 5 : 6>(a1, B, wpl, bias, out, mbits, lds);
+}
+
+// conv2 forward of output pixel 72 = (8, 0) (phase-grid v = 80, the sixth row tile's
+// only real row) for 16 images per tile: row i16 of the B operand is image 16 T +
+// i16, read straight from HBM (its 4 x 4 x 32 patch, a1 rows 16-19, columns 0-3).
+// The same operands as conv2_fwd_x9c_body's (the same split8 of the same 8-channel
+// chunks, the same weight planes), the same MFMA sequence per wave (k-steps of its
+// K half in order, parts in PPO_PRODUCTS order), the K halves summed kh 0 + kh 1,
+// the same epilogue: an MFMA output column depends only on its own B column, so the
+// result is bit-identical to a six-tile launch (test_trunk_fwd_equals_three_launches
+// compares against the fused trunk, which keeps six tiles).  Grid-stride over tiles.
+template <int NP, bool MASK>
+__global__ __launch_bounds__(512) void conv2_fwd_lone_kernel(const float* __restrict__ a1, int B,
+                                                             const uint16_t* __restrict__ wpl,
+                                                             const float* __restrict__ bias,
+                                                             float* __restrict__ out,
+                                                             uint16_t* __restrict__ mbits) {
+  constexpr int KS = 8, WN = 64 * 512, M = 72;
+  __shared__ f32x4 R[4 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int nt = wave & 3, kh = wave >> 2, co = 16 * nt + i16;
+  bf16x8 bw[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
+  const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
+  const int ntile = (B + 15) / 16;
+  for (int T = blockIdx.x; T < ntile; T += gridDim.x) {
+    const int b = 16 * T + i16;
+    const bool live = b < B;
+    // one resource per tile (uniform): the lanes of images past B read 0
+    const int nimg = B - 16 * T < 16 ? B - 16 * T : 16;
+    const auto ra = make_rsrc(a1 + (size_t)(16 * T) * 12800, nimg * 12800 * 4);
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int tap = 8 * kh + s, ky = tap >> 2, kx = tap & 3;
+      const int off = i16 * (12800 * 4) + (((16 + ky) * 20 + kx) * 32 + 8 * g) * 4;
+      const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+      const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
+      Frag3 a;
+      split8(x0, x1, a, NP == 1);
+      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+#define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
+      PPO_PRODUCTS(NP, PPO_PART)
+#undef PPO_PART
+    }
+    if (kh == 1) R[nt * 64 + lane] = acc;
+    __syncthreads();
+    if (kh == 0) {
+      const f32x4 v = acc + R[nt * 64 + lane];
+      f32x4 y;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
+      if (live) *reinterpret_cast<f32x4*>(out + (size_t)b * (81 * 64) + M * 64 + 16 * nt + 4 * g) = y;
+      if constexpr (MASK) {
+        int nib = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) nib |= (y[r] > 0.f ? 1 : 0) << r;
+        const int w16 = nib | (__shfl_down(nib, 16, 64) << 4) | (__shfl_down(nib, 32, 64) << 8) |
+                        (__shfl_down(nib, 48, 64) << 12);
+        if (g == 0 && live) mbits[((size_t)b * 81 + M) * 4 + nt] = (uint16_t)w16;
+      }
+    }
+    __syncthreads();   // R read before the next tile's partials
+  }
 }
 
 // conv2 weight gradient, image-resident on the bf16 matrix cores (exact split,
@@ -2058,6 +2145,16 @@ static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float*
   else if (mbits && g_products == 1) conv2_fwd_x9c_kernel<1, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
   else if (mbits) conv2_fwd_x9c_kernel<6, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
   else PPO_LAUNCH_NP(conv2_fwd_x9c_kernel, nb, 512, st, a1, B, wpl, b2, out, nullptr);
+  if (C2F_LONE) {   // output pixel 72 of every image (the five-tile kernel leaves it)
+    const int ntile = (B + 15) / 16;
+    const unsigned nl = (unsigned)(ntile < 1024 ? ntile : 1024);
+    if (mbits && g_products == 9) conv2_fwd_lone_kernel<9, true><<<nl, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+    else if (mbits && g_products == 1) conv2_fwd_lone_kernel<1, true><<<nl, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+    else if (mbits) conv2_fwd_lone_kernel<6, true><<<nl, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
+    else if (g_products == 9) conv2_fwd_lone_kernel<9, false><<<nl, 512, 0, st>>>(a1, B, wpl, b2, out, nullptr);
+    else if (g_products == 1) conv2_fwd_lone_kernel<1, false><<<nl, 512, 0, st>>>(a1, B, wpl, b2, out, nullptr);
+    else conv2_fwd_lone_kernel<6, false><<<nl, 512, 0, st>>>(a1, B, wpl, b2, out, nullptr);
+  }
   if (prof) ppo_prof_end(slot, st, 2.0 * B * 81 * 64 * 512);
   PPO_LAUNCH_CHECK("conv2_fwd_x9c_kernel");
   return 0;
