@@ -371,7 +371,8 @@ def pmc_traffic(kernel, workload):
 PMC_SYMBOL = {"conv2_fwd": "conv2_fwd_x9c_kernel<", "conv2_dgrad": "conv2_dgrad_x9_kernel<",
               "conv2_wgrad": "conv2_wgrad_x9_kernel<", "conv3_fwd": "conv3_fwd_x9_kernel<",
               "conv3_dgrad": "conv3_dgrad_x9_kernel<", "conv3_wgrad": "conv3_wgrad_x9_kernel<",
-              "conv1_wgrad_u8": "conv1_wgrad_parts_kernel<", "conv1_fwd_u8": "conv1_fwd_bf16x3_kernel<"}
+              "conv1_wgrad_u8": ("conv1_wgrad_kw3_kernel<", "conv1_wgrad_kw2_kernel<", "conv1_wgrad_parts_kernel<"),
+              "conv1_fwd_u8": "conv1_fwd_bf16x3_kernel<"}
 
 
 def pmc_mfma(workload):

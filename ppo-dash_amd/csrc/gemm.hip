@@ -789,21 +789,36 @@ __global__ __launch_bounds__(512) void conv2_fwd_lone_kernel(const float* __rest
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
   const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
   const int ntile = (B + 15) / 16;
+  // the tile's 8 k-steps of a1 chunks in registers; k-step s of the block's next
+  // tile is loaded as soon as this tile's k-step s has been split (one tile of
+  // load latency hidden behind the MFMAs, no extra registers)
+  f32x4 xa[KS][2];
+  auto load = [&](int T) {   // T >= ntile: loads of an image range of 0 bytes (read 0)
+    const int nimg = T < ntile ? (B - 16 * T < 16 ? B - 16 * T : 16) : 0;
+    const auto ra = make_rsrc(a1 + (size_t)(T < ntile ? 16 * T : 0) * 12800, nimg * 12800 * 4);
+    return ra;
+  };
+  auto load_s = [&](const __amdgpu_buffer_rsrc_t& ra, int s) {
+    const int tap = 8 * kh + s, ky = tap >> 2, kx = tap & 3;
+    const int off = i16 * (12800 * 4) + (((16 + ky) * 20 + kx) * 32 + 8 * g) * 4;
+    xa[s][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+    xa[s][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
+  };
+  {
+    const auto ra = load(blockIdx.x);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) load_s(ra, s);
+  }
   for (int T = blockIdx.x; T < ntile; T += gridDim.x) {
     const int b = 16 * T + i16;
     const bool live = b < B;
-    // one resource per tile (uniform): the lanes of images past B read 0
-    const int nimg = B - 16 * T < 16 ? B - 16 * T : 16;
-    const auto ra = make_rsrc(a1 + (size_t)(16 * T) * 12800, nimg * 12800 * 4);
+    const auto rn = load(T + gridDim.x);
     f32x4 acc = zero4();
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const int tap = 8 * kh + s, ky = tap >> 2, kx = tap & 3;
-      const int off = i16 * (12800 * 4) + (((16 + ky) * 20 + kx) * 32 + 8 * g) * 4;
-      const f32x4 x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
-      const f32x4 x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
       Frag3 a;
-      split8(x0, x1, a, NP == 1);
+      split8(xa[s][0], xa[s][1], a, NP == 1);
+      load_s(rn, s);
       const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
 #define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
       PPO_PRODUCTS(NP, PPO_PART)
@@ -2147,7 +2162,7 @@ static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float*
   else PPO_LAUNCH_NP(conv2_fwd_x9c_kernel, nb, 512, st, a1, B, wpl, b2, out, nullptr);
   if (C2F_LONE) {   // output pixel 72 of every image (the five-tile kernel leaves it)
     const int ntile = (B + 15) / 16;
-    const unsigned nl = (unsigned)(ntile < 1024 ? ntile : 1024);
+    const unsigned nl = (unsigned)(ntile < 512 ? ntile : 512);
     if (mbits && g_products == 9) conv2_fwd_lone_kernel<9, true><<<nl, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
     else if (mbits && g_products == 1) conv2_fwd_lone_kernel<1, true><<<nl, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
     else if (mbits) conv2_fwd_lone_kernel<6, true><<<nl, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);

@@ -60,16 +60,28 @@ def main():
     shutil.copy(os.path.join(OUT, "prof", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
     line = [l for l in open(os.path.join(OUT, "bench_full.log")) if l.startswith("{")][-1]
     open(os.path.join(prof, f"{tag}_bench.json"), "w").write(line)
-    fetch, nf = per_launch(os.path.join(OUT, "pmcb", "fetch_counter_collection.csv"), "FETCH_SIZE", sub)
-    write, nw = per_launch(os.path.join(OUT, "pmcb", "write_counter_collection.csv"), "WRITE_SIZE", sub)
-    # every instantiation of the kernel (e.g. the rollout and the mask-writing
-    # training forward) together: the launch mix bench.py's events time
-    tot_ns, calls = 0.0, 0
-    for r in csv.DictReader(open(os.path.join(OUT, "prof", "run_kernel_stats.csv"))):
-        if sub in r["Name"]:
-            tot_ns += float(r["TotalDurationNs"])
-            calls += int(r["Calls"])
-    avg_ms = tot_ns / calls / 1e6 if calls else None
+    # sub may name several kernels ("a|b"): one bench launch that runs them in
+    # sequence (conv2 forward: the five-tile kernel + the lone-pixel kernel); the
+    # per-launch figures are then the sums of the parts' per-launch averages
+    fetch = write = 0.0
+    nf = nw = 0
+    avg_ms = 0.0
+    calls = 0
+    for part in sub.split("|"):
+        f, n1 = per_launch(os.path.join(OUT, "pmcb", "fetch_counter_collection.csv"), "FETCH_SIZE", part)
+        w, n2 = per_launch(os.path.join(OUT, "pmcb", "write_counter_collection.csv"), "WRITE_SIZE", part)
+        fetch += f or 0.0
+        write += w or 0.0
+        nf, nw = max(nf, n1), max(nw, n2)
+        # every instantiation of the kernel (e.g. the rollout and the mask-writing
+        # training forward) together: the launch mix bench.py's events time
+        tot_ns, c = 0.0, 0
+        for r in csv.DictReader(open(os.path.join(OUT, "prof", "run_kernel_stats.csv"))):
+            if part in r["Name"]:
+                tot_ns += float(r["TotalDurationNs"])
+                c += int(r["Calls"])
+        avg_ms += tot_ns / c / 1e6 if c else 0.0
+        calls = max(calls, c)
     rd = 2.0 * fetch * 1024
     wr = write * 1024
     out = {"kernel": bench_kernel, "kernel_match": sub, "launches_fetch_pass": nf, "launches_write_pass": nw,
