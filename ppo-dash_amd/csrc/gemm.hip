@@ -1345,6 +1345,9 @@ __device__ __forceinline__ void conv3_fwd_x9_body(const float* __restrict__ a2, 
   }
 }
 
+#ifndef C3F_COMPACT
+#define C3F_COMPACT 1   // standalone conv3 forward: compact rows (conv3_fwd_c3_kernel) + the lone output
+#endif
 template <int NP>
 __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restrict__ a2, int B,
                                                           const uint16_t* __restrict__ wpl,
@@ -1353,6 +1356,167 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
   __shared__ __attribute__((aligned(16))) uint8_t lds[C3F_LDS];
   (void)stagger;
   conv3_fwd_x9_body<NP>(a2, B, wpl, bias, out, lds);
+}
+
+// conv3 forward with compact rows (round 5; the standalone launches): GEMM row m =
+// 7 oy + ox over the 49 real outputs (the 9-wide grid above issues 64 rows for
+// them), row tiles 0-2 (m < 48) on 12 waves — co tile w & 1, K half (w >> 1) & 1,
+// row tile w >> 2, one tile each — and output 48 = (6, 6) left to
+// conv3_fwd_lone_kernel.  A lane's tap pixel is p0(m) + 9 ky + kx, p0 = 9 oy + ox
+// (a per-lane base: the 16 rows of a tile are no longer 16 consecutive pixels, so
+// some ds_read_b128 groups meet 2-way bank conflicts).  The same operand splits,
+// k-steps, part order and K-half sum as conv3_fwd_x9_body, so every output is
+// bit-identical to it (the fused trunk keeps that body).  One block per CU (12
+// waves, 3 per SIMD).
+constexpr int C3C_LDS = 2 * 3 * C3F_PL * 2 + 2 * 2 * 3 * 64 * 16;   // stages + K-half partials (76,800 B)
+template <int NP>
+__global__ __launch_bounds__(768) void conv3_fwd_c3_kernel(const float* __restrict__ a2, int B,
+                                                           const uint16_t* __restrict__ wpl,
+                                                           const float* __restrict__ bias,
+                                                           float* __restrict__ out) {
+  constexpr int NPX = 84, PL = NPX * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, NT = 768;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[C3C_LDS];
+  uint16_t (*const S)[3 * PL] = reinterpret_cast<uint16_t (*)[3 * PL]>(lds);
+  f32x4 (*const R)[2][3][64] = reinterpret_cast<f32x4 (*)[2][3][64]>(lds + 2 * 3 * PL * 2);   // [stage][co tile][row tile][lane]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int nt = wave & 1, kh = (wave >> 1) & 1, mt = wave >> 2, co = 16 * nt + i16;
+  bf16x8 bw[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 576 + (9 * kh + s) * 32 + 8 * g);
+  const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
+  const int m = 16 * mt + i16, oy = m / 7, p0 = 9 * oy + (m - 7 * oy);
+  wait_vm0();
+  for (int i = tid; i < 2 * 3 * PL / 8; i += NT) reinterpret_cast<uint4*>(&S[0][0])[i] = uint4{0, 0, 0, 0};
+  f32x4 stg[2];
+  const bool has = tid < UNITS;   // one 8-channel unit per thread (648 of 768)
+  auto fetch = [&](int b) {   // a per-image buffer resource: the idle threads read 0, no branch
+    const auto ra = make_rsrc(a2 + (size_t)b * 5184, 5184 * 4);
+    const int off = has ? 32 * tid : 0x7fffffe0;
+    stg[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+    stg[1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
+  };
+  auto put = [&](int buf) {
+    if (has) {
+      const int p = tid >> 3, off = p * 64 + 8 * ((tid & 7) ^ ((p >> 1) & 7));
+      Frag3 f;
+      split8(stg[0], stg[1], f, false);
+      *reinterpret_cast<bf16x8*>(&S[buf][off]) = f.h;
+      *reinterpret_cast<bf16x8*>(&S[buf][PL + off]) = f.m;
+      *reinterpret_cast<bf16x8*>(&S[buf][2 * PL + off]) = f.l;
+    }
+  };
+  __syncthreads();   // the zeroed pad rows
+  const int G = gridDim.x;
+  int b = blockIdx.x, cur = 0;
+  if (b < B) {
+    fetch(b);
+    put(0);
+    fetch(b + G < B ? b + G : b);
+  }
+  __syncthreads();
+  for (; b < B; b += G) {
+    put(cur ^ 1);   // unconditional (past the end: a copy of this image into the idle stage)
+    const int bnn = b + 2 * G < B ? b + 2 * G : b;
+    const uint16_t* Sc = S[cur];
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int ks = 9 * kh + s, tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky, c = 4 * (ks & 1) + g;
+      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+      const int p = p0 + 9 * ky + kx;
+      const uint16_t* q = Sc + p * 64 + 8 * (c ^ ((p >> 1) & 7));
+      Frag3 a;
+      a.h = *reinterpret_cast<const bf16x8*>(q);
+      a.m = *reinterpret_cast<const bf16x8*>(q + PL);
+      a.l = *reinterpret_cast<const bf16x8*>(q + 2 * PL);
+#define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
+      PPO_PRODUCTS(NP, PPO_PART)
+#undef PPO_PART
+      if (s == 1) {
+        fetch(bnn);
+        __builtin_amdgcn_sched_barrier(0);   // the loads stay in their slot
+      }
+    }
+    if (kh == 1) R[cur][nt][mt][lane] = acc;
+    __syncthreads();   // stage cur consumed, stage cur ^ 1 complete, partials in R[cur]
+    if (kh == 0) {
+      const auto rs = make_rsrc(out + (size_t)b * (49 * 32), 49 * 32 * 4);
+      const f32x4 v = acc + R[cur][nt][mt][lane];
+      f32x4 y;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
+      bstore_f32x4(y, rs, 4 * (m * 32 + 16 * nt + 4 * g));
+    }
+    cur ^= 1;
+  }
+}
+
+// conv3 forward of output 48 = (6, 6) for 16 images per tile (row i16 of the B
+// operand: image 16 T + i16, its 3 x 3 x 64 patch straight from HBM), the same
+// operands, MFMA sequence, K-half sum and epilogue as the kernels above
+// (bit-identical); 4 waves (co tile w & 1, K half w >> 1), grid-stride over tiles,
+// the next tile's k-step s loaded once this tile's k-step s is split.
+template <int NP>
+__global__ __launch_bounds__(256) void conv3_fwd_lone_kernel(const float* __restrict__ a2, int B,
+                                                             const uint16_t* __restrict__ wpl,
+                                                             const float* __restrict__ bias,
+                                                             float* __restrict__ out) {
+  constexpr int KS = 9, WN = 32 * 576, M = 48, P0 = 60;
+  __shared__ f32x4 R[2 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int nt = wave & 1, kh = wave >> 1, co = 16 * nt + i16;
+  bf16x8 bw[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 576 + (9 * kh + s) * 32 + 8 * g);
+  const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
+  const int ntile = (B + 15) / 16;
+  f32x4 xa[KS][2];
+  auto load = [&](int T) {   // T >= ntile: a resource of 0 bytes (the loads read 0)
+    const int nimg = T < ntile ? (B - 16 * T < 16 ? B - 16 * T : 16) : 0;
+    return make_rsrc(a2 + (size_t)(T < ntile ? 16 * T : 0) * 5184, nimg * 5184 * 4);
+  };
+  auto load_s = [&](const __amdgpu_buffer_rsrc_t& ra, int s) {
+    const int ks = 9 * kh + s, tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky, c = 4 * (ks & 1) + g;
+    const int off = i16 * (5184 * 4) + ((P0 + 9 * ky + kx) * 64 + 8 * c) * 4;
+    xa[s][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+    xa[s][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
+  };
+  {
+    const auto ra = load(blockIdx.x);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) load_s(ra, s);
+  }
+  for (int T = blockIdx.x; T < ntile; T += gridDim.x) {
+    const int b = 16 * T + i16;
+    const auto rn = load(T + gridDim.x);
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      Frag3 a;
+      split8(xa[s][0], xa[s][1], a, false);
+      load_s(rn, s);
+      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+#define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
+      PPO_PRODUCTS(NP, PPO_PART)
+#undef PPO_PART
+    }
+    if (kh == 1) R[nt * 64 + lane] = acc;
+    __syncthreads();
+    if (kh == 0 && b < B) {
+      const f32x4 v = acc + R[nt * 64 + lane];
+      f32x4 y;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
+      *reinterpret_cast<f32x4*>(out + (size_t)b * (49 * 32) + M * 32 + 16 * nt + 4 * g) = y;
+    }
+    __syncthreads();   // R read before the next tile's partials
+  }
 }
 
 // The rollout's CNN trunk in one launch: conv1 -> conv2 -> conv3 forward as three
@@ -2192,8 +2356,15 @@ PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float*
   if (B <= 0) return 0;
   int slot;
   const bool prof = ppo_prof_begin("conv3_fwd", as_stream(stream), &slot);
-  PPO_LAUNCH_NP(conv3_fwd_x9_kernel, img_grid(B), 512, as_stream(stream), a2, B, planes_of(w3p, 32 * 576), b3, out,
-                g_stagger);
+  const uint16_t* wpl = planes_of(w3p, 32 * 576);
+  if (C3F_COMPACT) {   // compact rows (three tiles) + the lone output (6, 6)
+    PPO_LAUNCH_NP(conv3_fwd_c3_kernel, img_grid(B), 768, as_stream(stream), a2, B, wpl, b3, out);
+    const int ntile = (B + 15) / 16;
+    PPO_LAUNCH_NP(conv3_fwd_lone_kernel, (unsigned)(ntile < 512 ? ntile : 512), 256, as_stream(stream), a2, B, wpl,
+                  b3, out);
+  } else {
+    PPO_LAUNCH_NP(conv3_fwd_x9_kernel, img_grid(B), 512, as_stream(stream), a2, B, wpl, b3, out, g_stagger);
+  }
   if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
   PPO_LAUNCH_CHECK("conv3_fwd_x9_kernel");
   return 0;
