@@ -764,22 +764,30 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
 
 // conv2 forward of output pixel 72 = (8, 0) (phase-grid v = 80, the sixth row tile's
 // only real row) for 16 images per tile: row i16 of the B operand is image 16 T +
-// i16, read straight from HBM (its 4 x 4 x 32 patch, a1 rows 16-19, columns 0-3).
-// The same operands as conv2_fwd_x9c_body's (the same split8 of the same 8-channel
-// chunks, the same weight planes), the same MFMA sequence per wave (k-steps of its
-// K half in order, parts in PPO_PRODUCTS order), the K halves summed kh 0 + kh 1,
-// the same epilogue: an MFMA output column depends only on its own B column, so the
-// result is bit-identical to a six-tile launch (test_trunk_fwd_equals_three_launches
-// compares against the fused trunk, which keeps six tiles).  Grid-stride over tiles.
+// i16.  The tile's 16 patches (a1 rows 16-19, columns 0-3: 4 x 512 contiguous bytes
+// per image, 32 KB per tile) are loaded once per block — each thread four 16-B
+// pieces, the next tile's in registers during this tile's MFMAs — and staged in LDS
+// (two stages; image rows padded by 16 B so the 16 images of a fragment read hit
+// distinct banks): loading them per wave moved each chunk four times through the
+// L2, 107 vs 76 µs per 65,536 images (profiles/r05_zr_lone_anatomy.txt; two tiles
+// of loads in flight measured no faster).  The same operands as conv2_fwd_x9c_body's
+// (the same split8 of the same 8-channel chunks, the same weight planes), the same
+// MFMA sequence per wave (k-steps of its K half in order, parts in PPO_PRODUCTS
+// order), the K halves summed kh 0 + kh 1, the same epilogue: an MFMA output column
+// depends only on its own B column, so the result is bit-identical to a six-tile
+// launch (test_trunk_fwd_equals_three_launches compares against the fused trunk,
+// which keeps six tiles).  Grid-stride over tiles.
 template <int NP, bool MASK>
 __global__ __launch_bounds__(512) void conv2_fwd_lone_kernel(const float* __restrict__ a1, int B,
                                                              const uint16_t* __restrict__ wpl,
                                                              const float* __restrict__ bias,
                                                              float* __restrict__ out,
                                                              uint16_t* __restrict__ mbits) {
-  constexpr int KS = 8, WN = 64 * 512, M = 72;
+  constexpr int KS = 8, WN = 64 * 512, M = 72, IR = 129;   // IR: f32x4 per staged image row (128 + pad)
+  __shared__ f32x4 P[2][16 * IR];
   __shared__ f32x4 R[4 * 64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nt = wave & 3, kh = wave >> 2, co = 16 * nt + i16;
   bf16x8 bw[KS][3];
 #pragma unroll
@@ -787,46 +795,51 @@ __global__ __launch_bounds__(512) void conv2_fwd_lone_kernel(const float* __rest
 #pragma unroll
     for (int p = 0; p < 3; ++p)
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
-  const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
   const int ntile = (B + 15) / 16;
-  // the tile's 8 k-steps of a1 chunks in registers; k-step s of the block's next
-  // tile is loaded as soon as this tile's k-step s has been split (one tile of
-  // load latency hidden behind the MFMAs, no extra registers)
-  f32x4 xa[KS][2];
-  auto load = [&](int T) {   // T >= ntile: loads of an image range of 0 bytes (read 0)
+  // piece q = tid + 512 j (j < 4) of a tile: image q >> 7, f32x4 f = q & 127 of its
+  // patch = tap (4 ky + kx) * 8 + channel quad; a1 offset (16 + ky) * 640 + (f & 31) * 4
+  f32x4 pc[4];
+  auto fetch = [&](int T) {   // T >= ntile: a resource of 0 bytes (the loads read 0)
     const int nimg = T < ntile ? (B - 16 * T < 16 ? B - 16 * T : 16) : 0;
     const auto ra = make_rsrc(a1 + (size_t)(T < ntile ? 16 * T : 0) * 12800, nimg * 12800 * 4);
-    return ra;
-  };
-  auto load_s = [&](const __amdgpu_buffer_rsrc_t& ra, int s) {
-    const int tap = 8 * kh + s, ky = tap >> 2, kx = tap & 3;
-    const int off = i16 * (12800 * 4) + (((16 + ky) * 20 + kx) * 32 + 8 * g) * 4;
-    xa[s][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
-    xa[s][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
-  };
-  {
-    const auto ra = load(blockIdx.x);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) load_s(ra, s);
-  }
+    for (int j = 0; j < 4; ++j) {
+      const int q = tid + 512 * j, im = q >> 7, f = q & 127;
+      const int off = (im * 12800 + (16 + (f >> 5)) * 640 + (f & 31) * 4) * 4;
+      pc[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+    }
+  };
+  auto put = [&](int st) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = tid + 512 * j;
+      P[st][(q >> 7) * IR + (q & 127)] = pc[j];
+    }
+  };
+  fetch(blockIdx.x);
+  put(0);
+  __syncthreads();
+  int cur = 0;
   for (int T = blockIdx.x; T < ntile; T += gridDim.x) {
+    fetch(T + gridDim.x);
     const int b = 16 * T + i16;
     const bool live = b < B;
-    const auto rn = load(T + gridDim.x);
     f32x4 acc = zero4();
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
+      const f32x4* x = &P[cur][i16 * IR + (8 * kh + s) * 8 + 2 * g];
       Frag3 a;
-      split8(xa[s][0], xa[s][1], a, NP == 1);
-      load_s(rn, s);
+      split8(x[0], x[1], a, NP == 1);
       const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
 #define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
       PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
     }
     if (kh == 1) R[nt * 64 + lane] = acc;
-    __syncthreads();
+    put(cur ^ 1);   // the stage read one tile ago (the last barrier retired its reads)
+    __syncthreads();   // partials in R; stage cur ^ 1 complete
     if (kh == 0) {
+      const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
       const f32x4 v = acc + R[nt * 64 + lane];
       f32x4 y;
 #pragma unroll
@@ -842,6 +855,7 @@ __global__ __launch_bounds__(512) void conv2_fwd_lone_kernel(const float* __rest
       }
     }
     __syncthreads();   // R read before the next tile's partials
+    cur ^= 1;
   }
 }
 
