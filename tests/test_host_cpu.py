@@ -177,3 +177,35 @@ def test_gemm_plane_swizzle_conflict_free():
     out = subprocess.run([sys.executable, os.path.join(root, "tools", "swizzle_check.py")], capture_output=True,
                          text=True, check=True).stdout
     assert "reads 1 non-KC writes 1 KC writes 1" in out
+
+
+def test_conv_row_tiles_cover_every_output_once():
+    """Row-tile maps of the standalone conv forwards (gemm.hip conv2_fwd_x9c_body
+    with MT = 5 + conv2_fwd_lone_kernel; conv3_fwd_c3_kernel + conv3_fwd_lone_kernel),
+    restated: every output pixel is computed exactly once, dummy rows write nothing,
+    and a 16-row tile's phase-grid rows collide in residue mod 16 (a bank conflict of
+    the fragment read) at most 2-way.  conv2: v = 10 oy + ox over the 9 x 10 phase
+    grid, m = 9 oy + ox; the lone pixel is v = 80 (m = 72).  conv3: compact rows
+    m = 7 oy + ox < 48 on three tiles, m = 48 lone."""
+    vtab = [[None] * 16 for _ in range(5)]
+    for tid in range(16):
+        t = 0
+        for v in range(tid, 89, 16):
+            if v % 10 != 9 and t < 5:
+                vtab[t][tid] = v
+                t += 1
+        if t == 4:   # residues 9, 11, 13, 15 take v = 82 .. 88
+            vtab[4][tid] = 82 + (tid - 9)
+            t = 5
+        assert t == 5
+    outs = [9 * (v // 10) + v % 10 for row in vtab for v in row] + [72]
+    assert sorted(outs) == list(range(81))
+    for row in vtab:
+        res = [v % 16 for v in row]
+        assert max(res.count(r) for r in set(res)) <= 2
+    conv3 = [16 * t + i for t in range(3) for i in range(16)] + [48]
+    assert sorted(conv3) == list(range(49))
+    # tap pixels of the compact rows stay on the 9 x 9 grid (no pad row reached)
+    for m in range(48):
+        oy, ox = divmod(m, 7)
+        assert 9 * oy + ox + 9 * 2 + 2 <= 80
