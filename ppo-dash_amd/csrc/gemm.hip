@@ -1469,18 +1469,22 @@ __global__ __launch_bounds__(768) void conv3_fwd_c3_kernel(const float* __restri
 }
 
 // conv3 forward of output 48 = (6, 6) for 16 images per tile (row i16 of the B
-// operand: image 16 T + i16, its 3 x 3 x 64 patch straight from HBM), the same
-// operands, MFMA sequence, K-half sum and epilogue as the kernels above
-// (bit-identical); 4 waves (co tile w & 1, K half w >> 1), grid-stride over tiles,
-// the next tile's k-step s loaded once this tile's k-step s is split.
+// operand: image 16 T + i16), the same operands, MFMA sequence, K-half sum and
+// epilogue as the kernels above (bit-identical); 4 waves (co tile w & 1, K half
+// w >> 1), grid-stride over tiles.  As conv2_fwd_lone_kernel, the tile's 16 patches
+// (3 rows of 3 pixels x 64 channels, 768 contiguous bytes per row) are loaded once
+// per block, the next tile's in registers during this tile's MFMAs, and staged in
+// LDS (two stages, image rows padded by 16 B).
 template <int NP>
 __global__ __launch_bounds__(256) void conv3_fwd_lone_kernel(const float* __restrict__ a2, int B,
                                                              const uint16_t* __restrict__ wpl,
                                                              const float* __restrict__ bias,
                                                              float* __restrict__ out) {
-  constexpr int KS = 9, WN = 32 * 576, M = 48, P0 = 60;
+  constexpr int KS = 9, WN = 32 * 576, M = 48, IR = 145, NPC = 9;   // IR: f32x4 per staged image (144 + pad)
+  __shared__ f32x4 P[2][16 * IR];
   __shared__ f32x4 R[2 * 64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nt = wave & 1, kh = wave >> 1, co = 16 * nt + i16;
   bf16x8 bw[KS][3];
 #pragma unroll
@@ -1488,41 +1492,51 @@ __global__ __launch_bounds__(256) void conv3_fwd_lone_kernel(const float* __rest
 #pragma unroll
     for (int p = 0; p < 3; ++p)
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 576 + (9 * kh + s) * 32 + 8 * g);
-  const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
   const int ntile = (B + 15) / 16;
-  f32x4 xa[KS][2];
-  auto load = [&](int T) {   // T >= ntile: a resource of 0 bytes (the loads read 0)
+  // piece q = tid + 256 j (j < 9): image q / 144, f32x4 f = q % 144 of its patch =
+  // ky * 48 + kx * 16 + channel quad; a2 offset ((6 + ky) * 9 + 6) * 64 + (f % 48) * 4
+  f32x4 pc[NPC];
+  auto fetch = [&](int T) {   // T >= ntile: a resource of 0 bytes (the loads read 0)
     const int nimg = T < ntile ? (B - 16 * T < 16 ? B - 16 * T : 16) : 0;
-    return make_rsrc(a2 + (size_t)(T < ntile ? 16 * T : 0) * 5184, nimg * 5184 * 4);
-  };
-  auto load_s = [&](const __amdgpu_buffer_rsrc_t& ra, int s) {
-    const int ks = 9 * kh + s, tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky, c = 4 * (ks & 1) + g;
-    const int off = i16 * (5184 * 4) + ((P0 + 9 * ky + kx) * 64 + 8 * c) * 4;
-    xa[s][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
-    xa[s][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
-  };
-  {
-    const auto ra = load(blockIdx.x);
+    const auto ra = make_rsrc(a2 + (size_t)(T < ntile ? 16 * T : 0) * 5184, nimg * 5184 * 4);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) load_s(ra, s);
-  }
+    for (int j = 0; j < NPC; ++j) {
+      const int q = tid + 256 * j, im = q / 144, f = q - 144 * im, ky = f / 48;
+      const int off = (im * 5184 + ((6 + ky) * 9 + 6) * 64 + (f - 48 * ky) * 4) * 4;
+      pc[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+    }
+  };
+  auto put = [&](int st) {
+#pragma unroll
+    for (int j = 0; j < NPC; ++j) {
+      const int q = tid + 256 * j, im = q / 144;
+      P[st][im * IR + (q - 144 * im)] = pc[j];
+    }
+  };
+  fetch(blockIdx.x);
+  put(0);
+  __syncthreads();
+  int cur = 0;
   for (int T = blockIdx.x; T < ntile; T += gridDim.x) {
+    fetch(T + gridDim.x);
     const int b = 16 * T + i16;
-    const auto rn = load(T + gridDim.x);
     f32x4 acc = zero4();
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
+      const int ks = 9 * kh + s, tap = ks >> 1, c = 4 * (ks & 1) + g;
+      const f32x4* x = &P[cur][i16 * IR + tap * 16 + 2 * c];
       Frag3 a;
-      split8(xa[s][0], xa[s][1], a, false);
-      load_s(rn, s);
+      split8(x[0], x[1], a, false);
       const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
 #define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
       PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
     }
     if (kh == 1) R[nt * 64 + lane] = acc;
-    __syncthreads();
+    put(cur ^ 1);   // the stage read one tile ago (the last barrier retired its reads)
+    __syncthreads();   // partials in R; stage cur ^ 1 complete
     if (kh == 0 && b < B) {
+      const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
       const f32x4 v = acc + R[nt * 64 + lane];
       f32x4 y;
 #pragma unroll
@@ -1530,6 +1544,7 @@ __global__ __launch_bounds__(256) void conv3_fwd_lone_kernel(const float* __rest
       *reinterpret_cast<f32x4*>(out + (size_t)b * (49 * 32) + M * 32 + 16 * nt + 4 * g) = y;
     }
     __syncthreads();   // R read before the next tile's partials
+    cur ^= 1;
   }
 }
 
