@@ -48,6 +48,7 @@ METRIC = "env-steps/sec (rollout+GAE+PPO update) at 4096 envs×128 steps, 1/2/4/
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 MFMA = vector peak (dense)
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 PEAK_HBM_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+NOMINAL_SCLK_GHZ = 2.4          # the shader clock the MFMA peaks are quoted at
 
 # Every HIP kernel family of the iteration and the roofline that bounds it
 # (DESIGN.md §5): name (as the library's event profiler tags the launch) ->
@@ -163,7 +164,10 @@ def parse():
                         "accumulation and masters) — a separate line, never the fp32 headline")
     p.add_argument("--tune", default="", help="key=v[,key=v...] ppo_tune_set overrides (A/B runs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-envs", type=int, default=32)
+    p.add_argument("--cpu-envs", type=int, default=128)
+    p.add_argument("--cpu-steps", type=int, default=32,
+                   help="rollout steps per CPU-baseline iteration (per-env-step cost is independent of T)")
+    p.add_argument("--cpu-reps", type=int, default=5)
     p.add_argument("--cpu-threads", type=int, default=None,
                    help="threads of the multi-threaded CPU baseline (default: OMP_NUM_THREADS or the core count, <= 16)")
     p.add_argument("--no-gae-roofline", action="store_true")
@@ -368,9 +372,11 @@ def pmc_traffic(kernel, workload):
 
 
 # bench kernel name -> the kernel symbol in the rocprofv3 PMC summaries
-PMC_SYMBOL = {"conv2_fwd": "conv2_fwd_x9c_kernel<", "conv2_dgrad": "conv2_dgrad_x9_kernel<",
-              "conv2_wgrad": "conv2_wgrad_x9_kernel<", "conv3_fwd": "conv3_fwd_x9_kernel<",
+PMC_SYMBOL = {"conv2_fwd": ("conv2_fwd_x9c_kernel<", "conv2_fwd_lone_kernel<"),
+              "conv2_dgrad": "conv2_dgrad_x9_kernel<", "conv2_wgrad": "conv2_wgrad_x9_kernel<",
+              "conv3_fwd": ("conv3_fwd_c3_kernel<", "conv3_fwd_lone_kernel<", "conv3_fwd_x9_kernel<"),
               "conv3_dgrad": "conv3_dgrad_x9_kernel<", "conv3_wgrad": "conv3_wgrad_x9_kernel<",
+              "trunk_fwd": "trunk_fwd_kernel<",
               "conv1_wgrad_u8": ("conv1_wgrad_kw3_kernel<", "conv1_wgrad_kw2_kernel<", "conv1_wgrad_parts_kernel<"),
               "conv1_fwd_u8": "conv1_fwd_bf16x3_kernel<"}
 
@@ -385,7 +391,7 @@ def pmc_mfma(workload):
         return {}, None
     if m.get("workload") != workload:
         return {}, None
-    out = {}
+    out, clk = {}, {}
     for name, sym in PMC_SYMBOL.items():
         # all instantiations (e.g. the rollout and the mask-writing training
         # forward): busy cycles are proportional to MFMA instructions, so the
@@ -394,7 +400,12 @@ def pmc_mfma(workload):
                  for k, v in m["kernels"].items() if k.startswith(sym) and v["mfma_util"] > 0]
         if parts:
             out[name] = round(sum(w for w, _ in parts) / sum(w / u for w, u in parts), 4)
-    return out, d["mfma_util_file"]
+        # shader clock of the kernel's launches (cycles-weighted over its instantiations)
+        cyc = [(v["sclk_ghz"] * v["pmc_avg_launch_ms"] * v["launches"], v["pmc_avg_launch_ms"] * v["launches"])
+               for k, v in m["kernels"].items() if k.startswith(sym) and v.get("sclk_ghz")]
+        if cyc:
+            clk[name] = round(sum(c for c, _ in cyc) / sum(t for _, t in cyc), 4)
+    return out, clk, d["mfma_util_file"]
 
 
 def cpu_model():
@@ -446,15 +457,18 @@ def cpu_baseline(envs, T, E, M, hidden, threads, reps=3):
         torch.set_num_threads(saved)
         torch.set_rng_state(rng_state)
     best = max(runs, key=lambda k: runs[k][0])
+    bt = runs[best][2]
     return {"value": round(runs[best][0], 2), "unit": "env-steps/s", "cores": best, "kind": "port",
             "cpu_model": cpu_model(),
+            "runs_s": [round(x, 3) for x in bt],
+            "range": [round(envs * T / max(bt), 2), round(envs * T / min(bt), 2)],
             "by_threads": {str(k): {"value": round(v[0], 2), "seconds": round(v[1], 2),
                                     "runs_s": [round(x, 3) for x in v[2]]} for k, v in runs.items()},
             "sample": f"the reference CPU path (T/run.py:168-248) restated in torch on the host "
                       f"(oracle/torch_ref.py: F.conv2d/linear, autograd, torch.optim.Adam, clip_grad_norm_, "
                       f"fp32 obs storage), CNNBase H={hidden}, {envs} envs x {T} steps, {E} epochs x {M} "
                       f"minibatches; per thread setting one warm-up iteration then the median of {reps} "
-                      f"iterations; value = the faster setting"}
+                      f"iterations (range = slowest..fastest of them); value = the faster setting"}
 
 
 def free_port():
@@ -728,10 +742,16 @@ def main():
                 kernels[name]["ms_per_iteration"] = e["ms_per_iteration"]
             else:
                 kernels[name] = e
-    util, util_src = pmc_mfma(workload)
+    util, clk, util_src = pmc_mfma(workload)
     for name, u in util.items():
         if name in kernels:
             kernels[name]["mfma_util_pmc"] = u
+    for name, c in clk.items():
+        # frac is against the nominal 2.4 GHz peak (the headline); frac_at_clock
+        # against the peak at the clock the kernel was measured at in the PMC pass
+        if name in kernels:
+            kernels[name]["sclk_ghz_pmc"] = c
+            kernels[name]["frac_at_clock"] = round(kernels[name]["frac"] * NOMINAL_SCLK_GHZ / c, 4)
     roof = None
     timed = {k: v for k, v in kernels.items() if v["timed_in"] == "timed region"}
     if timed:
@@ -743,11 +763,12 @@ def main():
                 "traffic_unit": "bytes/launch (HBM, PMC)", "traffic_source": tsrc, "kernel": dom,
                 "launches": kd["launches"], "avg_launch_ms": kd["avg_launch_ms"],
                 "mfma_util_pmc": kd.get("mfma_util_pmc"), "mfma_util_source": util_src,
+                "sclk_ghz_pmc": kd.get("sclk_ghz_pmc"), "frac_at_clock": kd.get("frac_at_clock"),
                 "flop_per_launch": round(per_kernel[dom][2] / per_kernel[dom][0])}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1))
-        cpu = cpu_baseline(args.cpu_envs, T, E, M, H, threads)
+        cpu = cpu_baseline(args.cpu_envs, args.cpu_steps, E, M, H, threads, reps=args.cpu_reps)
     value = N * T * world * args.steps / elapsed
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,

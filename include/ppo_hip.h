@@ -38,6 +38,8 @@ extern "C" {
 #define PPO_ESHAPE 1002
 
 const char* ppo_last_error(void);
+/* 3 (round 6): symbols removed in round 5 (ppo_a1split_*, ppo_conv*_split, the anatomy
+ * probes) and the GRU counter buffer grown to (3 + 32)·G ints (ppo_gru_seq_counters) */
 int ppo_abi_version(void);
 /* launch-level event profiler used by bench.py: time every launch of the named
  * kernel (NULL disables); collect -> {launches, Σ ms, Σ algorithmic FLOP} */
@@ -223,17 +225,23 @@ int ppo_wgrad_reduce(const float* slab, const float* slab_bias, int Z, int M, in
 /* deterministic column sums out[c] = scale·Σ_r src[r*ld + c] (split-partial reduces) */
 int ppo_colsum(const float* src, long long ld, int rows, long long cols, float* out, float scale, int accumulate,
                void* stream);
-/* run-time knobs (A/B and test hooks; each key selects between the default and the
- * one kept alternative, any other value is refused with PPO_EARG):
- *   "products"    part products per operand pair of the split-bf16 fp32 GEMMs:
- *                 6 (default: dropped terms < 2^-26 |a·b|), 9 (every product exact),
- *                 1 (the half-precision mode's one bf16 product)
+/* run-time knobs (A/B and test hooks; each key takes the listed values, any other
+ * value is refused with PPO_EARG):
+ *   "products"    part products per operand pair of the split-bf16 fp32 GEMMs of the
+ *                 conv / fc kernels: 6 (default: dropped terms < 2^-26 |a·b|), 9 (every
+ *                 product exact), 1 (the half-precision mode's one bf16 product).  The
+ *                 GRU's W_hh products (H >= 128) always take 6 (fp32 MFMA at H = 64)
  *   "conv1_fwd"   0 image-resident kernel (default), 9 the generic tile GEMM
- *   "conv1_wgrad" 8 k-split kernel (default), 5 part-pipelined kernel
+ *   "conv1_wgrad" 9 one-wave-per-SIMD k-split kernel (default), 10 its wave-pair form,
+ *                 8 the eight-wave k-split kernel, 5 the part-pipelined kernel
  *   "x9"          1 split-bf16 dense GEMMs (default), 0 fp32 MFMA, 2 split everywhere
- *   "fc_splitk"   K slices of the rollout-sized fc forward (default 2)
+ *   "fc_splitk"   K slices of the rollout-sized fc forward, 0..8 (default 2)
  *   "rgb_aff"     1 affine-folded raw RGB conv1 (default), 0 bit-exact decode
- *   "stagger", "small_b", "heads_lds": schedule / small-batch / heads-kernel switches */
+ *   "stagger"     schedule bits 0..15 (default 2; every value gives the same results);
+ *                 larger values are refused (they select timing-anatomy paths that give
+ *                 wrong results by design, accepted only by a -DPPO_DIAG build)
+ *   "small_b"     forwards of at most this many samples take small.hip's kernels (>= 0)
+ *   "heads_lds"   0 / non-zero: the LDS-weight heads_train kernel off / on (default on) */
 int ppo_tune_set(const char* key, int value);
 /* current value of a tune key (-1 if unknown) */
 int ppo_tune_get(const char* key);

@@ -2194,6 +2194,12 @@ PPO_API int ppo_tune_set(const char* key, int value) {
     return 0;
   }
   if (strcmp(key, "stagger") == 0) {
+#ifndef PPO_DIAG
+    // bits 0-3 are schedule switches (same results); bits >= 4 select the timing-
+    // anatomy paths of diagnostic kernels (wrong results by design): -DPPO_DIAG only
+    PPO_REQUIRE(value >= 0 && value < 16, "ppo_tune_set: stagger takes schedule bits 0..15, got %d "
+                "(the anatomy bits need a -DPPO_DIAG build)", value);
+#endif
     g_stagger = value;
     return 0;
   }

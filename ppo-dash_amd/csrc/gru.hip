@@ -1034,10 +1034,7 @@ int launch_step16(const float* hprev, const float* masks, const int64_t* mask_id
                   const float* bhh, const float* gi, int M, float* hout, float* sr, float* sz, float* sn,
                   float* sghn, float* shin, hipStream_t st) {
   // at most two blocks per CU: more row groups than that loop inside a block
-  int dev = 0, n_cu = 256;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                              hipSuccess || n_cu <= 0)
-    n_cu = 256;
+  const int n_cu = gru_cus();
   // (4,096 rows, H = 256: 0.030 -> 0.021 ms; one, three or four blocks per CU 0.024-0.028,
   // profiles/r05_n_gru_step.log)
   const int gx = std::min((int)ceil_div(M, 32), std::max(1, 2 * n_cu / (H / 16)));

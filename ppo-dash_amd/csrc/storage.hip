@@ -118,7 +118,7 @@ PPO_API int ppo_prof_collect_one(int idx, double* out3) {
 }
 
 PPO_API int ppo_prof_collect(double* out3) { return ppo_prof_collect_one(-1, out3); }
-PPO_API int ppo_abi_version(void) { return 2; }
+PPO_API int ppo_abi_version(void) { return 3; }
 
 namespace {
 

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = _hip.lib()   # loads without a GPU; no compute calls are made
     missing = [s for s in header_symbols() if not hasattr(lib, s)]
     assert not missing, missing
-    assert lib.ppo_abi_version() == 2
+    assert lib.ppo_abi_version() == 3
 
 
 def test_ctypes_table_matches_header():
@@ -107,7 +107,40 @@ def test_policy_construction_matches_reference_init():
         pol.base.gru.bias_ih_l0.copy_(torch.rand(96, generator=gw) * 0.6 - 0.3)
         pol.base.gru.bias_hh_l0.copy_(torch.rand(96, generator=gw) * 0.6 - 0.3)
     assert np.array_equal(torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy(), u["init_params"])
+    # the production-size replays: c3's H = 512 CNN and c5's
+    # H = 256 GRU + 14 vector obs, constructed in the reference's order
+    for name in ("cnn_update_h512.npz", "cnn_update_wide.npz"):
+        c = golden(name)
+        torch.manual_seed(1)
+        pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase, base_kwargs={"recurrent": False, "hidden_size": 512})
+        assert np.array_equal(torch.get_rng_state().numpy(), c["rng_after_init"]), name
+        assert np.array_equal(torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy(), c["init_params"])
+    u = golden("gru_update_h256.npz")
+    torch.manual_seed(31)
+    pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase, base_kwargs={"recurrent": True, "hidden_size": 256},
+                   vector_obs_len=14)
+    assert np.array_equal(torch.get_rng_state().numpy(), u["rng_after_init"])
+    gw = torch.Generator().manual_seed(32)
+    with torch.no_grad():
+        pol.dist.linear.weight.mul_(40.0)
+        pol.base.gru.bias_ih_l0.copy_(torch.rand(768, generator=gw) * 0.6 - 0.3)
+        pol.base.gru.bias_hh_l0.copy_(torch.rand(768, generator=gw) * 0.6 - 0.3)
+    assert np.array_equal(torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).numpy(), u["init_params"])
     torch.set_num_threads(nt)
+
+
+def test_wide_fixture_observations_regenerate():
+    """cnn_update_wide.npz stores its 129 x 128 observation frames as a generator
+    seed: torch.randint on a seeded CPU generator reproduces them (byte sum and
+    CRC-32 recorded at generation), as the GPU replay regenerates them."""
+    import zlib
+    import torch
+    from conftest import golden
+    d = golden("cnn_update_wide.npz")
+    hidden, N, T, E, Mb = (int(x) for x in d["meta"])
+    o = torch.randint(0, 256, (T + 1, N, 4, 84, 84), dtype=torch.uint8,
+                      generator=torch.Generator().manual_seed(int(d["obs_seed"][0]))).numpy()
+    assert [int(o.sum(dtype=np.int64)), zlib.crc32(o.tobytes())] == [int(x) for x in d["obs_check"]]
 
 
 def test_update_linear_schedule_drives_optimizer_lr():

@@ -300,3 +300,69 @@ def test_oracle_gru_backward_vs_finite_difference():
         xx[i] -= 2 * eps
         fdx[i] = (lp - loss(p, xx)) / (2 * eps)
     np.testing.assert_allclose(dx, fdx, rtol=1e-6, atol=1e-8)
+
+
+# --------------------------------------------- production hidden sizes
+def _digest_check(got_flat, d, prefix, shapes, tol, scale=1.0):
+    """A fixture digest (tools/gen_golden.py digest: every 8th element, per-tensor
+    max |x| and L2) against a full flat array: sampled elements within tol x the
+    tensor's max |x|, each tensor's L2 within 1e-5 relative."""
+    idx = d[f"{prefix}_idx"]
+    ref = d[f"{prefix}_sampled"].astype(np.float64) * scale
+    got = np.asarray(got_flat, np.float64)
+    off = 0
+    for k, (name, shape) in enumerate(shapes):
+        n = int(np.prod(shape))
+        sel = (idx >= off) & (idx < off + n)
+        tmax = d[f"{prefix}_tmax"][k] * scale
+        err = np.abs(got[idx[sel]] - ref[sel]).max()
+        assert err <= tol * max(tmax, 1e-6), (prefix, name, err, tmax)
+        l2 = np.sqrt((got[off:off + n] ** 2).sum())
+        np.testing.assert_allclose(l2, d[f"{prefix}_tl2"][k] * scale, rtol=1e-5, err_msg=f"{prefix} {name}")
+        off += n
+    assert off == got.size
+
+
+def test_oracle_cnn_update_pinned_at_h512():
+    """cnn_update_h512.npz: the reference's whole T/run.py iteration at c3's hidden
+    size (CNNBase H = 512; 4 envs x 4 steps, E = 2, M = 2) replayed by the oracle —
+    actions bit-exact, returns 1e-5, losses 1e-5 relative, first-minibatch clipped
+    gradient (sampled) within 1e-5 of each tensor's max |g|, per-tensor L2 1e-5,
+    final parameters within 2e-5."""
+    d = golden("cnn_update_h512.npz")
+    hidden, N, T, E, Mb = (int(x) for x in d["meta"])
+    assert hidden == 512
+    shapes = O.cnn_param_shapes(hidden)
+    assert [str(n) for n in d["names"]] == [n for n, _ in shapes]
+    r = O.run_iteration(d["init_params"], shapes, d["obs_u8"], d["exp_noise"], d["rewards"][..., 0],
+                        d["masks"][..., 0], d["perms"], num_mini_batch=Mb, lr=float(d["lr"][0]))
+    assert np.array_equal(r["actions"], d["actions"][..., 0])
+    np.testing.assert_allclose(r["returns"][:T], d["returns"][:T, :, 0], atol=1e-5)
+    np.testing.assert_allclose(r["losses"], d["losses"], rtol=1e-5, atol=1e-7)
+    clipf = min(1.0, 0.5 / (float(d["total_norms"][0]) + 1e-6))
+    _digest_check(r["first"]["clipped_grad"], d, "mb0_preclip_grad", shapes, 1e-5, scale=clipf)
+    _digest_check(r["final_params"], d, "final_params", shapes, 2e-5)
+
+
+def test_oracle_recurrent_update_pinned_at_h256():
+    """gru_update_h256.npz: the reference's recurrent PPO.update at c5's hidden size
+    (GRU H = 256, V = 14; 8 envs x 16 steps, masks with zeros, E = 2, M = 2) —
+    oracle.run_update_recurrent's first-minibatch BPTT gradient (sampled) within
+    1e-5 of each tensor's max |g|, per-minibatch losses and total norms 1e-5
+    relative, final parameters within 2e-5."""
+    d = golden("gru_update_h256.npz")
+    hidden, V, N, T, E, Mb = (int(x) for x in d["meta"])
+    assert hidden == 256
+    clip, vcoef, ecoef = (float(x) for x in d["coefs"])
+    shapes = O.cnn_param_shapes(hidden, recurrent=True, vector_obs_len=V)
+    assert [str(n) for n in d["names"]] == [n for n, _ in shapes]
+    masks = np.concatenate([d["masks0"][None], d["masks"]], 0)[..., 0]
+    r = O.run_update_recurrent(d["init_params"], shapes, d["obs_u8"], d["vector_obs"], d["h0"], masks,
+                               d["actions"][..., 0], d["action_log_probs"][..., 0], d["value_preds_after"][..., 0],
+                               d["returns"][..., 0], d["perms"], num_mini_batch=Mb, clip=clip, value_coef=vcoef,
+                               entropy_coef=ecoef, lr=float(d["lr"][0]))
+    _digest_check(r["preclip_grads"][0], d, "mb0_preclip_grad", shapes, 1e-5)
+    np.testing.assert_allclose(r["mb_losses"], d["mb_losses"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(r["total_norms"], d["total_norms"], rtol=1e-5)
+    np.testing.assert_allclose(r["losses"], d["losses"], rtol=1e-5, atol=1e-7)
+    _digest_check(r["final_params"], d, "final_params", shapes, 2e-5)

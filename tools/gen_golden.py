@@ -15,8 +15,8 @@ A stub `<pkg>.envs` module stands in for the gym/baselines-backed envs.py,
 which only provides the VecNormalize type to utils.py.
 
 Run:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py [name ...]
-      (names: gae advnorm sampler categorical cnn_update adam mlp gru gru_update;
-       none = all)
+      (names: gae advnorm sampler categorical cnn_update cnn_update_h512
+       cnn_update_wide adam mlp gru gru_update gru_update_h256; none = all)
 """
 import importlib
 import importlib.util
@@ -79,6 +79,31 @@ def flat_params(module):
 
 def param_names(module):
     return np.array([n for n, _ in module.named_parameters()])
+
+
+def digest(prefix, flat, module, stride):
+    """A production-size tensor in a small fixture: every stride-th element (global
+    index), and per parameter tensor its max |x| and L2 norm (float64)."""
+    idx = np.arange(0, flat.size, stride, dtype=np.int64)
+    tmax, tl2, off = [], [], 0
+    for p in module.parameters():
+        seg = flat[off:off + p.numel()].astype(np.float64)
+        tmax.append(np.abs(seg).max())
+        tl2.append(np.sqrt((seg * seg).sum()))
+        off += p.numel()
+    return {f"{prefix}_idx": idx, f"{prefix}_sampled": flat[idx], f"{prefix}_tmax": np.array(tmax),
+            f"{prefix}_tl2": np.array(tl2)}
+
+
+def sample_margin(pol, obs, vec, hxs, masks, En):
+    """min over rows of the relative gap between the two largest probs / E (the
+    multinomial draw's argmax): a replay whose probabilities differ by
+    fp32 rounding picks the same actions when this is well above 1e-6"""
+    with torch.no_grad():
+        _, feats, _ = pol.base(obs, vec, hxs, masks)
+        q = (pol.dist(feats).probs / En).double()
+    top = torch.topk(q, 2, dim=1).values
+    return float(((top[:, 0] - top[:, 1]) / top[:, 0]).min())
 
 
 def save(name, **arrays):
@@ -215,19 +240,40 @@ def gen_categorical(D):
 # (5) one full CNN iteration, run.py:134-248 ordering:
 #     act → env → insert ×T, get_value, compute_returns, update, after_update
 # ---------------------------------------------------------------------------
-def gen_cnn_update(S, M, P, *, hidden, N, T, E, Mb, lr, fname):
+def gen_cnn_update(S, M, P, *, hidden, N, T, E, Mb, lr, fname, lowres=False, stride=0, obs_seed=None):
+    """lowres: 21x21 random bytes upsampled x4 (a compressible fixture); stride > 0:
+    final parameters and gradients as digests (every stride-th element + per-tensor
+    max |x| and L2, `digest`); obs_seed: observations not stored but drawn up front as
+    torch.randint(0, 256, (T+1, N, 4, 84, 84), generator=Generator().manual_seed(obs_seed))
+    — the CPU generator is deterministic, so the replay regenerates them (checked by
+    the stored byte sum and CRC-32)"""
     torch.manual_seed(1)
     pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase,
                    base_kwargs={"recurrent": False, "hidden_size": hidden}, vector_obs_len=0)
     agent = P.PPO(pol, 0.1, E, Mb, 0.5, 0.001, lr=lr, eps=1e-5, max_grad_norm=0.5)
     st = S.RolloutStorage(T, N, (4, 84, 84), [0], Discrete(8), pol.recurrent_hidden_state_size)
     init = flat_params(pol)
+    rng_init = torch.get_rng_state().numpy().copy()
     genv = torch.Generator().manual_seed(123)
+    all_obs = None
+    if obs_seed is not None:
+        all_obs = torch.randint(0, 256, (T + 1, N, 4, 84, 84), dtype=torch.uint8,
+                                generator=torch.Generator().manual_seed(obs_seed))
+
+    def frame(k):
+        if all_obs is not None:
+            return all_obs[k]
+        if lowres:
+            lo = torch.randint(0, 256, (N, 4, 21, 21), dtype=torch.uint8, generator=genv)
+            return lo.repeat_interleave(4, 2).repeat_interleave(4, 3).contiguous()
+        return torch.randint(0, 256, (N, 4, 84, 84), dtype=torch.uint8, generator=genv)
+
     obs_u8 = np.zeros((T + 1, N, 4, 84, 84), np.uint8)
-    o0 = torch.randint(0, 256, (N, 4, 84, 84), dtype=torch.uint8, generator=genv)
+    o0 = frame(0)
     obs_u8[0] = o0.numpy()
     st.obs[0].copy_(o0.float() / 255.0)
     noise, values, actions, logps, rewards, masks = [], [], [], [], [], []
+    margin = 1.0
     for step in range(T):
         with torch.no_grad():
             rs = torch.get_rng_state()
@@ -237,7 +283,10 @@ def gen_cnn_update(S, M, P, *, hidden, N, T, E, Mb, lr, fname):
             torch.set_rng_state(rs)
             En = torch.empty(N, 8).exponential_(1)
             assert torch.equal(torch.get_rng_state(), after)
-        o = torch.randint(0, 256, (N, 4, 84, 84), dtype=torch.uint8, generator=genv)
+            torch.set_rng_state(after)
+        margin = min(margin, sample_margin(pol, st.obs[step], st.vector_obs[step], st.recurrent_hidden_states[step],
+                                           st.masks[step], En))
+        o = frame(step + 1)
         rew = torch.rand(N, 1, generator=genv)
         done = torch.rand(N, generator=genv) < 0.3
         mk = torch.FloatTensor([[0.0] if d else [1.0] for d in done])
@@ -246,6 +295,7 @@ def gen_cnn_update(S, M, P, *, hidden, N, T, E, Mb, lr, fname):
         st.insert(o.float() / 255.0, torch.zeros(N, 0), hxs, action, logp, value, rew, mk, bmk)
         noise.append(En.numpy()); values.append(value.numpy()); actions.append(action.numpy())
         logps.append(logp.numpy()); rewards.append(rew.numpy()); masks.append(mk.numpy())
+    print(f"{fname}: min relative sampling margin {margin:.3e}")
     with torch.no_grad():
         next_value = pol.get_value(st.obs[-1], st.vector_obs[-1], st.recurrent_hidden_states[-1],
                                    st.masks[-1]).detach()
@@ -275,7 +325,21 @@ def gen_cnn_update(S, M, P, *, hidden, N, T, E, Mb, lr, fname):
         return orig_step(*a, **k)
 
     agent.optimizer.step = step_wrap
-    vl, al, ent = agent.update(st)
+    preclip, norms = [], []
+    orig_clip = torch.nn.utils.clip_grad_norm_
+
+    def clip_wrap(params, max_norm, *a, **k):   # clip_grad_norm_'s input and total norm
+        params = list(params)
+        preclip.append(np.concatenate([q.grad.reshape(-1).numpy().copy() for q in params]))
+        tn = orig_clip(params, max_norm, *a, **k)
+        norms.append(float(tn))
+        return tn
+
+    torch.nn.utils.clip_grad_norm_ = clip_wrap
+    try:
+        vl, al, ent = agent.update(st)
+    finally:
+        torch.nn.utils.clip_grad_norm_ = orig_clip
     pol.evaluate_actions = orig_eval
     rng_after_update = torch.get_rng_state()
     torch.set_rng_state(rng_before_update)
@@ -283,16 +347,33 @@ def gen_cnn_update(S, M, P, *, hidden, N, T, E, Mb, lr, fname):
     assert torch.equal(torch.get_rng_state(), rng_after_update)
     final = flat_params(pol)
     st.after_update()
-    save(fname, init_params=init, final_params=final, names=param_names(pol),
-         obs_u8=obs_u8, exp_noise=np.stack(noise), values=np.stack(values),
-         actions=np.stack(actions).astype(np.int64), action_log_probs=np.stack(logps),
-         rewards=np.stack(rewards), masks=np.stack(masks), next_value=next_value.numpy(),
-         returns=returns, value_preds_after=vpreds, perms=perms,
-         mb0_values=mb_records[0]["values"], mb0_logp=mb_records[0]["logp"],
-         mb_entropy=np.array([r["entropy"] for r in mb_records]),
-         mb0_clipped_grad=grads[0], last_clipped_grad=grads[-1],
-         losses=np.array([vl, al, ent]),
-         meta=np.array([hidden, N, T, E, Mb]), lr=np.array([lr]))
+    if not stride:
+        save(fname, init_params=init, final_params=final, names=param_names(pol),
+             obs_u8=obs_u8, exp_noise=np.stack(noise), values=np.stack(values),
+             actions=np.stack(actions).astype(np.int64), action_log_probs=np.stack(logps),
+             rewards=np.stack(rewards), masks=np.stack(masks), next_value=next_value.numpy(),
+             returns=returns, value_preds_after=vpreds, perms=perms,
+             mb0_values=mb_records[0]["values"], mb0_logp=mb_records[0]["logp"],
+             mb_entropy=np.array([r["entropy"] for r in mb_records]),
+             mb0_clipped_grad=grads[0], last_clipped_grad=grads[-1],
+             losses=np.array([vl, al, ent]),
+             meta=np.array([hidden, N, T, E, Mb]), lr=np.array([lr]))
+        return
+    extra = {}
+    if obs_seed is None:
+        extra["obs_u8"] = obs_u8
+    else:
+        import zlib
+        extra["obs_seed"] = np.array([obs_seed])
+        extra["obs_check"] = np.array([int(obs_u8.sum(dtype=np.int64)), zlib.crc32(obs_u8.tobytes())], np.int64)
+    save(fname, init_params=init, rng_after_init=rng_init, names=param_names(pol),
+         actions=np.stack(actions).astype(np.int64), action_log_probs=np.stack(logps), values=np.stack(values),
+         rewards=np.stack(rewards), masks=np.stack(masks), returns=returns, perms=perms,
+         mb_entropy=np.array([r["entropy"] for r in mb_records]), losses=np.array([vl, al, ent]),
+         sampling_margin=np.array([margin]), total_norms=np.array(norms), exp_noise=np.stack(noise),
+         value_preds_after=vpreds, next_value=next_value.numpy(),
+         meta=np.array([hidden, N, T, E, Mb]), lr=np.array([lr]), **extra,
+         **digest("final_params", final, pol, stride), **digest("mb0_preclip_grad", preclip[0], pol, stride))
 
 
 # ---------------------------------------------------------------------------
@@ -328,7 +409,7 @@ def gen_gru(S, M, P):
 #      reference's own PPO.update over recurrent_generator (storage.py:162-223,
 #      model.py:111-166, algo/ppo.py:43-96): BPTT -> clip_grad_norm_ -> Adam
 # ---------------------------------------------------------------------------
-def gen_gru_update(S, M, P, *, hidden=32, V=14, N=8, T=16, E=2, Mb=2, lr=1e-3, fname="gru_update.npz"):
+def gen_gru_update(S, M, P, *, hidden=32, V=14, N=8, T=16, E=2, Mb=2, lr=1e-3, fname="gru_update.npz", stride=0):
     torch.manual_seed(31)
     pol = M.Policy((4, 84, 84), Discrete(8), base=M.CNNBase,
                    base_kwargs={"recurrent": True, "hidden_size": hidden}, vector_obs_len=V)
@@ -434,16 +515,19 @@ def gen_gru_update(S, M, P, *, hidden=32, V=14, N=8, T=16, E=2, Mb=2, lr=1e-3, f
     for g, c, tn in zip(preclip, clipped, norms):   # step() saw clip_grad_norm_'s scaling of its input
         np.testing.assert_allclose(c, g * min(0.5 / (tn + 1e-6), 1.0), rtol=1e-6, atol=1e-12)
     final = flat_params(pol)
-    save(fname, init_params=init, rng_after_init=rng_init, final_params=final, names=param_names(pol),
-         obs_u8=obs_u8, vector_obs=vec, h0=h0.numpy(), masks0=m0.numpy(), hidden_T=hid_T,
-         exp_noise=np.stack(noise), values=np.stack(values),
-         actions=np.stack(actions).astype(np.int64), action_log_probs=np.stack(logps),
-         rewards=np.stack(rewards), masks=np.stack(masks), next_value=next_value.numpy(),
-         returns=returns, value_preds_after=vpreds, perms=perms,
-         mb_losses=np.array(items, np.float64).reshape(E * Mb, 3),
-         mb0_preclip_grad=preclip[0], last_preclip_grad=preclip[-1], total_norms=np.array(norms),
-         losses=np.array([vl, al, ent]),
-         meta=np.array([hidden, V, N, T, E, Mb]), coefs=np.array([0.1, 0.5, 0.01]), lr=np.array([lr]))
+    common = dict(init_params=init, rng_after_init=rng_init, names=param_names(pol),
+                  obs_u8=obs_u8, vector_obs=vec, h0=h0.numpy(), masks0=m0.numpy(), hidden_T=hid_T,
+                  values=np.stack(values), actions=np.stack(actions).astype(np.int64),
+                  action_log_probs=np.stack(logps), rewards=np.stack(rewards), masks=np.stack(masks),
+                  returns=returns, perms=perms, mb_losses=np.array(items, np.float64).reshape(E * Mb, 3),
+                  total_norms=np.array(norms), losses=np.array([vl, al, ent]), exp_noise=np.stack(noise),
+                  next_value=next_value.numpy(), value_preds_after=vpreds,
+                  meta=np.array([hidden, V, N, T, E, Mb]), coefs=np.array([0.1, 0.5, 0.01]), lr=np.array([lr]))
+    if stride:
+        save(fname, **common, **digest("final_params", final, pol, stride),
+             **digest("mb0_preclip_grad", preclip[0], pol, stride))
+        return
+    save(fname, **common, final_params=final, mb0_preclip_grad=preclip[0], last_preclip_grad=preclip[-1])
 
 
 # ---------------------------------------------------------------------------
@@ -506,6 +590,13 @@ def main():
         gen_categorical(D)
     if on("cnn_update"):
         gen_cnn_update(S, M, P, hidden=64, N=4, T=4, E=2, Mb=2, lr=1e-3, fname="cnn_update.npz")
+    if on("cnn_update_h512"):   # the production hidden size (c3), VERDICT r05 item 6
+        gen_cnn_update(S, M, P, hidden=512, N=4, T=4, E=2, Mb=2, lr=1e-3, fname="cnn_update_h512.npz",
+                       lowres=True, stride=8)
+    if on("cnn_update_wide"):   # c3's hidden size at a minibatch wide enough for the production fc tiles
+        seed = int(os.environ.get("GOLDEN_WIDE_SEED", "2027"))   # chosen for its sampling margin (2.9e-4)
+        gen_cnn_update(S, M, P, hidden=512, N=128, T=128, E=1, Mb=1, lr=1e-4,
+                       fname=os.environ.get("GOLDEN_WIDE_NAME", "cnn_update_wide.npz"), stride=8, obs_seed=seed)
     if on("adam"):
         gen_adam()
     if on("mlp"):
@@ -515,6 +606,9 @@ def main():
         gen_gru(S, M, P)
     if on("gru_update"):
         gen_gru_update(S, M, P)
+    if on("gru_update_h256"):   # c5's hidden size: the persistent split-bf16 GRU kernels, VERDICT r05 item 6
+        gen_gru_update(S, M, P, hidden=256, V=14, N=8, T=16, E=2, Mb=2, lr=1e-3, fname="gru_update_h256.npz",
+                       stride=8)
 
 
 if __name__ == "__main__":

@@ -30,25 +30,33 @@ def mfma_util(path):
     """per kernel name: average MFMA pipeline utilisation over its launches"""
     if not os.path.exists(path):
         return None
-    per = {}
+    per, dur = {}, {}
     for r in csv.DictReader(open(path)):
         key = (r["Kernel_Name"], r.get("Dispatch_Id") or r.get("Correlation_Id"))
         per.setdefault(key, {})[r["Counter_Name"]] = float(r["Counter_Value"])
+        if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+            dur[key] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
     agg = {}
-    for (name, _), c in per.items():
+    for key, c in per.items():
         if "GRBM_GUI_ACTIVE" not in c or "SQ_VALU_MFMA_BUSY_CYCLES" not in c or c["GRBM_GUI_ACTIVE"] <= 0:
             continue
-        short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:80]
-        a = agg.setdefault(short, [0, 0.0, 0.0, 0.0])
+        short = key[0].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:80]
+        a = agg.setdefault(short, [0, 0.0, 0.0, 0.0, 0.0])
         a[0] += 1
         a[1] += c["SQ_VALU_MFMA_BUSY_CYCLES"]
         a[2] += c["GRBM_GUI_ACTIVE"]
         a[3] += c.get("SQ_INSTS_MFMA", 0.0)
+        a[4] += dur.get(key, 0.0)
     out = {}
-    for k, (n, busy, gui, insts) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
+    for k, (n, busy, gui, insts, ns) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
         if insts <= 0:
             continue
         out[k] = {"launches": n, "mfma_util": round(busy / (1024 * gui / 8), 4), "mfma_insts_per_launch": insts / n}
+        if ns > 0:
+            # the shader clock the kernel ran at: GRBM_GUI_ACTIVE counts GPU-busy
+            # cycles summed over the 8 XCDs, over the same dispatches' durations
+            out[k]["sclk_ghz"] = round(gui / 8 / ns, 4)
+            out[k]["pmc_avg_launch_ms"] = round(ns / n / 1e6, 4)
     return out
 
 
@@ -94,7 +102,9 @@ def main():
     if mfma:
         json.dump({"tag": tag, "workload": json.loads(line)["config"]["workload"],
                    "definition": "util = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x GRBM_GUI_ACTIVE / XCDs); "
-                                 "SIMDs = 1024, XCDs = 8 (GRBM_GUI_ACTIVE sums the 8 XCDs)",
+                                 "SIMDs = 1024, XCDs = 8 (GRBM_GUI_ACTIVE sums the 8 XCDs); "
+                                 "sclk_ghz = GRBM_GUI_ACTIVE / XCDs / the same dispatches' duration "
+                                 "(End - Start timestamps of the counter pass)",
                    "kernels": mfma}, open(os.path.join(prof, f"{tag}_mfma.json"), "w"), indent=1)
         out["mfma_util_file"] = f"profiles/{tag}_mfma.json"
     out["tag"] = tag
