@@ -388,9 +388,9 @@ def pmc_mfma(workload):
         d = json.load(open(os.path.join(ROOT, "profiles", "roofline_traffic.json")))
         m = json.load(open(os.path.join(ROOT, d["mfma_util_file"])))
     except (OSError, ValueError, KeyError):
-        return {}, None
+        return {}, {}, None
     if m.get("workload") != workload:
-        return {}, None
+        return {}, {}, None
     out, clk = {}, {}
     for name, sym in PMC_SYMBOL.items():
         # all instantiations (e.g. the rollout and the mask-writing training

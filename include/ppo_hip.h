@@ -39,7 +39,8 @@ extern "C" {
 
 const char* ppo_last_error(void);
 /* 3 (round 6): symbols removed in round 5 (ppo_a1split_*, ppo_conv*_split, the anatomy
- * probes) and the GRU counter buffer grown to (3 + 32)·G ints (ppo_gru_seq_counters) */
+ * probes); round 6: ppo_gru_l2_set / _get removed (the BPTT hands dgh over by sc1 stores
+ * only) and the GRU counter buffer is 2·G ints (ppo_gru_seq_counters) */
 int ppo_abi_version(void);
 /* launch-level event profiler used by bench.py: time every launch of the named
  * kernel (NULL disables); collect -> {launches, Σ ms, Σ algorithmic FLOP} */
@@ -312,15 +313,9 @@ int ppo_gru_persist_spin_set(int polls);
  * stream-ordered read of the word) and clears it */
 int ppo_gru_persist_timeouts(void* stream);
 /* counters a persistent launch over n rows needs (ints; G = ceil(n/32) groups):
- * [G step counters][G BPTT start counters][32·G XCC_ID slots of the L2
- * agreement][G BPTT path reports: 1 sc1 hand-off, 2 L2 hand-off, 0 not run] */
+ * [G step counters][G BPTT reports: 1 the group ran the persistent BPTT (dgh handed
+ * over by sc1 stores and loads), 0 not run] */
 int ppo_gru_seq_counters(int n);
-/* the persistent BPTT's dgh hand-off (gru_seq_bwd16_kernel): 1 (default) a row
- * group whose unit blocks all report one XCC_ID stores dgh plain (kept in that
- * XCD's L2), else sc1 (write-through); 0 sc1 for every group.  The loads are sc1
- * (L1 bypassed) on both paths. */
-int ppo_gru_l2_set(int v);
-int ppo_gru_l2_get(void);
 /* ppo_gru_seq_fwd with caller-owned synchronisation words: counters
  * (ppo_gru_seq_counters(n) ints, reset by the call on `stream`) and err (one int,
  * see above); both may be NULL when the step launches run (persist 0) */

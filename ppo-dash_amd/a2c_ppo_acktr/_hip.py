@@ -93,8 +93,6 @@ SIGNATURES = {
     "ppo_gru_variant_get": [],
     "ppo_gru_persist_set": [c_int],
     "ppo_gru_persist_get": [],
-    "ppo_gru_l2_set": [c_int],
-    "ppo_gru_l2_get": [],
     "ppo_gru_persist_timeouts": [c_p],
     "ppo_gru_persist_spin_set": [c_int],
     "ppo_gru_seq_counters": [c_int],
@@ -125,7 +123,7 @@ _RESTYPES = {"ppo_last_error": ctypes.c_char_p, "ppo_packed_weights_size": c_ll,
 _VALUE_FUNCS = {"ppo_abi_version", "ppo_gae_partials_count", "ppo_gae_scan_partials_count", "ppo_adv_diff_partials_count",
                 "ppo_packed_weights_size", "ppo_fc_fwd_ws_bytes", "ppo_wgrad_splits", "ppo_heads_train_blocks", "ppo_grad_partials_count",
                 "ppo_conv2_dgrad_bits_ok", "ppo_conv3_dgrad_bits_ok", "ppo_tune_get",
-                "ppo_gru_persist_get", "ppo_gru_l2_get", "ppo_gru_persist_timeouts", "ppo_gru_seq_counters"}
+                "ppo_gru_persist_get", "ppo_gru_persist_timeouts", "ppo_gru_seq_counters"}
 
 _LIB = None
 

@@ -560,7 +560,12 @@ __global__ __launch_bounds__(256) void relu_bits_kernel(const float* __restrict_
 // loads, 8 the epilogue stores (profiles/r04_c2f_anatomy_kbench.log)
 constexpr int C2F_STG = 3 * 4 * 400, C2F_MT = 6;   // conv2 forward: bf16x8 units per stage, row tiles
 constexpr int C2F_LDS = 2 * C2F_STG * 16 + 2 * C2F_MT * 16 * 4;   // stages + vtab + otab (154,368 B)
-template <int NP, bool MASK = false, int DBG = 0, int MT = C2F_MT>
+template <int NP, bool MASK>
+__device__ __forceinline__ void conv2_lone_tiles(const float* __restrict__ a1, const bf16x8 (&bw)[8][3],
+                                                 const float* __restrict__ bias, float* __restrict__ out,
+                                                 uint16_t* __restrict__ mbits, uint8_t* __restrict__ lds,
+                                                 long long base, long long stride, int nimg, int t0, int tstep);
+template <int NP, bool MASK = false, int DBG = 0, int MT = C2F_MT, bool LONE = false>
 __device__ __forceinline__ void conv2_fwd_x9c_body(const float* __restrict__ a1, int B,
                                                    const uint16_t* __restrict__ wpl, const float* __restrict__ bias,
                                                    float* __restrict__ out, uint16_t* __restrict__ mbits,
@@ -747,10 +752,27 @@ __device__ __forceinline__ void conv2_fwd_x9c_body(const float* __restrict__ a1,
     }
     cur ^= 1;
   }
+  if constexpr (MT == 5 && LONE) {
+    // the lone pixel (output 72) of this block's own images, 16 per tile, after its
+    // image loop (round 6, VERDICT r05 item 7: no separate launch; the weight
+    // fragments are the ones the image loop used)
+    __syncthreads();   // the last image's K-half partials (in the LDS) are read
+    const int blk = blockIdx.x;
+    const int nimg = blk < B ? (B - 1 - blk) / G + 1 : 0;
+    conv2_lone_tiles<NP, MASK>(a1, bw, bias, out, mbits, lds, blk, G, nimg, 0, 1);
+  }
 }
 
 #ifndef C2F_LONE
-#define C2F_LONE 1   // standalone conv2 forward: five row tiles + conv2_fwd_lone_kernel
+// standalone conv2 forward: 1 five row tiles + conv2_fwd_lone_kernel (default), 2 the
+// lone pixel inside the same launch after each block's image loop, 0 six tiles.
+// Round 6 measured 2 against 1 on one box, alternating
+// (profiles/r06_d_lone_trunk_kbab.log): 1.804-1.817 vs 1.787-1.789 ms (conv2_fwd),
+// 1.746-1.754 vs 1.740-1.744 ms (the masked training form) — the separate launch
+// runs two 70-KB-LDS blocks per CU (16 waves) where the folded tiles run at the
+// tail of one 8-wave block per CU, so it stays.  The fused trunk folds them (one
+// tile per block at the rollout's 16 images per block, no extra launch).
+#define C2F_LONE 1
 #endif
 template <int NP, bool MASK = false, int DBG = 0>
 __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restrict__ a1, int B,
@@ -759,12 +781,11 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
                                                            float* __restrict__ out,
                                                            uint16_t* __restrict__ mbits) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[C2F_LDS];
-  conv2_fwd_x9c_body<NP, MASK, DBG, C2F_LONE ? 5 : 6>(a1, B, wpl, bias, out, mbits, lds);
+  conv2_fwd_x9c_body<NP, MASK, DBG, C2F_LONE ? 5 : 6, C2F_LONE == 2>(a1, B, wpl, bias, out, mbits, lds);
 }
 
 // conv2 forward of output pixel 72 = (8, 0) (phase-grid v = 80, the sixth row tile's
-// only real row) for 16 images per tile: row i16 of the B operand is image 16 T +
-// i16.  The tile's 16 patches (a1 rows 16-19, columns 0-3: 4 x 512 contiguous bytes
+// only real row) for 16 images per tile.  The tile's 16 patches (a1 rows 16-19, columns 0-3: 4 x 512 contiguous bytes
 // per image, 32 KB per tile) are loaded once per block — each thread four 16-B
 // pieces, the next tile's in registers during this tile's MFMAs — and staged in LDS
 // (two stages; image rows padded by 16 B so the 16 images of a fragment read hit
@@ -775,38 +796,37 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
 // MFMA sequence per wave (k-steps of its K half in order, parts in PPO_PRODUCTS
 // order), the K halves summed kh 0 + kh 1, the same epilogue: an MFMA output column
 // depends only on its own B column, so the result is bit-identical to a six-tile
-// launch (test_trunk_fwd_equals_three_launches compares against the fused trunk,
-// which keeps six tiles).  Grid-stride over tiles.
+// launch whichever images share a tile (test_trunk_fwd_equals_three_launches; the
+// six-tile form is C2F_LONE = 0).
+// Tiles t0, t0 + tstep, ... of the images base + stride * i (i < nimg, 16 per tile:
+// row i16 of the B operand is image base + stride * (16 t + i16)).  The kernel above
+// runs it after its image loop over the block's own images (base = blockIdx.x, stride
+// = the grid), conv2_fwd_lone_kernel (C2F_LONE = 1) over contiguous images.
+constexpr int C2L_IR = 129;   // f32x4 per staged image row (128 + pad)
+constexpr int C2L_LDS = 2 * 16 * C2L_IR * 16 + 4 * 64 * 16;   // two patch stages + K-half partials (70,144 B)
+static_assert(C2L_LDS <= C2F_LDS, "the lone tiles reuse the image loop's LDS");
 template <int NP, bool MASK>
-__global__ __launch_bounds__(512) void conv2_fwd_lone_kernel(const float* __restrict__ a1, int B,
-                                                             const uint16_t* __restrict__ wpl,
-                                                             const float* __restrict__ bias,
-                                                             float* __restrict__ out,
-                                                             uint16_t* __restrict__ mbits) {
-  constexpr int KS = 8, WN = 64 * 512, M = 72, IR = 129;   // IR: f32x4 per staged image row (128 + pad)
-  __shared__ f32x4 P[2][16 * IR];
-  __shared__ f32x4 R[4 * 64];
+__device__ __forceinline__ void conv2_lone_tiles(const float* __restrict__ a1, const bf16x8 (&bw)[8][3],
+                                                 const float* __restrict__ bias, float* __restrict__ out,
+                                                 uint16_t* __restrict__ mbits, uint8_t* __restrict__ lds,
+                                                 long long base, long long stride, int nimg, int t0, int tstep) {
+  constexpr int KS = 8, M = 72, IR = C2L_IR;
+  f32x4 (*const P)[16 * IR] = reinterpret_cast<f32x4 (*)[16 * IR]>(lds);
+  f32x4* const R = reinterpret_cast<f32x4*>(lds + 2 * 16 * IR * 16);
   const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nt = wave & 3, kh = wave >> 2, co = 16 * nt + i16;
-  bf16x8 bw[KS][3];
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
-  const int ntile = (B + 15) / 16;
+  const int nt = wave & 3, kh = wave >> 2;
+  const int ntile = (nimg + 15) / 16;
   // piece q = tid + 512 j (j < 4) of a tile: image q >> 7, f32x4 f = q & 127 of its
   // patch = tap (4 ky + kx) * 8 + channel quad; a1 offset (16 + ky) * 640 + (f & 31) * 4
   f32x4 pc[4];
-  auto fetch = [&](int T) {   // T >= ntile: a resource of 0 bytes (the loads read 0)
-    const int nimg = T < ntile ? (B - 16 * T < 16 ? B - 16 * T : 16) : 0;
-    const auto ra = make_rsrc(a1 + (size_t)(T < ntile ? 16 * T : 0) * 12800, nimg * 12800 * 4);
+  auto fetch = [&](int T) {   // past the last tile / image: zeros, nothing loaded
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int q = tid + 512 * j, im = q >> 7, f = q & 127;
-      const int off = (im * 12800 + (16 + (f >> 5)) * 640 + (f & 31) * 4) * 4;
-      pc[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+      const int q = tid + 512 * j, im = q >> 7, f = q & 127, i = 16 * T + im;
+      const bool live = T < ntile && i < nimg;
+      const float* src = a1 + (size_t)(base + stride * (live ? i : 0)) * 12800 + (16 + (f >> 5)) * 640 + (f & 31) * 4;
+      pc[j] = live ? *reinterpret_cast<const f32x4*>(src) : zero4();
     }
   };
   auto put = [&](int st) {
@@ -816,14 +836,15 @@ __global__ __launch_bounds__(512) void conv2_fwd_lone_kernel(const float* __rest
       P[st][(q >> 7) * IR + (q & 127)] = pc[j];
     }
   };
-  fetch(blockIdx.x);
+  fetch(t0);
   put(0);
   __syncthreads();
   int cur = 0;
-  for (int T = blockIdx.x; T < ntile; T += gridDim.x) {
-    fetch(T + gridDim.x);
-    const int b = 16 * T + i16;
-    const bool live = b < B;
+  for (int T = t0; T < ntile; T += tstep) {
+    fetch(T + tstep);
+    const int i = 16 * T + i16;
+    const bool live = i < nimg;
+    const long long b = base + stride * (long long)i;
     f32x4 acc = zero4();
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -857,6 +878,25 @@ __global__ __launch_bounds__(512) void conv2_fwd_lone_kernel(const float* __rest
     __syncthreads();   // R read before the next tile's partials
     cur ^= 1;
   }
+}
+
+template <int NP, bool MASK>
+__global__ __launch_bounds__(512) void conv2_fwd_lone_kernel(const float* __restrict__ a1, int B,
+                                                             const uint16_t* __restrict__ wpl,
+                                                             const float* __restrict__ bias,
+                                                             float* __restrict__ out,
+                                                             uint16_t* __restrict__ mbits) {
+  constexpr int KS = 8, WN = 64 * 512;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[C2L_LDS];
+  const int tid = threadIdx.x, i16 = tid & 15, g = (tid & 63) >> 4, wave = tid >> 6;
+  const int co = 16 * (wave & 3) + i16, kh = wave >> 2;
+  bf16x8 bw[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 512 + (8 * kh + s) * 32 + 8 * g);
+  conv2_lone_tiles<NP, MASK>(a1, bw, bias, out, mbits, lds, 0, 1, B, blockIdx.x, gridDim.x);
 }
 
 // conv2 weight gradient, image-resident on the bf16 matrix cores (exact split,
@@ -1372,28 +1412,111 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
   conv3_fwd_x9_body<NP>(a2, B, wpl, bias, out, lds);
 }
 
-// conv3 forward with compact rows (round 5; the standalone launches): GEMM row m =
-// 7 oy + ox over the 49 real outputs (the 9-wide grid above issues 64 rows for
-// them), row tiles 0-2 (m < 48) on 12 waves — co tile w & 1, K half (w >> 1) & 1,
-// row tile w >> 2, one tile each — and output 48 = (6, 6) left to
-// conv3_fwd_lone_kernel.  A lane's tap pixel is p0(m) + 9 ky + kx, p0 = 9 oy + ox
-// (a per-lane base: the 16 rows of a tile are no longer 16 consecutive pixels, so
-// some ds_read_b128 groups meet 2-way bank conflicts).  The same operand splits,
-// k-steps, part order and K-half sum as conv3_fwd_x9_body, so every output is
-// bit-identical to it (the fused trunk keeps that body).  One block per CU (12
-// waves, 3 per SIMD).
+// conv3 forward with compact rows (round 5): GEMM row m = 7 oy + ox over the 49 real
+// outputs (the 9-wide grid above issues 64 rows for them), row tiles 0-2 (m < 48)
+// and output 48 = (6, 6) left to conv3_lone_tiles.  Wave w: co tile w & 1, K half
+// (w >> 1) & 1; with NT = 768 threads (the standalone launch, 3 waves per SIMD) row
+// tile w >> 2, with NT = 512 (the fused trunk's third phase) row tiles 0-1 for waves
+// 0-3 and tile 2 for waves 4-7 — waves w and w + 4 share a SIMD, so the SIMD's
+// matrix core runs 3 tiles per image instead of the 9-wide grid's 4.  A lane's tap
+// pixel is p0(m) + 9 ky + kx, p0 = 9 oy + ox (a per-lane base: the 16 rows of a tile
+// are no longer 16 consecutive pixels, so some ds_read_b128 groups meet 2-way bank
+// conflicts).  The same operand splits, k-steps, part order and K-half sum as
+// conv3_fwd_x9_body, so every output is bit-identical to it whatever the wave count.
+// LONE: the lone output of the block's own images after its image loop (round 6,
+// VERDICT r05 item 7); else conv3_fwd_lone_kernel covers it (C3F_COMPACT = 1).
 constexpr int C3C_LDS = 2 * 3 * C3F_PL * 2 + 2 * 2 * 3 * 64 * 16;   // stages + K-half partials (76,800 B)
-template <int NP>
-__global__ __launch_bounds__(768) void conv3_fwd_c3_kernel(const float* __restrict__ a2, int B,
-                                                           const uint16_t* __restrict__ wpl,
-                                                           const float* __restrict__ bias,
-                                                           float* __restrict__ out) {
-  constexpr int NPX = 84, PL = NPX * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, NT = 768;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[C3C_LDS];
+constexpr int C3L_IR = 145;   // f32x4 per staged lone patch (144 + pad)
+constexpr int C3L_LDS = 2 * 16 * C3L_IR * 16 + 2 * 64 * 16;   // two patch stages + K-half partials (76,288 B)
+static_assert(C3L_LDS <= C3C_LDS, "the lone tiles reuse the image loop's LDS");
+
+// conv3 forward of output 48 = (6, 6) for 16 images per tile: tiles t0, t0 + tstep, ...
+// of the images base + stride * i (i < nimg; row i16 of the B operand is image base +
+// stride * (16 t + i16)); the same operands, MFMA sequence, K-half sum and epilogue as
+// the compact kernel (bit-identical).  Waves 0-3 compute (co tile w & 1, K half w >> 1,
+// their weight fragments bw), every thread of the NT stages.  As conv2's lone tiles,
+// the tile's 16 patches (3 rows of 3 pixels x 64 channels, 768 contiguous bytes per
+// row) are loaded once per block, the next tile's in registers during this tile's
+// MFMAs, and staged in LDS (two stages, image rows padded by 16 B).
+template <int NP, int NT>
+__device__ __forceinline__ void conv3_lone_tiles(const float* __restrict__ a2, const bf16x8 (&bw)[9][3],
+                                                 const float* __restrict__ bias, float* __restrict__ out,
+                                                 uint8_t* __restrict__ lds, long long base, long long stride,
+                                                 int nimg, int t0, int tstep) {
+  constexpr int KS = 9, M = 48, IR = C3L_IR, NPIECE = 16 * 144, NPC = (NPIECE + NT - 1) / NT;
+  f32x4 (*const P)[16 * IR] = reinterpret_cast<f32x4 (*)[16 * IR]>(lds);
+  f32x4* const R = reinterpret_cast<f32x4*>(lds + 2 * 16 * IR * 16);
+  const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nt = wave & 1, kh = (wave >> 1) & 1;
+  const int ntile = (nimg + 15) / 16;
+  // piece q = tid + NT j: image q / 144, f32x4 f = q % 144 of its patch = ky * 48 +
+  // kx * 16 + channel quad; a2 offset ((6 + ky) * 9 + 6) * 64 + (f % 48) * 4
+  f32x4 pc[NPC];
+  auto fetch = [&](int T) {   // past the last tile / image: zeros, nothing loaded
+#pragma unroll
+    for (int j = 0; j < NPC; ++j) {
+      const int q = tid + NT * j, im = q / 144, f = q - 144 * im, ky = f / 48, i = 16 * T + im;
+      const bool live = q < NPIECE && T < ntile && i < nimg;
+      const float* src = a2 + (size_t)(base + stride * (live ? i : 0)) * 5184 + ((6 + ky) * 9 + 6) * 64 + (f - 48 * ky) * 4;
+      pc[j] = live ? *reinterpret_cast<const f32x4*>(src) : zero4();
+    }
+  };
+  auto put = [&](int st) {
+#pragma unroll
+    for (int j = 0; j < NPC; ++j) {
+      const int q = tid + NT * j, im = q / 144;
+      if (q < NPIECE) P[st][im * IR + (q - 144 * im)] = pc[j];
+    }
+  };
+  fetch(t0);
+  put(0);
+  __syncthreads();
+  int cur = 0;
+  for (int T = t0; T < ntile; T += tstep) {
+    fetch(T + tstep);
+    const int i = 16 * T + i16;
+    const long long b = base + stride * (long long)i;
+    f32x4 acc = zero4();
+    if (wave < 4) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int ks = 9 * kh + s, tap = ks >> 1, c = 4 * (ks & 1) + g;
+        const f32x4* x = &P[cur][i16 * IR + tap * 16 + 2 * c];
+        Frag3 a;
+        split8(x[0], x[1], a, false);
+        const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+#define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
+        PPO_PRODUCTS(NP, PPO_PART)
+#undef PPO_PART
+      }
+      if (kh == 1) R[nt * 64 + lane] = acc;
+    }
+    put(cur ^ 1);   // the stage read one tile ago (the last barrier retired its reads)
+    __syncthreads();   // partials in R; stage cur ^ 1 complete
+    if (wave < 2 && i < nimg) {   // kh == 0
+      const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
+      const f32x4 v = acc + R[nt * 64 + lane];
+      f32x4 y;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
+      *reinterpret_cast<f32x4*>(out + (size_t)b * (49 * 32) + M * 32 + 16 * nt + 4 * g) = y;
+    }
+    __syncthreads();   // R read before the next tile's partials
+    cur ^= 1;
+  }
+}
+
+template <int NP, int NT, bool LONE>
+__device__ __forceinline__ void conv3_fwd_c3_body(const float* __restrict__ a2, int B,
+                                                  const uint16_t* __restrict__ wpl, const float* __restrict__ bias,
+                                                  float* __restrict__ out, uint8_t* __restrict__ lds) {
+  static_assert(NT == 512 || NT == 768, "8 or 12 waves");
+  constexpr int NPX = 84, PL = NPX * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, UPER = (UNITS + NT - 1) / NT;
   uint16_t (*const S)[3 * PL] = reinterpret_cast<uint16_t (*)[3 * PL]>(lds);
   f32x4 (*const R)[2][3][64] = reinterpret_cast<f32x4 (*)[2][3][64]>(lds + 2 * 3 * PL * 2);   // [stage][co tile][row tile][lane]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
-  const int nt = wave & 1, kh = (wave >> 1) & 1, mt = wave >> 2, co = 16 * nt + i16;
+  const int nt = wave & 1, kh = (wave >> 1) & 1, co = 16 * nt + i16;
   bf16x8 bw[KS][3];
 #pragma unroll
   for (int s = 0; s < KS; ++s)
@@ -1401,25 +1524,30 @@ __global__ __launch_bounds__(768) void conv3_fwd_c3_kernel(const float* __restri
     for (int p = 0; p < 3; ++p)
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 576 + (9 * kh + s) * 32 + 8 * g);
   const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
-  const int m = 16 * mt + i16, oy = m / 7, p0 = 9 * oy + (m - 7 * oy);
   wait_vm0();
   for (int i = tid; i < 2 * 3 * PL / 8; i += NT) reinterpret_cast<uint4*>(&S[0][0])[i] = uint4{0, 0, 0, 0};
-  f32x4 stg[2];
-  const bool has = tid < UNITS;   // one 8-channel unit per thread (648 of 768)
-  auto fetch = [&](int b) {   // a per-image buffer resource: the idle threads read 0, no branch
+  f32x4 stg[UPER][2];
+  auto fetch = [&](int b) {   // a per-image buffer resource: units past the image read 0, no branch
     const auto ra = make_rsrc(a2 + (size_t)b * 5184, 5184 * 4);
-    const int off = has ? 32 * tid : 0x7fffffe0;
-    stg[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
-    stg[1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
+#pragma unroll
+    for (int j = 0; j < UPER; ++j) {
+      const int u = tid + NT * j, off = u < UNITS ? 32 * u : 0x7fffffe0;
+      stg[j][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
+      stg[j][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off + 16, 0, 0));
+    }
   };
   auto put = [&](int buf) {
-    if (has) {
-      const int p = tid >> 3, off = p * 64 + 8 * ((tid & 7) ^ ((p >> 1) & 7));
-      Frag3 f;
-      split8(stg[0], stg[1], f, false);
-      *reinterpret_cast<bf16x8*>(&S[buf][off]) = f.h;
-      *reinterpret_cast<bf16x8*>(&S[buf][PL + off]) = f.m;
-      *reinterpret_cast<bf16x8*>(&S[buf][2 * PL + off]) = f.l;
+#pragma unroll
+    for (int j = 0; j < UPER; ++j) {
+      const int u = tid + NT * j;
+      if (u < UNITS) {
+        const int p = u >> 3, off = p * 64 + 8 * ((u & 7) ^ ((p >> 1) & 7));
+        Frag3 f;
+        split8(stg[j][0], stg[j][1], f, false);
+        *reinterpret_cast<bf16x8*>(&S[buf][off]) = f.h;
+        *reinterpret_cast<bf16x8*>(&S[buf][PL + off]) = f.m;
+        *reinterpret_cast<bf16x8*>(&S[buf][2 * PL + off]) = f.l;
+      }
     }
   };
   __syncthreads();   // the zeroed pad rows
@@ -1431,121 +1559,107 @@ __global__ __launch_bounds__(768) void conv3_fwd_c3_kernel(const float* __restri
     fetch(b + G < B ? b + G : b);
   }
   __syncthreads();
+  // row tiles of this wave: mt0 .. mt0 + ntl - 1; the k loop takes the count as a
+  // compile-time constant (a run-time bound would issue the second tile's MFMAs on
+  // every wave), the barriers stay outside the wave-dependent branch
+  const int mt0 = NT == 768 ? (wave >> 2) : (wave < 4 ? 0 : 2);
+  const int ntl = NT == 768 || wave >= 4 ? 1 : 2;
+  int p0[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int m = 16 * (mt0 + t) + i16, oy = m / 7;
+    p0[t] = 9 * oy + (m - 7 * oy);
+  }
   for (; b < B; b += G) {
     put(cur ^ 1);   // unconditional (past the end: a copy of this image into the idle stage)
     const int bnn = b + 2 * G < B ? b + 2 * G : b;
     const uint16_t* Sc = S[cur];
-    f32x4 acc = zero4();
+    f32x4 acc[2] = {zero4(), zero4()};
+    auto kloop = [&](auto ntc) __attribute__((always_inline)) {
+      constexpr int NTL = decltype(ntc)::value;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int ks = 9 * kh + s, tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky, c = 4 * (ks & 1) + g;
-      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
-      const int p = p0 + 9 * ky + kx;
-      const uint16_t* q = Sc + p * 64 + 8 * (c ^ ((p >> 1) & 7));
-      Frag3 a;
-      a.h = *reinterpret_cast<const bf16x8*>(q);
-      a.m = *reinterpret_cast<const bf16x8*>(q + PL);
-      a.l = *reinterpret_cast<const bf16x8*>(q + 2 * PL);
-#define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
-      PPO_PRODUCTS(NP, PPO_PART)
+      for (int s = 0; s < KS; ++s) {
+        const int ks = 9 * kh + s, tap = ks >> 1, ky = tap / 3, kx = tap - 3 * ky, c = 4 * (ks & 1) + g;
+        const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
+        Frag3 a[NTL];
+#pragma unroll
+        for (int t = 0; t < NTL; ++t) {
+          const int p = p0[t] + 9 * ky + kx;
+          const uint16_t* q = Sc + p * 64 + 8 * (c ^ ((p >> 1) & 7));
+          a[t].h = *reinterpret_cast<const bf16x8*>(q);
+          a[t].m = *reinterpret_cast<const bf16x8*>(q + PL);
+          a[t].l = *reinterpret_cast<const bf16x8*>(q + 2 * PL);
+        }
+#define PPO_PART(X, Y) \
+  _Pragma("unroll") for (int t = 0; t < NTL; ++t) acc[t] = mma(w.Y, a[t].X, acc[t]);
+        PPO_PRODUCTS(NP, PPO_PART)
 #undef PPO_PART
-      if (s == 1) {
-        fetch(bnn);
-        __builtin_amdgcn_sched_barrier(0);   // the loads stay in their slot
+        if (s == 1) {
+          fetch(bnn);
+          __builtin_amdgcn_sched_barrier(0);   // the loads stay in their slot
+        }
       }
+    };
+    if constexpr (NT == 768) kloop(std::integral_constant<int, 1>{});
+    else if (wave < 4) kloop(std::integral_constant<int, 2>{});
+    else kloop(std::integral_constant<int, 1>{});
+    if (kh == 1) {
+      R[cur][nt][mt0][lane] = acc[0];
+      if (ntl == 2) R[cur][nt][mt0 + 1][lane] = acc[1];
     }
-    if (kh == 1) R[cur][nt][mt][lane] = acc;
     __syncthreads();   // stage cur consumed, stage cur ^ 1 complete, partials in R[cur]
     if (kh == 0) {
       const auto rs = make_rsrc(out + (size_t)b * (49 * 32), 49 * 32 * 4);
-      const f32x4 v = acc + R[cur][nt][mt][lane];
-      f32x4 y;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
-      bstore_f32x4(y, rs, 4 * (m * 32 + 16 * nt + 4 * g));
+      for (int t = 0; t < 2; ++t) {
+        if (t < ntl) {
+          const f32x4 v = acc[t] + R[cur][nt][mt0 + t][lane];
+          f32x4 y;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
+          bstore_f32x4(y, rs, 4 * ((16 * (mt0 + t) + i16) * 32 + 16 * nt + 4 * g));
+        }
+      }
     }
     cur ^= 1;
   }
+  if constexpr (LONE) {
+    __syncthreads();   // the last image's partials (R) are read
+    const int blk = blockIdx.x;
+    const int nimg = blk < B ? (B - 1 - blk) / G + 1 : 0;
+    conv3_lone_tiles<NP, NT>(a2, bw, bias, out, lds, blk, G, nimg, 0, 1);
+  }
 }
 
-// conv3 forward of output 48 = (6, 6) for 16 images per tile (row i16 of the B
-// operand: image 16 T + i16), the same operands, MFMA sequence, K-half sum and
-// epilogue as the kernels above (bit-identical); 4 waves (co tile w & 1, K half
-// w >> 1), grid-stride over tiles.  As conv2_fwd_lone_kernel, the tile's 16 patches
-// (3 rows of 3 pixels x 64 channels, 768 contiguous bytes per row) are loaded once
-// per block, the next tile's in registers during this tile's MFMAs, and staged in
-// LDS (two stages, image rows padded by 16 B).
+#ifndef C3F_COMPACT
+#define C3F_COMPACT 2   // standalone conv3 forward: 2 compact rows + the lone output in the same
+                        // launch (default), 1 compact rows + conv3_fwd_lone_kernel, 0 the 9-wide grid
+#endif
+template <int NP>
+__global__ __launch_bounds__(768) void conv3_fwd_c3_kernel(const float* __restrict__ a2, int B,
+                                                           const uint16_t* __restrict__ wpl,
+                                                           const float* __restrict__ bias,
+                                                           float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[C3C_LDS];
+  conv3_fwd_c3_body<NP, 768, C3F_COMPACT == 2>(a2, B, wpl, bias, out, lds);
+}
+
 template <int NP>
 __global__ __launch_bounds__(256) void conv3_fwd_lone_kernel(const float* __restrict__ a2, int B,
                                                              const uint16_t* __restrict__ wpl,
                                                              const float* __restrict__ bias,
                                                              float* __restrict__ out) {
-  constexpr int KS = 9, WN = 32 * 576, M = 48, IR = 145, NPC = 9;   // IR: f32x4 per staged image (144 + pad)
-  __shared__ f32x4 P[2][16 * IR];
-  __shared__ f32x4 R[2 * 64];
-  const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nt = wave & 1, kh = wave >> 1, co = 16 * nt + i16;
+  constexpr int KS = 9, WN = 32 * 576;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[C3L_LDS];
+  const int tid = threadIdx.x, i16 = tid & 15, g = (tid & 63) >> 4, wave = tid >> 6;
+  const int co = 16 * (wave & 1) + i16, kh = wave >> 1;
   bf16x8 bw[KS][3];
 #pragma unroll
   for (int s = 0; s < KS; ++s)
 #pragma unroll
     for (int p = 0; p < 3; ++p)
       bw[s][p] = *reinterpret_cast<const bf16x8*>(wpl + (size_t)p * WN + co * 576 + (9 * kh + s) * 32 + 8 * g);
-  const int ntile = (B + 15) / 16;
-  // piece q = tid + 256 j (j < 9): image q / 144, f32x4 f = q % 144 of its patch =
-  // ky * 48 + kx * 16 + channel quad; a2 offset ((6 + ky) * 9 + 6) * 64 + (f % 48) * 4
-  f32x4 pc[NPC];
-  auto fetch = [&](int T) {   // T >= ntile: a resource of 0 bytes (the loads read 0)
-    const int nimg = T < ntile ? (B - 16 * T < 16 ? B - 16 * T : 16) : 0;
-    const auto ra = make_rsrc(a2 + (size_t)(T < ntile ? 16 * T : 0) * 5184, nimg * 5184 * 4);
-#pragma unroll
-    for (int j = 0; j < NPC; ++j) {
-      const int q = tid + 256 * j, im = q / 144, f = q - 144 * im, ky = f / 48;
-      const int off = (im * 5184 + ((6 + ky) * 9 + 6) * 64 + (f - 48 * ky) * 4) * 4;
-      pc[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, off, 0, 0));
-    }
-  };
-  auto put = [&](int st) {
-#pragma unroll
-    for (int j = 0; j < NPC; ++j) {
-      const int q = tid + 256 * j, im = q / 144;
-      P[st][im * IR + (q - 144 * im)] = pc[j];
-    }
-  };
-  fetch(blockIdx.x);
-  put(0);
-  __syncthreads();
-  int cur = 0;
-  for (int T = blockIdx.x; T < ntile; T += gridDim.x) {
-    fetch(T + gridDim.x);
-    const int b = 16 * T + i16;
-    f32x4 acc = zero4();
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int ks = 9 * kh + s, tap = ks >> 1, c = 4 * (ks & 1) + g;
-      const f32x4* x = &P[cur][i16 * IR + tap * 16 + 2 * c];
-      Frag3 a;
-      split8(x[0], x[1], a, false);
-      const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
-#define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
-      PPO_PRODUCTS(NP, PPO_PART)
-#undef PPO_PART
-    }
-    if (kh == 1) R[nt * 64 + lane] = acc;
-    put(cur ^ 1);   // the stage read one tile ago (the last barrier retired its reads)
-    __syncthreads();   // partials in R; stage cur ^ 1 complete
-    if (kh == 0 && b < B) {
-      const f32x4 bv4 = *reinterpret_cast<const f32x4*>(bias + 16 * nt + 4 * g);
-      const f32x4 v = acc + R[nt * 64 + lane];
-      f32x4 y;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
-      *reinterpret_cast<f32x4*>(out + (size_t)b * (49 * 32) + M * 32 + 16 * nt + 4 * g) = y;
-    }
-    __syncthreads();   // R read before the next tile's partials
-    cur ^= 1;
-  }
+  conv3_lone_tiles<NP, 256>(a2, bw, bias, out, lds, 0, 1, B, blockIdx.x, gridDim.x);
 }
 
 // The rollout's CNN trunk in one launch: conv1 -> conv2 -> conv3 forward as three
@@ -1577,9 +1691,9 @@ __global__ __launch_bounds__(512) void trunk_fwd_kernel(const uint8_t* __restric
   conv1_fwd_bf16x3_body<4, MASK, NP == 1 ? 1 : 3>(obs, idx, row0, B, w1, b1, a1, m1,
                                                    reinterpret_cast<uint16_t (*)[4 * IMG2]>(lds));
   trunk_phase_sync();
-  conv2_fwd_x9c_body<NP, MASK>(a1, B, w2pl, b2, a2, m2, lds);
+  conv2_fwd_x9c_body<NP, MASK, 0, 5, true>(a1, B, w2pl, b2, a2, m2, lds);
   trunk_phase_sync();
-  conv3_fwd_x9_body<NP>(a2, B, w3pl, b3, a3, lds);
+  conv3_fwd_c3_body<NP, 512, true>(a2, B, w3pl, b3, a3, lds);
 }
 
 // conv3 weight gradient, image-resident on the bf16 matrix cores (exact split,
@@ -2359,7 +2473,7 @@ static int conv2_fwd_impl(const float* a1, int B, const float* w2p, const float*
   else if (mbits && g_products == 1) conv2_fwd_x9c_kernel<1, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
   else if (mbits) conv2_fwd_x9c_kernel<6, true><<<nb, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
   else PPO_LAUNCH_NP(conv2_fwd_x9c_kernel, nb, 512, st, a1, B, wpl, b2, out, nullptr);
-  if (C2F_LONE) {   // output pixel 72 of every image (the five-tile kernel leaves it)
+  if (C2F_LONE == 1) {   // output pixel 72 of every image in a launch of its own
     const int ntile = (B + 15) / 16;
     const unsigned nl = (unsigned)(ntile < 512 ? ntile : 512);
     if (mbits && g_products == 9) conv2_fwd_lone_kernel<9, true><<<nl, 512, 0, st>>>(a1, B, wpl, b2, out, mbits);
@@ -2394,9 +2508,11 @@ PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float*
   const uint16_t* wpl = planes_of(w3p, 32 * 576);
   if (C3F_COMPACT) {   // compact rows (three tiles) + the lone output (6, 6)
     PPO_LAUNCH_NP(conv3_fwd_c3_kernel, img_grid(B), 768, as_stream(stream), a2, B, wpl, b3, out);
-    const int ntile = (B + 15) / 16;
-    PPO_LAUNCH_NP(conv3_fwd_lone_kernel, (unsigned)(ntile < 512 ? ntile : 512), 256, as_stream(stream), a2, B, wpl,
-                  b3, out);
+    if (C3F_COMPACT == 1) {
+      const int ntile = (B + 15) / 16;
+      PPO_LAUNCH_NP(conv3_fwd_lone_kernel, (unsigned)(ntile < 512 ? ntile : 512), 256, as_stream(stream), a2, B,
+                    wpl, b3, out);
+    }
   } else {
     PPO_LAUNCH_NP(conv3_fwd_x9_kernel, img_grid(B), 512, as_stream(stream), a2, B, wpl, b3, out, g_stagger);
   }

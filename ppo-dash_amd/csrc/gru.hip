@@ -725,7 +725,7 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
     const float* __restrict__ sn, const float* __restrict__ sghn, const float* __restrict__ shin,
     const float* __restrict__ masks, const int64_t* __restrict__ idx, const float* __restrict__ whhT, int T, int n,
     float* __restrict__ dgi, float* __restrict__ dgh, float* __restrict__ dhz, float* __restrict__ carry,
-    int* __restrict__ cnt, int* __restrict__ err, int spin_max, int l2_mode) {
+    int* __restrict__ cnt, int* __restrict__ err, int spin_max) {
   constexpr int KW = 3 * H / 16;
   constexpr int NH = KW % 16 == 0 ? 2 : 1, KH = KW / NH;
   constexpr bool BF = KH % 8 == 0;
@@ -750,56 +750,17 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
       }
     gru_row_set(b, w[0]);
   }
-  // L2 agreement: when every unit block of the row group runs on one XCD, dgh is
-  // handed over through that XCD's L2: the producers store it plain (the line stays
-  // in the XCD's L2; a write-through sc1 store drops it, so 16 readers re-fetched
-  // the group's dgh from the memory side) and the consumers load it sc1.  The
-  // consumer's loads are sc1 on BOTH paths, so no dgh byte is ever served from a
-  // CU's vector L1 — the stale-L1 hazard of a plain load after a relaxed poll
-  // (MI355X_MICROARCH "Correctness boundaries") cannot arise whatever the L1 holds.
-  // Invariant of the L2 path (gru_seq_bwd16 row): (1) a producer's plain
-  // store is acknowledged (vmcnt) once it is in its XCD's L2, and every storing wave
-  // waits vmcnt(0) and joins a barrier before lane 0 adds to the group counter;
-  // (2) the consumer polls that counter, joins a barrier, then loads with sc1, which
-  // skips L1 and reads the XCD's L2; (3) producer and consumer share that L2 — each
-  // block reads its own HW_REG_XCC_ID and publishes it (release / acquire, once per
-  // launch), and the group takes the path only if all ids agree.  (3) is checked,
-  // never assumed: the grid's round-robin dispatch puts the unit blocks of group x
-  // on one XCD only when gridDim.x (= ceil(n/32)) is a multiple of 8; other groups,
-  // and every group with ppo_gru_l2_set(0), keep sc1 stores.  Block (x, 0) reports
-  // the path its group took (1 sc1, 2 L2) in the counter buffer (ppo_gru_seq_counters).
-  __shared__ int s_local;
-  {
-    int* start = cnt + gridDim.x;
-    int* xslot = cnt + 2 * gridDim.x + grp * 32;
-    if (tid == 0) {
-      const int xcc = __builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11)) & 15;   // HW_REG_XCC_ID[3:0]
-      __hip_atomic_store(xslot + blockIdx.y, xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(start + grp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      int it = 0, ab = 0;
-      while (spin_max == 0 || __hip_atomic_load(start + grp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < need) {
-        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-          ab = 1;
-          break;
-        }
-        if (++it > spin_max) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ab = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      int loc = !ab && l2_mode != 0;
-      for (int y = 0; y < need && loc; ++y)
-        loc = __hip_atomic_load(xslot + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == xcc + 1;
-      if (blockIdx.y == 0 && !ab)   // the group's path, for ppo_gru_seq_counters' report slots
-        __hip_atomic_store(cnt + (2 + 32) * gridDim.x + grp, loc ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_abort = ab;
-      s_local = loc;
-    }
-    __syncthreads();
-    if (s_abort) return;
-  }
+  // dgh hand-off (MI355X_MICROARCH "Correctness boundaries", hand-off table row 1):
+  // every dgh store is write-through (sc1), each storing wave drains (vmcnt(0)) and
+  // joins a barrier before lane 0 adds to the group counter (relaxed, agent scope);
+  // the consumer polls the counter, joins a barrier, then loads dgh with sc1 (the
+  // CU's L1 bypassed).  Round 6: the L2 variant (plain stores
+  // where a row group's unit blocks shared one XCD, checked by their XCC_IDs) bought
+  // 1.8 % of gru_seq_bwd at c5 (1.972-1.992 vs 2.011-2.019 ms, same box, alternating,
+  // profiles/r06_c_l2ab.log) for a form outside the guide's table, and was removed.
+  // Block (x, 0) reports that its group ran persistent (1) in the counter buffer.
+  if (tid == 0 && blockIdx.y == 0)
+    __hip_atomic_store(cnt + gridDim.x + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t gbytes = (uint32_t)((size_t)n * 3 * H * 4);
   // the epilogue's elements (as gru_step_bwd16_kernel): rows re[e] (clamped), units je[e]
   int re[2], je[2];
@@ -835,10 +796,7 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
   load_step(T - 1, (T - 1) & 1);
 #pragma unroll
   for (int e = 0; e < 2; ++e) pd[e] = dhz[(size_t)re[e] * H + je[e]];
-  auto steps = [&](auto local) {
-  // dgh stores: plain on the L2 path (the line stays in the group's L2), else sc1;
-  // dgh loads: sc1 on both (L1 bypassed, L2-served)
-  constexpr int CP_ST = decltype(local)::value ? 0 : 16, CP_LD = 16;
+  constexpr int CP_ST = 16, CP_LD = 16;   // sc1 stores and loads of dgh
   for (int t = T - 1; t >= 1; --t) {
     if (t < T - 1) {   // dgh(t) of the group's rows complete
       if (tid == 0) {
@@ -938,11 +896,6 @@ __global__ __launch_bounds__(256) void gru_seq_bwd16_kernel(
       store_rest();
     }
   }
-  };
-  if (s_local)
-    steps(std::true_type{});
-  else
-    steps(std::false_type{});
 }
 
 // 0: register-tiled step kernels where H allows; 1: the tile-GEMM steps (A/B)
@@ -958,10 +911,6 @@ static int g_gru_persist = 3;
 // bounded-wait length of the persistent kernels (polls of ~64 clocks each; 0: every
 // wait times out, which the fail-safe tests use)
 static int g_gru_spin = 1 << 21;
-
-// BPTT dgh hand-off: 1 (default) the L2 path where a row group's XCC_IDs agree,
-// 0 sc1 stores everywhere (gru_seq_bwd16_kernel)
-static int g_gru_l2 = 1;
 
 // Library-held synchronisation words for ppo_gru_seq_fwd (callers that pass their
 // own use ppo_gru_seq_fwd_ws): one buffer {err, counters...} per (device, stream),
@@ -1058,10 +1007,10 @@ int launch_seq_bwd16(const float* dout, const float* sr, const float* sz, const 
                      const float* shin, const float* masks, const int64_t* idx, const float* whhT, int T, int n,
                      float* dgi, float* dgh, float* dhz, float* carry, int* cnt, int* err, hipStream_t st) {
   const int groups = ceil_div(n, 32);
-  PPO_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)groups * (3 + 32) * sizeof(int), st), "ppo_gru_seq_bwd: counter reset");
+  PPO_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)groups * 2 * sizeof(int), st), "ppo_gru_seq_bwd: counter reset");
   dim3 grid((unsigned)groups, H / 16);
   gru_seq_bwd16_kernel<H><<<grid, 256, 0, st>>>(dout, sr, sz, sn, sghn, shin, masks, idx, whhT, T, n, dgi, dgh, dhz,
-                                                carry, cnt, err, g_gru_spin, g_gru_l2);
+                                                carry, cnt, err, g_gru_spin);
   PPO_LAUNCH_CHECK("gru_seq_bwd16_kernel");
   return 0;
 }
@@ -1157,7 +1106,7 @@ PPO_API int ppo_gru_variant_get(void) { return g_gru_variant; }
 // to 32 unit blocks (gru_seq_bwd16_kernel's L2 agreement) and the BPTT's path
 // report; layout [G step counters][G start counters][32 G XCC slots][G paths]
 // with G = ceil(n/32), path 1 = sc1 hand-off, 2 = L2 hand-off, 0 = not run
-PPO_API int ppo_gru_seq_counters(int n) { return n > 0 ? ceil_div(n, 32) * (3 + 32) : 1; }
+PPO_API int ppo_gru_seq_counters(int n) { return n > 0 ? ceil_div(n, 32) * 2 : 1; }
 
 PPO_API int ppo_gru_seq_fwd_ws(const float* h0, const float* masks, const int64_t* idx, const float* whh,
                                const float* bhh, const float* gi, int T, int n, int H, float* hout, float* save_r,
@@ -1266,15 +1215,6 @@ PPO_API int ppo_gru_persist_set(int v) {
   return 0;
 }
 PPO_API int ppo_gru_persist_get(void) { return g_gru_persist; }
-
-// persistent BPTT's dgh hand-off: 1 L2 path where a row group's XCC_IDs agree
-// (default), 0 sc1 stores for every group
-PPO_API int ppo_gru_l2_set(int v) {
-  PPO_REQUIRE(v == 0 || v == 1, "ppo_gru_l2_set: %d (0 sc1 everywhere, 1 L2 where the XCC_IDs agree)", v);
-  g_gru_l2 = v;
-  return 0;
-}
-PPO_API int ppo_gru_l2_get(void) { return g_gru_l2; }
 
 // bounded-wait length (polls) of the persistent kernels; tests force a timeout with 1
 PPO_API int ppo_gru_persist_spin_set(int polls) {

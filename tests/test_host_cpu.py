@@ -242,3 +242,13 @@ def test_conv_row_tiles_cover_every_output_once():
     for m in range(48):
         oy, ox = divmod(m, 7)
         assert 9 * oy + ox + 9 * 2 + 2 <= 80
+
+
+def test_bench_pmc_lookups_tolerate_other_workloads():
+    """bench.py's PMC lookups (MFMA utilisation, shader clock, HBM traffic) return
+    empty results — never raise — for a workload the committed profiles do not hold."""
+    import bench
+    util, clk, src = bench.pmc_mfma("no such workload")
+    assert util == {} and clk == {}
+    traffic, tsrc = bench.pmc_traffic("conv2_fwd", "no such workload")
+    assert traffic is None

@@ -41,21 +41,57 @@ def _load_flat(pol, flat):
             off += p.numel()
 
 
-def _digest_check(got_flat, d, prefix, shapes, tol):
+def _digest_check(got_flat, d, prefix, shapes, tol, rel=True, scale=1.0):
+    """rel: sampled elements within tol x the tensor's max |x| and each tensor's L2
+    within 1e-5 relative (gradients); else within tol absolute and the L2 within
+    tol x sqrt(numel) (parameters: an Adam step moves every element by ~lr whatever
+    its size)."""
     idx = d[f"{prefix}_idx"]
-    ref = d[f"{prefix}_sampled"].astype(np.float64)
+    ref = d[f"{prefix}_sampled"].astype(np.float64) * scale
     got = np.asarray(got_flat, np.float64)
     off = 0
     for k, (name, shape) in enumerate(shapes):
         n = int(np.prod(shape))
         sel = (idx >= off) & (idx < off + n)
-        tmax = d[f"{prefix}_tmax"][k]
+        tmax = d[f"{prefix}_tmax"][k] * scale
         err = np.abs(got[idx[sel]] - ref[sel]).max()
-        assert err <= tol * max(tmax, 1e-6), (prefix, name, err, tmax)
-        l2 = np.sqrt((got[off:off + n] ** 2).sum())
-        np.testing.assert_allclose(l2, d[f"{prefix}_tl2"][k], rtol=1e-5, err_msg=f"{prefix} {name}")
+        l2, l2ref = np.sqrt((got[off:off + n] ** 2).sum()), d[f"{prefix}_tl2"][k] * scale
+        if rel:
+            assert err <= tol * max(tmax, 1e-6), (prefix, name, err, tmax)
+            np.testing.assert_allclose(l2, l2ref, rtol=1e-5, err_msg=f"{prefix} {name}")
+        else:
+            assert err <= tol, (prefix, name, err)
+            assert abs(l2 - l2ref) <= tol * np.sqrt(n), (prefix, name, l2, l2ref)
         off += n
     assert off == got.size
+
+
+def _grads_vs_float64(got_flat, d, shapes, fro_tol=3e-5, max_tol=1e-4, ratio=2.0, floor=1e-6):
+    """The first minibatch's gradient against the fixture's float64 digest of the
+    same gradient (oracle/torch_ref float64 autograd on the recorded rollout), with
+    the reference's own fp32 gradient (its digest) as the precision yardstick — the
+    rule of tests/helpers/gradcheck.py on the sampled elements: per tensor, max |err|
+    <= max(max_tol, ratio x the reference's) of max |g|, relative Frobenius error <=
+    max(fro_tol, ratio x the reference's) and <= ratio x the reference's + floor."""
+    idx = d["mb0_grad_f64_idx"]
+    f64 = d["mb0_grad_f64_sampled"].astype(np.float64)
+    r32 = d["mb0_preclip_grad_sampled"].astype(np.float64)
+    got = np.asarray(got_flat, np.float64)[idx]
+    off, bad = 0, []
+    for k, (name, shape) in enumerate(shapes):
+        n = int(np.prod(shape))
+        sel = (idx >= off) & (idx < off + n)
+        scale, norm = max(d["mb0_grad_f64_tmax"][k], 1e-12), max(np.linalg.norm(f64[sel]), 1e-12)
+        e, e32 = got[sel] - f64[sel], r32[sel] - f64[sel]
+        mx, fro = np.abs(e).max() / scale, np.linalg.norm(e) / norm
+        mx32, fro32 = np.abs(e32).max() / scale, np.linalg.norm(e32) / norm
+        line = f"{name:28s} HIP max {mx:.2e} fro {fro:.2e} | reference fp32 max {mx32:.2e} fro {fro32:.2e}"
+        print(line, flush=True)
+        if not (mx <= max(max_tol, ratio * mx32) and fro <= max(fro_tol, ratio * fro32)
+                and fro <= ratio * fro32 + floor):
+            bad.append(line)
+        off += n
+    assert not bad, bad
 
 
 def _capture_steps(agent):
@@ -112,9 +148,12 @@ def _cnn_replay(gpu, d, obs_u8):
     np.testing.assert_allclose(losses, d["losses"], rtol=1e-4, atol=1e-6)
     assert len(grads) == E * Mb
     shapes = O.cnn_param_shapes(hidden)
-    _digest_check(grads[0].cpu().numpy(), d, "mb0_preclip_grad", shapes, 1e-5)
+    if "mb0_grad_f64_idx" in d.files:   # a production-size minibatch: held to the reference's own precision
+        _grads_vs_float64(grads[0].cpu().numpy(), d, shapes)
+    else:
+        _digest_check(grads[0].cpu().numpy(), d, "mb0_preclip_grad", shapes, 1e-5)
     final = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).cpu().numpy()
-    _digest_check(final, d, "final_params", shapes, 2e-5)
+    _digest_check(final, d, "final_params", shapes, 2e-5, rel=False)
 
 
 def test_cnn_h512_iteration_replays_reference(gpu):
@@ -131,7 +170,11 @@ def test_cnn_wide_iteration_replays_reference(gpu):
     the CU count, so ppo_fc_fwd runs the production 128 x 128 tile kernel
     (DenseReluFwdB<XP128>) and the persistent conv kernels walk 64 images per
     block, as at c3's 65,536-sample minibatch.  The observations are regenerated
-    from the fixture's generator seed (checked by byte sum and CRC-32)."""
+    from the fixture's generator seed (checked by byte sum and CRC-32).  The
+    gradient of this 16,384-sample minibatch is checked against its float64 value
+    with the reference's own fp32 error as the bar (_grads_vs_float64): the
+    reference itself is 5.5e-5 (max) / 4.0e-5 (Frobenius) from float64 on conv1's
+    weight gradient here."""
     import zlib
     d = golden("cnn_update_wide.npz")
     hidden, N, T, E, Mb = (int(x) for x in d["meta"])
@@ -187,12 +230,12 @@ def test_recurrent_h256_iteration_replays_reference(gpu):
         M.set_sampling_mode("device")
         agent.optimizer._step_flat = orig
     torch.cuda.synchronize()
-    # the BPTT's path report (ppo_gru_seq_counters layout: [G step][G BPTT start][32 G XCC_ID][G paths]):
-    # 1 = sc1 hand-off, 2 = L2 hand-off; 0 would mean the step launches ran
+    # the BPTT's report (ppo_gru_seq_counters layout: [G step counters][G reports]): 1 = the
+    # group ran the persistent kernel; 0 would mean the step launches ran
     n = N // Mb
     G = -(-n // 32)
     cnt = eng.ws["train"].bufs["gru_cnt"].cpu().numpy()
-    assert all(int(x) in (1, 2) for x in cnt[34 * G:35 * G]), cnt[34 * G:35 * G]
+    assert (cnt[G:2 * G] == 1).all(), cnt[:2 * G]
     assert np.array_equal(st.actions.cpu().numpy(), d["actions"])
     np.testing.assert_allclose(st.action_log_probs.cpu().numpy(), d["action_log_probs"], atol=1e-5)
     np.testing.assert_allclose(st.value_preds[:T].cpu().numpy(), d["values"], atol=1e-5)
@@ -206,4 +249,4 @@ def test_recurrent_h256_iteration_replays_reference(gpu):
     np.testing.assert_allclose(mb, d["mb_losses"], rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(losses, d["losses"], rtol=1e-4, atol=1e-6)
     final = torch.cat([p.detach().reshape(-1) for p in pol.parameters()]).cpu().numpy()
-    _digest_check(final, d, "final_params", shapes, 2e-5)
+    _digest_check(final, d, "final_params", shapes, 2e-5, rel=False)

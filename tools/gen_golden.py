@@ -360,6 +360,26 @@ def gen_cnn_update(S, M, P, *, hidden, N, T, E, Mb, lr, fname, lowres=False, str
              meta=np.array([hidden, N, T, E, Mb]), lr=np.array([lr]))
         return
     extra = {}
+    if obs_seed is not None:
+        # the float64 gradient of the first minibatch (oracle/torch_ref: the same loss by
+        # float64 autograd, on the reference's recorded rollout): at 16,384 samples a
+        # weight gradient sums up to 6.5 M products, and the reference's own fp32
+        # arithmetic is 1e-5 .. 3e-5 from float64 — the replay is held to its precision
+        # against this (tests/helpers/gradcheck.py's rule), not to 1e-5 of the fp32 record
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+        from oracle import torch_ref as TR
+        T_, N_ = T, N
+        fl = lambda t: torch.as_tensor(t).reshape(T_ * N_)  # noqa: E731
+        adv = torch.from_numpy(returns[:-1] - vpreds[:-1])
+        adv = (adv - adv.mean()) / (adv.std() + 1e-5)   # ppo.py:35-37, fp32 as the reference
+        p64 = TR.unflatten(torch.from_numpy(init), hidden, dtype=torch.float64, requires_grad=True)
+        torch.set_num_threads(8)
+        g64, _ = TR.minibatch_grads(p64, all_obs[:T].reshape(T * N, 4, 84, 84),
+                                    torch.from_numpy(np.stack(actions).astype(np.int64)).reshape(-1),
+                                    fl(np.stack(logps)), fl(adv), fl(vpreds[:-1]), fl(returns[:-1]),
+                                    clip=0.1, value_coef=0.5, entropy_coef=0.001, chunk=1024)
+        torch.set_num_threads(1)
+        extra.update(digest("mb0_grad_f64", torch.cat([t.detach().reshape(-1) for t in g64]).numpy(), pol, stride))
     if obs_seed is None:
         extra["obs_u8"] = obs_u8
     else:

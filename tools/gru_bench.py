@@ -22,8 +22,6 @@ def main():
     ap.add_argument("--H", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--modes", default="0,1,5")
-    ap.add_argument("--l2", default="", help="BPTT hand-off A/B: comma list of ppo_gru_l2_set values "
-                    "timed alternately in persistent mode 3 (e.g. 1,0,1,0,1,0)")
     a = ap.parse_args()
     T, n, H = a.T, a.n, a.H
     dev = torch.device("cuda:0")
@@ -53,32 +51,6 @@ def main():
         call("ppo_gru_seq_bwd", dout.data_ptr(), o["r"].data_ptr(), o["z"].data_ptr(), o["n"].data_ptr(),
              o["ghn"].data_ptr(), o["hin"].data_ptr(), masks.data_ptr(), None, whhT.data_ptr(), T, n, H,
              dgi.data_ptr(), dgh.data_ptr(), dhz.data_ptr(), carry.data_ptr(), s)
-
-    if a.l2:
-        prev_l2 = call("ppo_gru_l2_get")
-        call("ppo_gru_persist_set", 3)
-        try:
-            fwd()
-            href = None
-            for v in [int(x) for x in a.l2.split(",")]:
-                call("ppo_gru_l2_set", v)
-                bwd()
-                torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.reps):
-                    bwd()
-                e1.record()
-                torch.cuda.synchronize()
-                ms = e0.elapsed_time(e1) / a.reps
-                same = "" if href is None else f" dgh bit-identical: {torch.equal(href, dgh)}"
-                href = dgh.clone() if href is None else href
-                print(f"l2 {v} bwd: {ms:7.3f} ms  {1e3 * ms / T:6.2f} us/step{same}", flush=True)
-                assert call("ppo_gru_persist_timeouts", s) == 0
-        finally:
-            call("ppo_gru_l2_set", prev_l2)
-            call("ppo_gru_persist_set", prev)
-        return
 
     ref = None
     try:

@@ -163,12 +163,20 @@ def main():
                      2.0 * B * 768 * 256),
         "conv1_wreduce": (lambda: call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), z1, 32, 256, 0, 0, 0,
                                        gw.data_ptr(), gb.data_ptr(), 1.0 / 255, 0, s), 0.0),
+        # the rollout's fused trunk (conv1 -> conv2 -> conv3 in one launch) on one rollout step's 4,096 images
+        "trunk_4096": (lambda: call("ppo_trunk_fwd", obs.data_ptr(), idx.data_ptr(), 0, min(B, 4096), w1.data_ptr(),
+                                    b1.data_ptr(), a1.data_ptr(), None, pk[0], b2.data_ptr(), a2.data_ptr(), None,
+                                    pk[1], b3.data_ptr(), a3.data_ptr(), s),
+                       2.0 * min(B, 4096) * (400 * 32 * 256 + 81 * 64 * 512 + 49 * 32 * 576)),
     }
     # realistic activations for the backward kernels
     K["conv1_fwd_mask"][0](); K["conv2_fwd_mask"][0](); K["conv3_fwd"][0](); K["fc_fwd"][0]()
     K["fc_dgrad"][0](); K["conv3_dgrad"][0](); K["conv2_dgrad"][0]()
     torch.cuda.synchronize()
-    only = [x for x in a.only.split(",") if x]
+    # default: the c3 iteration's kernels (the engine's training forms) and the rollout trunk
+    only = [x for x in a.only.split(",") if x] or [
+        "conv1_fwd_mask", "conv2_fwd_mask", "conv3_fwd", "fc_fwd", "fc_dgrad", "fc_wgrad", "conv3_dgrad_bits",
+        "conv3_wgrad", "conv2_dgrad_bits", "conv2_wgrad", "conv1_wgrad", "conv1_fwd", "conv2_fwd", "trunk_4096"]
     total = 0.0
     for name, (fn, fl) in K.items():
         if only and name not in only:
