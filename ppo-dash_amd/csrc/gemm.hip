@@ -1399,9 +1399,6 @@ __device__ __forceinline__ void conv3_fwd_x9_body(const float* __restrict__ a2, 
   }
 }
 
-#ifndef C3F_COMPACT
-#define C3F_COMPACT 1   // standalone conv3 forward: compact rows (conv3_fwd_c3_kernel) + the lone output
-#endif
 template <int NP>
 __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restrict__ a2, int B,
                                                           const uint16_t* __restrict__ wpl,
@@ -2307,6 +2304,7 @@ PPO_API int ppo_tune_set(const char* key, int value) {
     g_small_b = value;
     return 0;
   }
+
   if (strcmp(key, "stagger") == 0) {
 #ifndef PPO_DIAG
     // bits 0-3 are schedule switches (same results); bits >= 4 select the timing-

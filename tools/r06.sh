@@ -27,6 +27,8 @@ for st in ${STEPS:-tests}; do
     bench) run bench 500 python -u bench.py ${BENCH_ARGS:-} ;;
     kbab) run kbab 600 bash -c 'for r in 1 2; do for L in ${KB_LIBS:-base cur}; do echo "--- lib=$L"; if [ $L = cur ]; then unset PPO_HIP_LIB; else export PPO_HIP_LIB=ppo-dash_amd/lib/libppo_hip_$L.so; fi; timeout -k 10 150 python tools/kbench.py --reps 10 ${KB_ARGS:-} || exit 1; done; done' ;;
     ab) TAILN=12 run abrun 900 env TAG=${TAG} LIBS="${AB_LIBS:-base cur}" ROUNDS=${AB_ROUNDS:-2} ARGS="${AB_ARGS:-}" bash tools/ab_bench.sh ;;
+    kbtune) run kbtune 600 bash -c 'for r in 1 2; do for T in ${KB_TUNES:?}; do echo "--- tune=$T"; timeout -k 10 150 python tools/kbench.py --reps 10 --tune $T ${KBT_ARGS:-} || exit 1; done; done' ;;
+    sqab) run sqab 900 bash -c 'for L in ${SQ_LIBS:-base cur}; do if [ $L = cur ]; then unset PPO_HIP_LIB; else export PPO_HIP_LIB=$PWD/ppo-dash_amd/lib/libppo_hip_$L.so; fi; ONLY=${SQ_ONLY:?} bash tools/pmc_sq.sh || exit 1; rm -rf gpurun_out/pmc1_$L; mv gpurun_out/pmc1 gpurun_out/pmc1_$L; done' ;;
     c5) run c5 600 python -u bench.py --recurrent --num-steps 256 --no-cpu-baseline --no-gae-roofline --no-boundary ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
