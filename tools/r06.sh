@@ -20,7 +20,7 @@ run() {   # name seconds cmd...
 }
 for st in ${STEPS:-tests}; do
   case $st in
-    tests) run tests ${TESTS_S:-900} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${K:-} ;;
+    tests) run tests ${TESTS_S:-900} python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${KEXPR:+-k "$KEXPR"} ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     gru) run gru 240 python -u tools/gru_bench.py --modes 0,3 ;;
     kbench) run kbench 240 python -u tools/kbench.py ${KB_ARGS:-} ;;
