@@ -31,6 +31,12 @@ namespace {
 // Forward problems
 // ---------------------------------------------------------------------------
 constexpr int IMG = 84, IMG2 = 84 * 84;
+// conv1 forward's LDS image stage: channel stride 7,104 bf16 = 3,552 dwords, which is
+// 32 mod 64 (a ds_read_b64 lane's bank is its dword address mod 64), so that the two
+// 16-lane halves of a 32-lane group, reading the same rows of channels c and c + 1,
+// use complementary banks (see conv1_fwd_bf16x3_body)
+constexpr int C1S = 7104;
+static_assert(C1S >= IMG2 && (C1S / 2) % 64 == 32, "conv1 stage channel stride");
 
 // conv1: 8x8 stride 4 over the u8/f32 NCHW observation, k = (c, ky, kx) (torch order)
 template <typename InT, class C_>
@@ -68,12 +74,19 @@ struct Conv1Fwd : C_ {
 // fp32 arithmetic (as exact per product as v_mfma_f32_*_f32), at 3 bf16 MFMAs
 // per 16x16x32 block instead of 8 f32 16x16x4 MFMAs of twice the cycles.
 // One persistent block (8 waves) per CU walks images: the image being computed
-// sits in LDS as bf16 (2 x 28,224 B -> 56,448 B; two stages), the next image is
-// in flight into registers and converted/stored behind the compute.  Wave w:
+// sits in LDS as bf16 (4 channels at stride C1S: 56,832 B; two stages), the next
+// image is in flight into registers and converted/stored behind the compute.  Wave w:
 // output channels 16 * (w & 1) + [0, 16), row tiles {w >> 1, (w >> 1) + 4, ...}
-// of 16 output pixels.  k-step s covers k = 32s + [0, 32); lane group
-// g = lane >> 4 supplies k = 32s + 8g + j, j = 0..7 — one kx row of the patch,
-// 8 adjacent pixels, so an A fragment is one 16-byte LDS read.
+// of 16 output pixels.  k-step s covers channels 2 (s >> 2) + {0, 1} and kernel
+// rows 2 (s & 3) + {0, 1}; lane group g = lane >> 4 supplies channel
+// 2 (s >> 2) + (g & 1), row 2 (s & 3) + (g >> 1), kx = j = 0..7 — 8 adjacent
+// pixels, 16 bytes at an 8-byte-aligned address, read as two ds_read_b64.  Lanes
+// 0-31 (g = 0, 1) then read the same rows of two channels C1S apart: each 16-lane
+// half covers 32 consecutive dwords mod 64 (16 consecutive output pixels, also
+// across an output-row wrap: 4 input rows = 168 dwords = 40 mod 64), the other
+// half the complementary 32, so both reads are conflict-free at 2 LDS cycles.
+// (Left to itself the compiler merges two 8-byte reads into one ds_read2_b64, 8 LDS
+// cycles, MI355X_MICROARCH §LDS; the reads are volatile so that it does not.)
 // NPW: weight parts summed (3: exact fp32 weights; 1: half-precision mode, bf16 weights)
 // The body takes its LDS (img: two image stages) so that the fused rollout trunk
 // (trunk_fwd_kernel) can run it as its first phase in a shared buffer.
@@ -82,9 +95,10 @@ __device__ __forceinline__ void conv1_fwd_bf16x3_body(const uint8_t* __restrict_
                                                       const int64_t* __restrict__ idx, long long row0, int B,
                                                       const float* __restrict__ w, const float* __restrict__ bias,
                                                       float* __restrict__ out, uint16_t* __restrict__ mbits,
-                                                      uint16_t (*__restrict__ img)[C * IMG2]) {
+                                                      uint16_t (*__restrict__ img)[C * C1S]) {
   constexpr int NPX = C * IMG2, CH = NPX / 16, K = C * 64, KS = K / 32, PER = (CH + 511) / 512;
-  static_assert(NPX % 16 == 0, "16-pixel chunks");
+  constexpr int CCH = IMG2 / 16;   // 16-pixel chunks per channel (441)
+  static_assert(IMG2 % 16 == 0 && C % 2 == 0, "16-pixel chunks, channel pairs");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ct = wave & 1, rq = wave >> 1;
   const int i16 = lane & 15, g = lane >> 4;
@@ -94,7 +108,8 @@ __device__ __forceinline__ void conv1_fwd_bf16x3_body(const uint8_t* __restrict_
   bf16x8 wf[3][KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    const float* wp = w + (size_t)col * K + 32 * s + 8 * g;
+    const int c = 2 * (s >> 2) + (g & 1), ky = 2 * (s & 3) + (g >> 1);
+    const float* wp = w + (size_t)col * K + c * 64 + ky * 8;
     uint32_t h[8], m[8], l[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) split_bf16x3(wp[j], h[j], m[j], l[j]);
@@ -127,7 +142,8 @@ __device__ __forceinline__ void conv1_fwd_bf16x3_body(const uint8_t* __restrict_
           o[2 * q] = __builtin_amdgcn_perm(__float_as_uint(f[1]), __float_as_uint(f[0]), 0x07060302u);
           o[2 * q + 1] = __builtin_amdgcn_perm(__float_as_uint(f[3]), __float_as_uint(f[2]), 0x07060302u);
         }
-        uint4* d = reinterpret_cast<uint4*>(img[buf] + 16 * c);
+        const int ch = c / CCH;
+        uint4* d = reinterpret_cast<uint4*>(img[buf] + ch * C1S + 16 * (c - ch * CCH));
         d[0] = uint4{o[0], o[1], o[2], o[3]};
         d[1] = uint4{o[4], o[5], o[6], o[7]};
       }
@@ -154,21 +170,23 @@ __device__ __forceinline__ void conv1_fwd_bf16x3_body(const uint8_t* __restrict_
       f32x4 acc[NTL];
 #pragma unroll
       for (int t = 0; t < NTL; ++t) acc[t] = zero4();
-      int pix[NTL];   // pixel offset of this lane's output row, per row tile
+      // this lane's patch origin per row tile (channel g & 1, row g >> 1)
+      int pix[NTL];
 #pragma unroll
       for (int t = 0; t < NTL; ++t) {
         const int row = (rq + 4 * t) * 16 + i16, oy = row / 20, ox = row - oy * 20;
-        pix[t] = oy * (4 * IMG) + ox * 4;
+        pix[t] = (g & 1) * C1S + (g >> 1) * IMG + oy * (4 * IMG) + ox * 4;
       }
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const int k0 = 32 * s + 8 * g;
-        const uint16_t* Is = I + (k0 >> 6) * IMG2 + ((k0 >> 3) & 7) * IMG;
+        const uint16_t* Is = I + 2 * (s >> 2) * C1S + 2 * (s & 3) * IMG;
         bf16x8 a[NTL];
 #pragma unroll
-        for (int t = 0; t < NTL; ++t) {
-          const uint2* p2 = reinterpret_cast<const uint2*>(Is + pix[t]);   // 8-B aligned: 4ox bf16
-          const uint2 lo = p2[0], hi = p2[1];
+        for (int t = 0; t < NTL; ++t) {   // 8-B aligned: 4ox bf16; volatile: not merged into ds_read2_b64
+          typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+          const volatile __attribute__((address_space(3))) u32x2* p2 =
+              (const volatile __attribute__((address_space(3))) u32x2*)(Is + pix[t]);
+          const u32x2 lo = p2[0], hi = p2[1];
           a[t] = __builtin_bit_cast(bf16x8, uint4{lo.x, lo.y, hi.x, hi.y});
         }
 #pragma unroll
@@ -212,7 +230,7 @@ __global__ __launch_bounds__(512) void conv1_fwd_bf16x3_kernel(const uint8_t* __
                                                                const float* __restrict__ bias,
                                                                float* __restrict__ out,
                                                                uint16_t* __restrict__ mbits) {
-  __shared__ __attribute__((aligned(16))) uint16_t img[2][C * IMG2];
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][C * C1S];
   conv1_fwd_bf16x3_body<C, MASK, NPW>(obs, idx, row0, B, w, bias, out, mbits, img);
 }
 
@@ -1669,8 +1687,8 @@ __global__ __launch_bounds__(256) void conv3_fwd_lone_kernel(const float* __rest
 // profiles/r05_l_c5_kernel_stats.csv) — and each phase is the unchanged kernel body
 // (bit-identical outputs to the three launches).  The phases share one LDS buffer
 // (the largest phase, conv2: 154,368 B).
-constexpr int TRUNK_LDS = C2F_LDS > C3F_LDS ? (C2F_LDS > 2 * 4 * IMG2 * 2 ? C2F_LDS : 2 * 4 * IMG2 * 2)
-                                            : (C3F_LDS > 2 * 4 * IMG2 * 2 ? C3F_LDS : 2 * 4 * IMG2 * 2);
+constexpr int TRUNK_LDS = C2F_LDS > C3F_LDS ? (C2F_LDS > 2 * 4 * C1S * 2 ? C2F_LDS : 2 * 4 * C1S * 2)
+                                            : (C3F_LDS > 2 * 4 * C1S * 2 ? C3F_LDS : 2 * 4 * C1S * 2);
 __device__ __forceinline__ void trunk_phase_sync() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's output stores are in L2
   __syncthreads();
@@ -1686,7 +1704,7 @@ __global__ __launch_bounds__(512) void trunk_fwd_kernel(const uint8_t* __restric
                                                        const float* __restrict__ b3, float* __restrict__ a3) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[TRUNK_LDS];
   conv1_fwd_bf16x3_body<4, MASK, NP == 1 ? 1 : 3>(obs, idx, row0, B, w1, b1, a1, m1,
-                                                   reinterpret_cast<uint16_t (*)[4 * IMG2]>(lds));
+                                                   reinterpret_cast<uint16_t (*)[4 * C1S]>(lds));
   trunk_phase_sync();
   conv2_fwd_x9c_body<NP, MASK, 0, 5, true>(a1, B, w2pl, b2, a2, m2, lds);
   trunk_phase_sync();
