@@ -69,6 +69,44 @@ def _check_returns(st, nv):
     return adv
 
 
+def _engine_relu_masks(eng, B, H):
+    """the ReLU decisions of the engine's training forward of the minibatch just run
+    (its workspace activations a1..a3 and fc output h, NHWC -> the reference's NCHW)"""
+    bufs = eng.ws["train"].bufs
+    a1 = bufs["a1"][:B * 12800].view(B, 20, 20, 32).permute(0, 3, 1, 2)
+    a2 = bufs["a2"][:B * 5184].view(B, 9, 9, 64).permute(0, 3, 1, 2)
+    a3 = bufs["a3"][:B * 1568].view(B, 7, 7, 32).permute(0, 3, 1, 2)
+    h = bufs["h"][:B * H].view(B, H)
+    return [t > 0 for t in (a1, a2, a3, h)]
+
+
+def _check_relu_decisions(p, obs_in, ridx, masks, chunk=4096, rel=1e-5):
+    """every ReLU decision of the engine agrees with float64's, except where the
+    float64 pre-activation is within rel x that layer's max |pre-activation| of 0;
+    returns the number of such flips per layer"""
+    w1, b1, w2, b2, w3, b3, w4, b4 = [t.detach() for t in p[:8]]
+    B = masks[0].shape[0]
+    flips, worst, zmax = [0] * 4, [0.0] * 4, [0.0] * 4
+    with torch.no_grad():
+        for s in range(0, B, chunk):
+            e = min(B, s + chunk)
+            rows = slice(s, e) if ridx is None else ridx[s:e].to(obs_in.device)
+            x = TR._decode(obs_in[rows], w1.device, torch.float64)
+            z1 = TR.conv_unfold(x, w1, b1, 4)
+            z2 = TR.conv_unfold(torch.relu(z1), w2, b2, 2)
+            z3 = TR.conv_unfold(torch.relu(z2), w3, b3, 1)
+            z4 = torch.nn.functional.linear(torch.relu(z3).reshape(e - s, -1), w4, b4)
+            for k, z in enumerate((z1, z2, z3, z4)):
+                d = (z > 0) != masks[k][s:e]
+                zmax[k] = max(zmax[k], z.abs().max().item())
+                if d.any():
+                    flips[k] += int(d.sum())
+                    worst[k] = max(worst[k], z[d].abs().max().item())
+    for k in range(4):
+        assert worst[k] <= rel * zmax[k], (k, flips, worst, zmax)
+    return flips
+
+
 def _obs_setup(kind, N, T, gpu, pol, env):
     """storage + env-step writer for an observation form (bench.py --obs):
     u8 — synthetic u8 4x84x84 frames (the headline); f32 — the reference's fp32
@@ -155,14 +193,21 @@ def test_cnn_iteration_full_size(gpu, N, kind):
                   flat(st.value_preds)[idx], flat(st.returns)[idx]]
         ridx = None
     p = TR.unflatten(flat0, H, dtype=torch.float64, device=gpu, requires_grad=True)
+    # both references take the engine's ReLU decisions, each checked first against
+    # float64's own: they may differ only where float64's pre-activation is within
+    # rounding of 0 (a flip there moves a gradient by a whole row's term — at c2's
+    # 16,384 rows one fc flip is ~3e-6 of the fc bias gradient, which made the
+    # comparison a coin toss on summation order); the gradients then measure arithmetic
+    masks = _engine_relu_masks(eng, B, H)
+    print("ReLU decisions differing from float64's:", _check_relu_decisions(p, obs_in, ridx, masks), flush=True)
     grads, losses = TR.minibatch_grads(p, obs_in, *planes, idx=ridx, clip=HP["clip"], value_coef=HP["value_coef"],
-                                       entropy_coef=HP["entropy_coef"])
+                                       entropy_coef=HP["entropy_coef"], masks=masks)
     print("float64 reference done", flush=True)
     # the same gradient at the reference's precision: torch fp32 autograd on the
     # device (im2col GEMMs on the vendor BLAS, chunk gradients summed in fp32)
     p32 = TR.unflatten(flat0, H, dtype=torch.float32, device=gpu, requires_grad=True)
     g32, _ = TR.minibatch_grads(p32, obs_in, *planes, idx=ridx, chunk=8192, clip=HP["clip"],
-                                value_coef=HP["value_coef"], entropy_coef=HP["entropy_coef"])
+                                value_coef=HP["value_coef"], entropy_coef=HP["entropy_coef"], masks=masks)
     print("fp32 comparator done", flush=True)
     g32 = torch.cat([t.reshape(-1) for t in g32]).cpu().numpy()
     _check_grads(cap.grad.cpu().numpy(), grads, shapes, fp32_flat=g32)
