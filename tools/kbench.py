@@ -93,7 +93,24 @@ def main():
         obs32 = (torch.randn(rows, 4, 84, 84, device=dev, generator=g) * 0.8).contiguous()
         frames = torch.randint(0, 256, (rows, 84, 84, 3), dtype=torch.uint8, device=dev, generator=g)
         mean = torch.rand(84, 84, 3, device=dev, generator=g) * 60 + 20
+    # heads_train inputs: storage planes indexed by idx (the minibatch rows), partials
+    # sized for 32 rows per wave or fewer
+    st_act = torch.randint(0, 8, (rows,), dtype=torch.int64, device=dev, generator=g)
+    st_f = rn(4, rows, sc=1.0)   # old_logp, adv, vpred, ret
+    st_f[0] = -st_f[0].abs() - 1.0
+    hmax = -(-B // 32)
+    part = torch.empty(hmax * (9 * H + 9 + 4), device=dev)
+
+    def heads_train():
+        nb = call("ppo_heads_train_blocks", B)
+        call("ppo_heads_train", h.data_ptr(), None, B, H, hw.data_ptr(), hw.data_ptr() + 4 * H,
+             hw.data_ptr() + 4 * (H + 1), hw.data_ptr() + 4 * (9 * H + 1), 8, idx.data_ptr(), 0, st_act.data_ptr(),
+             st_f[0].data_ptr(), st_f[1].data_ptr(), st_f[2].data_ptr(), st_f[3].data_ptr(), 0.1, 0.5, 0.01, 1.0 / B, 1,
+             1, dz3.data_ptr(), None, part.data_ptr(), part.data_ptr() + 4 * nb * 9 * H,
+             part.data_ptr() + 4 * nb * (9 * H + 9), s)
+
     K = {
+        "heads_train": (heads_train, 0.0),
         "conv1_fwd": (lambda: call("ppo_conv1_fwd", obs.data_ptr(), 1, idx.data_ptr(), 0, 4, B, w1.data_ptr(),
                                    b1.data_ptr(), a1.data_ptr(), s), 2.0 * B * 400 * 32 * 256),
         "conv2_fwd": (lambda: call("ppo_conv2_fwd", a1.data_ptr(), B, pk[0], b2.data_ptr(), a2.data_ptr(), s),
