@@ -194,6 +194,14 @@ int ppo_transpose(const float* src, int rows, int cols, float* dst, void* stream
  * of the layer below fused, wgrad as split-K partial slabs + deterministic reduce */
 int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt, int N, const float* act, float* dx,
                           void* stream);
+/* the training forward's conv3 (model.py:179) that also writes its ReLU mask bits,
+ * uint16 [B][49][2] (bit j of word (p, t): output channel 16 t + j of pixel p > 0), and
+ * the fc dgrad (N = 1568) masked by those bits instead of the fp32 activation:
+ * bit-identical to ppo_conv3_fwd + ppo_linear_dgrad_mask(act = conv3's output) */
+int ppo_conv3_fwd_mask(const float* a2, int B, const float* w3p, const float* b3, float* out, uint16_t* mbits,
+                       void* stream);
+int ppo_fc_dgrad_bits(const float* dy, int M, int K, const float* wt, const uint16_t* mbits, float* dx,
+                      void* stream);
 int ppo_conv3_dgrad(const float* dz3, int B, const float* w3d, const float* a2, float* dz2, void* stream);
 /* conv3 dgrad with conv2's ReLU mask as bits (from ppo_conv2_fwd_mask): 648 B instead of
  * 20.7 KB read per image; ppo_conv3_dgrad_bits_ok() is 1 (kept for ABI stability) */
@@ -236,7 +244,9 @@ int ppo_colsum(const float* src, long long ld, int rows, long long cols, float* 
  *   "conv1_wgrad" 9 one-wave-per-SIMD k-split kernel (default), 10 its wave-pair form,
  *                 8 the eight-wave k-split kernel, 5 the part-pipelined kernel
  *   "x9"          1 split-bf16 dense GEMMs (default), 0 fp32 MFMA, 2 split everywhere
- *   "fc_splitk"   K slices of the rollout-sized fc forward, 0..8 (default 2)
+ *   "fc_splitk"   K slices of the rollout-sized fc forward, 0..8 (default 4)
+ *   "fc_splitk_tile" 1 that fc on 128 x 128 tiles with 16-B slab stores (default), 0 on
+ *                 128 x 64 tiles (bit-identical results for the same slice count)
  *   "rgb_aff"     1 affine-folded raw RGB conv1 (default), 0 bit-exact decode
  *   "stagger"     schedule bits 0..15 (default 2; every value gives the same results);
  *                 larger values are refused (they select timing-anatomy paths that give

@@ -244,21 +244,25 @@ class CNNEngine:
         train = ws is self.ws["train"]
         # training forward: conv1 and conv2 also write their ReLU masks as bits,
         # read by the conv2 / conv3 dgrads instead of the fp32 activations
+        # (and conv3's, read by the fc dgrad instead of a3)
         m1 = ws.get("m1bits", B * 400, dtype=torch.int32, device=dev) if train else None
         m2 = ws.get("m2bits", B * 81, dtype=torch.int64, device=dev) if train else None
-        if obs.dtype == torch.uint8 and self.C == 4 and not self._is_rgb(obs) and FUSED_TRUNK:
+        m3 = ws.get("m3bits", B * 49, dtype=torch.int32, device=dev) if train else None
+        if obs.dtype == torch.uint8 and self.C == 4 and not self._is_rgb(obs) and FUSED_TRUNK and not train:
             # u8 rows: conv1 -> conv2 -> conv3 in one persistent launch (ppo_trunk_fwd)
             call("ppo_trunk_fwd", obs.data_ptr(), ptr(idx, torch.int64, "idx"), 0, B, self.pv(self.W1),
-                 self.pv(self.B1), a1.data_ptr(), ptr(m1), self.pk(0), self.pv(self.B2), a2.data_ptr(), ptr(m2),
+                 self.pv(self.B1), a1.data_ptr(), None, self.pk(0), self.pv(self.B2), a2.data_ptr(), None,
                  self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
         else:
             self._conv1(obs, idx, B, a1, m1[:B * 400] if train else None, s)
             if train:
                 call("ppo_conv2_fwd_mask", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(),
                      m2.data_ptr(), s)
+                call("ppo_conv3_fwd_mask", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(),
+                     m3.data_ptr(), s)
             else:
                 call("ppo_conv2_fwd", a1.data_ptr(), B, self.pk(0), self.pv(self.B2), a2.data_ptr(), s)
-            call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
+                call("ppo_conv3_fwd", a2.data_ptr(), B, self.pk(1), self.pv(self.B3), a3.data_ptr(), s)
         if train:
             self._mask_rows = B
         nb = call("ppo_fc_fwd_ws_bytes", B, self.H)   # rollout-sized B: split-K into a workspace slab
@@ -341,13 +345,18 @@ class CNNEngine:
         dz3 = ws.get("dz3", B * FEAT, device=dev)
         dz2 = ws.get("dz2", B * 81 * 64, device=dev)
         dz1 = ws.get("dz1", B * 400 * 32, device=dev)
-        call("ppo_linear_dgrad_mask", dh.data_ptr(), B, self.H, self.pk(3), FEAT, a3.data_ptr(), dz3.data_ptr(), s)
+        bits = getattr(self, "_mask_rows", None) == B   # masks of this minibatch's forward
+        if bits:
+            call("ppo_fc_dgrad_bits", dh.data_ptr(), B, self.H, self.pk(3), ws.bufs["m3bits"].data_ptr(),
+                 dz3.data_ptr(), s)
+        else:
+            call("ppo_linear_dgrad_mask", dh.data_ptr(), B, self.H, self.pk(3), FEAT, a3.data_ptr(), dz3.data_ptr(),
+                 s)
         self._wgrad("fc", B, dh, a3, None, s)
         # the fc + heads tail of the flat gradient (the last parameters in torch order,
         # 92 % of the bytes at H = 512) is final here: its all-reduce (G > 1) overlaps
         # the conv backward on a side stream (_dist.start_bucket); PPO's step waits for it
         _dist.start_bucket(self.grad[self.offsets[self.W4]:])
-        bits = getattr(self, "_mask_rows", None) == B   # masks of this minibatch's forward
         if bits:
             call("ppo_conv3_dgrad_bits", dz3.data_ptr(), B, self.pk(4), ws.bufs["m2bits"].data_ptr(), dz2.data_ptr(),
                  s)

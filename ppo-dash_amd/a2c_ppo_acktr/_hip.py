@@ -59,6 +59,8 @@ SIGNATURES = {
     "ppo_fc_fwd_ws_bytes": [c_int, c_int],
     "ppo_fc_fwd_ws": [c_p, c_int, c_p, c_p, c_int, c_p, c_int, c_p, c_ll, c_p],
     "ppo_linear_dgrad_mask": [c_p, c_int, c_int, c_p, c_int, c_p, c_p, c_p],
+    "ppo_conv3_fwd_mask": [c_p, c_int, c_p, c_p, c_p, c_p, c_p],
+    "ppo_fc_dgrad_bits": [c_p, c_int, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv3_dgrad": [c_p, c_int, c_p, c_p, c_p, c_p],
     "ppo_conv3_dgrad_bits_ok": [],
     "ppo_conv3_dgrad_bits": [c_p, c_int, c_p, c_p, c_p, c_p],

@@ -1453,11 +1453,24 @@ static_assert(C3L_LDS <= C3C_LDS, "the lone tiles reuse the image loop's LDS");
 // the tile's 16 patches (3 rows of 3 pixels x 64 channels, 768 contiguous bytes per
 // row) are loaded once per block, the next tile's in registers during this tile's
 // MFMAs, and staged in LDS (two stages, image rows padded by 16 B).
+// ReLU mask bits of conv3's output (the training forward; read by the fc dgrad instead
+// of the 411 MB fp32 activation): uint16 [B][49 pixels][2 channel tiles], bit j of word
+// (p, t) = output channel 16 t + j of pixel p > 0.  Lane (g, i16) holds channels
+// 16 t + 4 g + r (r < 4) of one pixel; lanes i16, i16 + 16, +32, +48 combine by two
+// shuffles and lane g = 0 stores the word.
+__device__ __forceinline__ void conv3_mask_store(const f32x4& y, int g, uint16_t* dst) {
+  uint32_t w = ((y[0] > 0.f ? 1u : 0u) | (y[1] > 0.f ? 2u : 0u) | (y[2] > 0.f ? 4u : 0u) | (y[3] > 0.f ? 8u : 0u))
+               << (4 * g);
+  w |= (uint32_t)__shfl_xor((int)w, 16, 64);
+  w |= (uint32_t)__shfl_xor((int)w, 32, 64);
+  if (g == 0) *dst = (uint16_t)w;
+}
+
 template <int NP, int NT>
 __device__ __forceinline__ void conv3_lone_tiles(const float* __restrict__ a2, const bf16x8 (&bw)[9][3],
                                                  const float* __restrict__ bias, float* __restrict__ out,
                                                  uint8_t* __restrict__ lds, long long base, long long stride,
-                                                 int nimg, int t0, int tstep) {
+                                                 int nimg, int t0, int tstep, uint16_t* __restrict__ m3 = nullptr) {
   constexpr int KS = 9, M = 48, IR = C3L_IR, NPIECE = 16 * 144, NPC = (NPIECE + NT - 1) / NT;
   f32x4 (*const P)[16 * IR] = reinterpret_cast<f32x4 (*)[16 * IR]>(lds);
   f32x4* const R = reinterpret_cast<f32x4*>(lds + 2 * 16 * IR * 16);
@@ -1516,6 +1529,8 @@ __device__ __forceinline__ void conv3_lone_tiles(const float* __restrict__ a2, c
 #pragma unroll
       for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
       *reinterpret_cast<f32x4*>(out + (size_t)b * (49 * 32) + M * 32 + 16 * nt + 4 * g) = y;
+      // the four lanes of image i (g = 0..3) share its activity: the shuffles read live lanes
+      if (m3) conv3_mask_store(y, g, m3 + (size_t)b * 98 + M * 2 + nt);
     }
     __syncthreads();   // R read before the next tile's partials
     cur ^= 1;
@@ -1525,7 +1540,8 @@ __device__ __forceinline__ void conv3_lone_tiles(const float* __restrict__ a2, c
 template <int NP, int NT, bool LONE>
 __device__ __forceinline__ void conv3_fwd_c3_body(const float* __restrict__ a2, int B,
                                                   const uint16_t* __restrict__ wpl, const float* __restrict__ bias,
-                                                  float* __restrict__ out, uint8_t* __restrict__ lds) {
+                                                  float* __restrict__ out, uint8_t* __restrict__ lds,
+                                                  uint16_t* __restrict__ m3 = nullptr) {
   static_assert(NT == 512 || NT == 768, "8 or 12 waves");
   constexpr int NPX = 84, PL = NPX * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, UPER = (UNITS + NT - 1) / NT;
   uint16_t (*const S)[3 * PL] = reinterpret_cast<uint16_t (*)[3 * PL]>(lds);
@@ -1633,6 +1649,7 @@ __device__ __forceinline__ void conv3_fwd_c3_body(const float* __restrict__ a2, 
 #pragma unroll
           for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
           bstore_f32x4(y, rs, 4 * ((16 * (mt0 + t) + i16) * 32 + 16 * nt + 4 * g));
+          if (m3) conv3_mask_store(y, g, m3 + (size_t)b * 98 + (16 * (mt0 + t) + i16) * 2 + nt);
         }
       }
     }
@@ -1642,7 +1659,7 @@ __device__ __forceinline__ void conv3_fwd_c3_body(const float* __restrict__ a2, 
     __syncthreads();   // the last image's partials (R) are read
     const int blk = blockIdx.x;
     const int nimg = blk < B ? (B - 1 - blk) / G + 1 : 0;
-    conv3_lone_tiles<NP, NT>(a2, bw, bias, out, lds, blk, G, nimg, 0, 1);
+    conv3_lone_tiles<NP, NT>(a2, bw, bias, out, lds, blk, G, nimg, 0, 1, m3);
   }
 }
 
@@ -1654,9 +1671,9 @@ template <int NP>
 __global__ __launch_bounds__(768) void conv3_fwd_c3_kernel(const float* __restrict__ a2, int B,
                                                            const uint16_t* __restrict__ wpl,
                                                            const float* __restrict__ bias,
-                                                           float* __restrict__ out) {
+                                                           float* __restrict__ out, uint16_t* __restrict__ m3) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[C3C_LDS];
-  conv3_fwd_c3_body<NP, 768, C3F_COMPACT == 2>(a2, B, wpl, bias, out, lds);
+  conv3_fwd_c3_body<NP, 768, C3F_COMPACT == 2>(a2, B, wpl, bias, out, lds, m3);
 }
 
 template <int NP>
@@ -2289,10 +2306,14 @@ PPO_API int ppo_pack_weights(const float* w2, const float* w3, const float* w4, 
 //                they measured faster; 0: fp32 MFMA (igemm.h); 2: the split core everywhere
 //   fc_splitk    K slices of the rollout-sized fc forward with a workspace (<= 1: unsplit)
 //   rgb_aff      1: conv1 on raw RGB frames by the affine fold (rgbaff.hip); 0: bit-exact decode
+//   fc_splitk_tile 1: the rollout's split-K fc on 128 x 128 tiles (4 waves of 32 x 128), 16-B
+//                slab stores; 0: 128 x 64 tiles (8 waves of 16 x 64), 4-B stores
 // ---------------------------------------------------------------------------
-enum { TK_CONV1_FWD, TK_CONV1_WGRAD, TK_X9, TK_FC_SPLITK, TK_RGB_AFF, TK_N };
-static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv1_wgrad", "x9", "fc_splitk", "rgb_aff"};
-static int g_tune[TK_N] = {0, 9, 1, 2, 1};
+enum { TK_CONV1_FWD, TK_CONV1_WGRAD, TK_X9, TK_FC_SPLITK, TK_RGB_AFF, TK_FC_SPLITK_TILE, TK_N };
+static const char* g_tune_names[TK_N] = {"conv1_fwd", "conv1_wgrad", "x9", "fc_splitk", "rgb_aff", "fc_splitk_tile"};
+// fc_splitk 4 with 128 x 128 tiles: 0.050-0.052 vs 0.054-0.055 ms per 4,096-row act for 2
+// slices of 128 x 64 tiles (profiles/r06_s7_fc_splitk_sweep.log)
+static int g_tune[TK_N] = {0, 9, 1, 4, 1, 1};
 // stagger: the image-resident kernels with two LDS stages let waves 4-7 stage the
 // next image after their compute (conv2 / conv3 dgrad, conv3 forward)
 static int g_stagger = 2;   // bit 1 (conv2 dgrad deferred 16-B stores): measured best
@@ -2306,6 +2327,7 @@ static bool tune_ok(int k, int v) {
     case TK_CONV1_WGRAD: return v == 5 || v == 8 || v == 9 || v == 10;
     case TK_X9: return v >= 0 && v <= 2;
     case TK_FC_SPLITK: return v >= 0 && v <= 8;
+    case TK_FC_SPLITK_TILE: return v == 0 || v == 1;
     default: return v == 0 || v == 1;
   }
 }
@@ -2516,15 +2538,16 @@ PPO_API int ppo_conv2_fwd_mask(const float* a1, int B, const float* w2p, const f
   return conv2_fwd_impl(a1, B, w2p, b2, out, reinterpret_cast<uint16_t*>(mbits), stream);
 }
 
-PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream) {
-  if (B > 0 && B <= g_small_b) return small_conv3_fwd(a2, B, w3p, b3, out, as_stream(stream));
+static int conv3_fwd_impl(const float* a2, int B, const float* w3p, const float* b3, float* out, uint16_t* m3,
+                          void* stream) {
+  if (B > 0 && B <= g_small_b && !m3) return small_conv3_fwd(a2, B, w3p, b3, out, as_stream(stream));
   if (B <= 0) return 0;
   int slot;
   const bool prof = ppo_prof_begin("conv3_fwd", as_stream(stream), &slot);
   const uint16_t* wpl = planes_of(w3p, 32 * 576);
-  if (C3F_COMPACT) {   // compact rows (three tiles) + the lone output (6, 6)
-    PPO_LAUNCH_NP(conv3_fwd_c3_kernel, img_grid(B), 768, as_stream(stream), a2, B, wpl, b3, out);
-    if (C3F_COMPACT == 1) {
+  if (C3F_COMPACT || m3) {   // compact rows (three tiles) + the lone output (6, 6)
+    PPO_LAUNCH_NP(conv3_fwd_c3_kernel, img_grid(B), 768, as_stream(stream), a2, B, wpl, b3, out, m3);
+    if (C3F_COMPACT == 1 && !m3) {
       const int ntile = (B + 15) / 16;
       PPO_LAUNCH_NP(conv3_fwd_lone_kernel, (unsigned)(ntile < 512 ? ntile : 512), 256, as_stream(stream), a2, B,
                     wpl, b3, out);
@@ -2535,6 +2558,18 @@ PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float*
   if (prof) ppo_prof_end(slot, as_stream(stream), 2.0 * B * 49 * 32 * 576);
   PPO_LAUNCH_CHECK("conv3_fwd_x9_kernel");
   return 0;
+}
+
+PPO_API int ppo_conv3_fwd(const float* a2, int B, const float* w3p, const float* b3, float* out, void* stream) {
+  return conv3_fwd_impl(a2, B, w3p, b3, out, nullptr, stream);
+}
+
+// the training forward: also the ReLU mask bits of the output, uint16 [B][49][2]
+// (conv3_mask_store), read by ppo_fc_dgrad_bits
+PPO_API int ppo_conv3_fwd_mask(const float* a2, int B, const float* w3p, const float* b3, float* out,
+                               uint16_t* mbits, void* stream) {
+  PPO_REQUIRE(mbits != nullptr, "ppo_conv3_fwd_mask: null mask");
+  return conv3_fwd_impl(a2, B, w3p, b3, out, mbits, stream);
 }
 
 // conv1 -> conv2 -> conv3 forward (model.py:177-179) of u8 4-channel observation rows in
@@ -2615,7 +2650,6 @@ PPO_API int ppo_fc_fwd(const float* x, int M, const float* w4p, const float* b, 
 // and applies ReLU.
 template <class C_>
 struct DenseFwdSplitK : DenseReluFwdB<C_> {   // branch-free operand loads (the launcher checks 4·M·K < 2^31)
-  static constexpr bool VEC_STORE = false;   // partials go to the slab (store), never store4
   float* slab = nullptr;
   int chunk = 0;   // k per slice, a multiple of 32
   __device__ void k_range(int z, int& b, int& e) const {
@@ -2625,7 +2659,12 @@ struct DenseFwdSplitK : DenseReluFwdB<C_> {   // branch-free operand loads (the 
   __device__ void store(int m, int n, int z, float v) const {
     if (m < this->M && n < this->N) slab[((size_t)z * this->M + m) * this->N + n] = v;
   }
+  // vec = 1 (16-B slab rows): the raw partials of columns n .. n + 3 (no bias, no ReLU)
+  __device__ void store4(int m, int n, int z, const f32x4& v) const {
+    if (m < this->M && n < this->N) *reinterpret_cast<f32x4*>(slab + ((size_t)z * this->M + m) * this->N + n) = v;
+  }
 };
+
 
 __global__ __launch_bounds__(256) void fc_splitk_reduce_kernel(const float* __restrict__ slab, int Z, int M, int N,
                                                                const float* __restrict__ bias, float* __restrict__ out,
@@ -2661,13 +2700,21 @@ PPO_API int ppo_fc_fwd_ws(const float* x, int M, const float* w4p, const float* 
     return ppo_fc_fwd(x, M, w4p, b, H, out, ldo, stream);
   const int K = 1568, Z = (int)(need / (4LL * M * H));
   hipStream_t st = as_stream(stream);
-  DenseFwdSplitK<XP128x64w8> p;
-  p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1;
-  set_planes(p, w4p, (long long)H * K, H, K);
-  p.n_fast = 1;
-  p.slab = ws;
-  p.chunk = ((K + Z - 1) / Z + 31) / 32 * 32;
-  int rc = launch_x9(p, M, H, Z, st, "fc_fwd", 2.0 * M * H * K);
+  int rc;
+#define PPO_FCSK(CFG, VEC)                                                                   \
+  {                                                                                          \
+    DenseFwdSplitK<CFG> p;                                                                   \
+    p.x = x; p.w = w4p; p.bias = b; p.out = out; p.M = M; p.N = H; p.K = K; p.ldo = ldo; p.relu = 1; \
+    set_planes(p, w4p, (long long)H * K, H, K);                                              \
+    p.n_fast = 1;                                                                            \
+    p.slab = ws;                                                                             \
+    p.vec = VEC;                                                                             \
+    p.chunk = ((K + Z - 1) / Z + 31) / 32 * 32;                                              \
+    rc = launch_x9(p, M, H, Z, st, "fc_fwd", 2.0 * M * H * K);                               \
+  }
+  if (g_tune[TK_FC_SPLITK_TILE]) PPO_FCSK(XP128, 1)
+  else PPO_FCSK(XP128x64w8, 0)
+#undef PPO_FCSK
   if (rc) return rc;
   const long long n = (long long)M * (H / 4);
   fc_splitk_reduce_kernel<<<(unsigned)std::min<long long>((n + 255) / 256, 4096), 256, 0, st>>>(ws, Z, M, H, b, out,
@@ -2794,6 +2841,44 @@ PPO_API int ppo_linear_dgrad_mask(const float* dy, int M, int K, const float* wt
   }
   DenseDgradMask<CfgN128> p;
   p.dy = dy; p.wt = wt; p.act = act; p.dx = dx; p.M = M; p.N = N; p.K = K;
+  return launch(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);
+}
+
+// The fc dgrad with conv3's ReLU mask as bits (ppo_conv3_fwd_mask: uint16 [M][49][2],
+// bit j of word (p, t) = feature 32 p + 16 t + j): 196 B per row read in the epilogue
+// instead of the 6,272 B fp32 activation (0.605 vs 0.695 ms for the fc dgrad at the c3
+// minibatch with no mask read at all, profiles/r06_s8_fc_dgrad_mask_kbench.log)
+template <class Base>
+struct WithMask3Bits : Base {
+  const uint16_t* mbits = nullptr;
+  __device__ uint32_t bits(int m, int n) const { return (uint32_t)mbits[(size_t)m * 98 + (n >> 4)] >> (n & 15); }
+  __device__ void store(int m, int n, int, float v) const {
+    if (m < this->M && n < this->N) this->dx[(size_t)m * this->N + n] = (bits(m, n) & 1u) ? v : 0.f;
+  }
+  __device__ void store4(int m, int n, int, const f32x4& v) const {
+    if (m >= this->M || n >= this->N) return;
+    const uint32_t b = bits(m, n);
+    f32x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = ((b >> r) & 1u) ? v[r] : 0.f;
+    *reinterpret_cast<f32x4*>(this->dx + (size_t)m * this->N + n) = o;
+  }
+};
+
+PPO_API int ppo_fc_dgrad_bits(const float* dy, int M, int K, const float* wt, const uint16_t* mbits, float* dx,
+                              void* stream) {
+  PPO_REQUIRE(M >= 0 && K > 0 && K % 8 == 0 && mbits != nullptr, "ppo_fc_dgrad_bits: M=%d K=%d", M, K);
+  const int N = 1568;
+  if (use_x9() && 4LL * M * K < 0x80000000LL) {   // as ppo_linear_dgrad_mask (wt: the packed W4T segment)
+    WithMask3Bits<DenseDgradMaskB<XP128w8>> p;
+    p.dy = dy; p.wt = wt; p.act = nullptr; p.dx = dx; p.M = M; p.N = N; p.K = K; p.mbits = mbits;
+    set_planes(p, wt, (long long)N * K, N, K);
+    p.n_fast = 0;
+    p.vec = ((uintptr_t)dx & 15) == 0;
+    return launch_x9(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);
+  }
+  WithMask3Bits<DenseDgradMask<CfgN128>> p;
+  p.dy = dy; p.wt = wt; p.act = nullptr; p.dx = dx; p.M = M; p.N = N; p.K = K; p.mbits = mbits;
   return launch(p, M, N, 1, as_stream(stream), "linear_dgrad_mask", 2.0 * M * N * K);
 }
 

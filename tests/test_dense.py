@@ -161,6 +161,36 @@ def test_fc_fwd_splitk_vs_float64(gpu, Z, B, H):
     assert torch.equal(short, ref_ub)   # too small a workspace: the unsplit kernel
 
 
+@pytest.mark.parametrize("Z", [2, 3])
+@pytest.mark.parametrize("B,H", [(4096, 512), (1000, 256), (77, 64)])
+def test_fc_splitk_tiles_bit_identical(gpu, Z, B, H):
+    """fc_splitk_tile 1 (128 x 128 tiles, 16-B slab stores) and 0 (128 x 64) run the same
+    k order and part products per output: bit-identical outputs"""
+    H_ = _hip()
+    w4, packed, pk = _packed(gpu, H, 9 + H)
+    g = torch.Generator().manual_seed(B + 3 * Z)
+    xd = torch.relu(torch.randn(B, 1568, generator=g)).cuda()
+    bd = (torch.randn(H, generator=g) * 0.1).cuda()
+    old = H_.call("ppo_tune_get", b"fc_splitk"), H_.call("ppo_tune_get", b"fc_splitk_tile")
+    outs = []
+    try:
+        H_.call("ppo_tune_set", b"fc_splitk", Z)
+        nb = H_.call("ppo_fc_fwd_ws_bytes", B, H)
+        for tile in (1, 0):
+            H_.call("ppo_tune_set", b"fc_splitk_tile", tile)
+            ws = torch.full((nb // 4,), float("nan"), device=gpu)
+            out = torch.full((B, H), float("nan"), device=gpu)
+            H_.call("ppo_fc_fwd_ws", xd.data_ptr(), B, pk[2], bd.data_ptr(), H, out.data_ptr(), H, ws.data_ptr(), nb,
+                    _s())
+            torch.cuda.synchronize()
+            outs.append(out)
+    finally:
+        H_.call("ppo_tune_set", b"fc_splitk", old[0])
+        H_.call("ppo_tune_set", b"fc_splitk_tile", old[1])
+    assert not torch.isnan(outs[0]).any()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("Z,cols", [(7, 100), (39, 802816), (96, 9000), (512, 512), (512, 1), (300, 4096), (1, 33)])
 def test_colsum_vs_float64(gpu, Z, cols):
     """ppo_colsum (the deterministic split-K / block-partial reduce behind every
@@ -180,3 +210,53 @@ def test_colsum_vs_float64(gpu, Z, cols):
     err = (outs[0].double() - ref).abs().max().item()
     assert err <= 1e-6 * Z * src.abs().max().item() + 1e-7
     assert torch.equal(outs[0], outs[1])
+
+
+def _pack_mask3(a3):
+    """conv3 output [B, 1568] (HWC: feature 32 p + c) -> the uint16 [B][49][2] mask words of
+    ppo_conv3_fwd_mask (bit j of word (p, t): channel 16 t + j of pixel p > 0), as int32 [B, 98]"""
+    bits = (a3 > 0).view(a3.shape[0], 98, 16).to(torch.int64)
+    return (bits << torch.arange(16)).sum(-1).to(torch.int32)
+
+
+@pytest.mark.parametrize("B", [300, 17, 4096, 3])
+def test_conv3_fwd_mask_bits(gpu, B):
+    """ppo_conv3_fwd_mask: the same output as ppo_conv3_fwd (bit-identical; B = 3 takes the
+    image-resident kernel instead of the small-batch path, which is within fp32 tolerance)
+    and the ReLU bits of exactly that output, lone output (6, 6) included"""
+    H_ = _hip()
+    w4, packed, pk = _packed(gpu, 64, 13)
+    g = torch.Generator().manual_seed(B)
+    a2 = torch.relu(torch.randn(B, 81 * 64, generator=g)).cuda()
+    b3 = (torch.randn(32, generator=g) * 0.1).cuda()
+    out = torch.full((B, 1568), float("nan"), device=gpu)
+    ref = torch.full((B, 1568), float("nan"), device=gpu)
+    m3 = torch.full((B * 49,), -1, dtype=torch.int32, device=gpu)
+    H_.call("ppo_conv3_fwd_mask", a2.data_ptr(), B, pk[1], b3.data_ptr(), out.data_ptr(), m3.data_ptr(), _s())
+    H_.call("ppo_conv3_fwd", a2.data_ptr(), B, pk[1], b3.data_ptr(), ref.data_ptr(), _s())
+    torch.cuda.synchronize()
+    if B > 4:
+        assert torch.equal(out, ref)
+    else:
+        assert (out - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    got = m3.cpu().view(torch.int16).view(B, 98).to(torch.int32) & 0xFFFF
+    assert torch.equal(got, _pack_mask3(out.cpu()))
+    assert (out > 0).any() and (out == 0).any()
+
+
+@pytest.mark.parametrize("B,H", [(300, 512), (77, 64), (200, 40)])
+def test_fc_dgrad_bits_equals_act_mask(gpu, B, H):
+    """ppo_fc_dgrad_bits (conv3's mask bits) == ppo_linear_dgrad_mask(act = a3), bit for bit"""
+    H_ = _hip()
+    w4, packed, pk = _packed(gpu, H, 5 + H)
+    g = torch.Generator().manual_seed(B + 2)
+    dh = torch.randn(B, H, generator=g).cuda()
+    a3 = torch.relu(torch.randn(B, 1568, generator=g))
+    m3 = _pack_mask3(a3).to(torch.int16).contiguous().cuda()   # the uint16 words [B][98] (bit patterns)
+    a3d = a3.cuda()
+    got = torch.full((B, 1568), float("nan"), device=gpu)
+    ref = torch.full((B, 1568), float("nan"), device=gpu)
+    H_.call("ppo_fc_dgrad_bits", dh.data_ptr(), B, H, pk[3], m3.data_ptr(), got.data_ptr(), _s())
+    H_.call("ppo_linear_dgrad_mask", dh.data_ptr(), B, H, pk[3], 1568, a3d.data_ptr(), ref.data_ptr(), _s())
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)

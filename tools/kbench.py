@@ -55,6 +55,7 @@ def main():
     a1 = torch.empty(B * 400 * 32, device=dev)
     m1 = torch.empty(B * 400, dtype=torch.int32, device=dev)   # ReLU mask bits of a1, a2
     m2 = torch.empty(B * 81, dtype=torch.int64, device=dev)
+    m3 = torch.empty(B * 49, dtype=torch.int32, device=dev)
     a2 = torch.empty(B * 81 * 64, device=dev)
     a3 = torch.empty(B * 1568, device=dev)
     h = torch.empty(B * H, device=dev)
@@ -136,6 +137,13 @@ def main():
                                         h.data_ptr(), s), 2.0 * B * 1568 * H),
         "fc_dgrad": (lambda: call("ppo_linear_dgrad_mask", dh.data_ptr(), B, H, pk[3], 1568, a3.data_ptr(),
                                   dz3.data_ptr(), s), 2.0 * B * 1568 * H),
+        "conv3_fwd_mask": (lambda: call("ppo_conv3_fwd_mask", a2.data_ptr(), B, pk[1], b3.data_ptr(), a3.data_ptr(),
+                                        m3.data_ptr(), s), 2.0 * B * 49 * 32 * 576),
+        "fc_dgrad_bits": (lambda: call("ppo_fc_dgrad_bits", dh.data_ptr(), B, H, pk[3], m3.data_ptr(), dz3.data_ptr(),
+                                       s), 2.0 * B * 1568 * H),
+        # the fc dgrad without the ReLU-mask read (bounds what mask bits could save)
+        "fc_dgrad_nomask": (lambda: call("ppo_linear_dgrad_mask", dh.data_ptr(), B, H, pk[3], 1568, None,
+                                         dz3.data_ptr(), s), 2.0 * B * 1568 * H),
         "fc_wgrad": (lambda: call("ppo_linear_wgrad", dh.data_ptr(), a3.data_ptr(), B, H, 1568, z4, slab.data_ptr(),
                                   slab_b.data_ptr(), s), 2.0 * B * 1568 * H),
         "fc_wreduce": (lambda: call("ppo_wgrad_reduce", slab.data_ptr(), slab_b.data_ptr(), z4, H, 1568, 2, 32, 49,
@@ -187,12 +195,12 @@ def main():
                        2.0 * min(B, 4096) * (400 * 32 * 256 + 81 * 64 * 512 + 49 * 32 * 576)),
     }
     # realistic activations for the backward kernels
-    K["conv1_fwd_mask"][0](); K["conv2_fwd_mask"][0](); K["conv3_fwd"][0](); K["fc_fwd"][0]()
+    K["conv1_fwd_mask"][0](); K["conv2_fwd_mask"][0](); K["conv3_fwd_mask"][0](); K["fc_fwd"][0]()
     K["fc_dgrad"][0](); K["conv3_dgrad"][0](); K["conv2_dgrad"][0]()
     torch.cuda.synchronize()
     # default: the c3 iteration's kernels (the engine's training forms) and the rollout trunk
     only = [x for x in a.only.split(",") if x] or [
-        "conv1_fwd_mask", "conv2_fwd_mask", "conv3_fwd", "fc_fwd", "fc_dgrad", "fc_wgrad", "conv3_dgrad_bits",
+        "conv1_fwd_mask", "conv2_fwd_mask", "conv3_fwd_mask", "fc_fwd", "fc_dgrad_bits", "fc_wgrad", "conv3_dgrad_bits",
         "conv3_wgrad", "conv2_dgrad_bits", "conv2_wgrad", "conv1_wgrad", "conv1_fwd", "conv2_fwd", "trunk_4096"]
     total = 0.0
     for name, (fn, fl) in K.items():
