@@ -31,6 +31,16 @@ def test_library_exports_every_declared_symbol():
     assert lib.ppo_abi_version() == 3
 
 
+def test_library_resolves_every_symbol_at_load():
+    """RTLD_NOW: a symbol the library references but nothing defines (e.g. a helper
+    left with internal linkage in one source and declared extern in another) fails
+    here instead of at the first call on a GPU box"""
+    import ctypes
+    import os
+    from a2c_ppo_acktr import _hip
+    ctypes.CDLL(_hip.LIB_PATH, mode=os.RTLD_NOW)
+
+
 def test_ctypes_table_matches_header():
     from a2c_ppo_acktr import _hip
     assert sorted(_hip.SIGNATURES) == header_symbols()
