@@ -820,38 +820,50 @@ __global__ __launch_bounds__(512) void conv2_fwd_x9c_kernel(const float* __restr
 // row i16 of the B operand is image base + stride * (16 t + i16)).  The kernel above
 // runs it after its image loop over the block's own images (base = blockIdx.x, stride
 // = the grid), conv2_fwd_lone_kernel (C2F_LONE = 1) over contiguous images.
-constexpr int C2L_IR = 129;   // f32x4 per staged image row (128 + pad)
-constexpr int C2L_LDS = 2 * 16 * C2L_IR * 16 + 4 * 64 * 16;   // two patch stages + K-half partials (70,144 B)
+// Round 6: the patches are split into their bf16 planes once, while staged (each thread
+// one 8-channel chunk of one image), instead of by every wave at fragment read (the 4
+// waves of a K half split the same chunks: 7 split VALU per MFMA).
+constexpr int C2L_IR = 65;    // 16-B units per staged image row and plane (64 + pad: the 16
+                              // images of a fragment read hit distinct 16-B slots)
+constexpr int C2L_PL = 16 * C2L_IR;   // units per plane
+constexpr int C2L_LDS = 2 * 3 * C2L_PL * 16 + 4 * 64 * 16;   // two 3-plane stages + K-half partials (103,936 B)
 static_assert(C2L_LDS <= C2F_LDS, "the lone tiles reuse the image loop's LDS");
 template <int NP, bool MASK>
 __device__ __forceinline__ void conv2_lone_tiles(const float* __restrict__ a1, const bf16x8 (&bw)[8][3],
                                                  const float* __restrict__ bias, float* __restrict__ out,
                                                  uint16_t* __restrict__ mbits, uint8_t* __restrict__ lds,
                                                  long long base, long long stride, int nimg, int t0, int tstep) {
-  constexpr int KS = 8, M = 72, IR = C2L_IR;
-  f32x4 (*const P)[16 * IR] = reinterpret_cast<f32x4 (*)[16 * IR]>(lds);
-  f32x4* const R = reinterpret_cast<f32x4*>(lds + 2 * 16 * IR * 16);
+  constexpr int KS = 8, M = 72, IR = C2L_IR, PL = C2L_PL;
+  uint4 (*const P)[3 * PL] = reinterpret_cast<uint4 (*)[3 * PL]>(lds);
+  f32x4* const R = reinterpret_cast<f32x4*>(lds + 2 * 3 * PL * 16);
   const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nt = wave & 3, kh = wave >> 2;
   const int ntile = (nimg + 15) / 16;
-  // piece q = tid + 512 j (j < 4) of a tile: image q >> 7, f32x4 f = q & 127 of its
-  // patch = tap (4 ky + kx) * 8 + channel quad; a1 offset (16 + ky) * 640 + (f & 31) * 4
-  f32x4 pc[4];
+  // chunk c = tid + 512 j (j < 2) of a tile: image c >> 6, 8-channel chunk u = c & 63 of
+  // its patch = tap (4 ky + kx) * 4 + channel octet; a1 offset (16 + ky) * 640 + (u & 15) * 8
+  f32x4 pc[2][2];
   auto fetch = [&](int T) {   // past the last tile / image: zeros, nothing loaded
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = tid + 512 * j, im = q >> 7, f = q & 127, i = 16 * T + im;
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 512 * j, im = c >> 6, u = c & 63, i = 16 * T + im;
       const bool live = T < ntile && i < nimg;
-      const float* src = a1 + (size_t)(base + stride * (live ? i : 0)) * 12800 + (16 + (f >> 5)) * 640 + (f & 31) * 4;
-      pc[j] = live ? *reinterpret_cast<const f32x4*>(src) : zero4();
+      const float* src = a1 + (size_t)(base + stride * (live ? i : 0)) * 12800 + (16 + (u >> 4)) * 640 + (u & 15) * 8;
+      pc[j][0] = live ? *reinterpret_cast<const f32x4*>(src) : zero4();
+      pc[j][1] = live ? *reinterpret_cast<const f32x4*>(src + 4) : zero4();
     }
   };
   auto put = [&](int st) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = tid + 512 * j;
-      P[st][(q >> 7) * IR + (q & 127)] = pc[j];
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 512 * j, o = (c >> 6) * IR + (c & 63);
+      Frag3 f;
+      split8(pc[j][0], pc[j][1], f, NP == 1);
+      P[st][o] = __builtin_bit_cast(uint4, f.h);
+      if constexpr (NP != 1) {
+        P[st][PL + o] = __builtin_bit_cast(uint4, f.m);
+        P[st][2 * PL + o] = __builtin_bit_cast(uint4, f.l);
+      }
     }
   };
   fetch(t0);
@@ -866,9 +878,13 @@ __device__ __forceinline__ void conv2_lone_tiles(const float* __restrict__ a1, c
     f32x4 acc = zero4();
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const f32x4* x = &P[cur][i16 * IR + (8 * kh + s) * 8 + 2 * g];
+      const int o = i16 * IR + (8 * kh + s) * 4 + g;
       Frag3 a;
-      split8(x[0], x[1], a, NP == 1);
+      a.h = __builtin_bit_cast(bf16x8, P[cur][o]);
+      if constexpr (NP != 1) {
+        a.m = __builtin_bit_cast(bf16x8, P[cur][PL + o]);
+        a.l = __builtin_bit_cast(bf16x8, P[cur][2 * PL + o]);
+      }
       const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
 #define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
       PPO_PRODUCTS(NP, PPO_PART)
