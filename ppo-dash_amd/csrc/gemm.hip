@@ -1456,19 +1456,12 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
 // conv3_fwd_x9_body, so every output is bit-identical to it whatever the wave count.
 // LONE: the lone output of the block's own images after its image loop (round 6,
 // VERDICT r05 item 7); else conv3_fwd_lone_kernel covers it (C3F_COMPACT = 1).
-constexpr int C3C_LDS = 2 * 3 * C3F_PL * 2 + 2 * 2 * 3 * 64 * 16;   // stages + K-half partials (76,800 B)
-constexpr int C3L_IR = 145;   // f32x4 per staged lone patch (144 + pad)
-constexpr int C3L_LDS = 2 * 16 * C3L_IR * 16 + 2 * 64 * 16;   // two patch stages + K-half partials (76,288 B)
-static_assert(C3L_LDS <= C3C_LDS, "the lone tiles reuse the image loop's LDS");
+constexpr int C3L_IR = 73;    // 16-B units per staged lone patch and plane (72 + pad)
+constexpr int C3L_PL = 16 * C3L_IR;
+constexpr int C3L_LDS = 2 * 3 * C3L_PL * 16 + 2 * 64 * 16;   // two 3-plane patch stages + K-half partials (114,176 B)
+constexpr int C3C_LDS0 = 2 * 3 * C3F_PL * 2 + 2 * 2 * 3 * 64 * 16;   // the image loop: stages + K-half partials (76,800 B)
+constexpr int C3C_LDS = C3C_LDS0 > C3L_LDS ? C3C_LDS0 : C3L_LDS;   // the lone tiles after it reuse the LDS
 
-// conv3 forward of output 48 = (6, 6) for 16 images per tile: tiles t0, t0 + tstep, ...
-// of the images base + stride * i (i < nimg; row i16 of the B operand is image base +
-// stride * (16 t + i16)); the same operands, MFMA sequence, K-half sum and epilogue as
-// the compact kernel (bit-identical).  Waves 0-3 compute (co tile w & 1, K half w >> 1,
-// their weight fragments bw), every thread of the NT stages.  As conv2's lone tiles,
-// the tile's 16 patches (3 rows of 3 pixels x 64 channels, 768 contiguous bytes per
-// row) are loaded once per block, the next tile's in registers during this tile's
-// MFMAs, and staged in LDS (two stages, image rows padded by 16 B).
 // ReLU mask bits of conv3's output (the training forward; read by the fc dgrad instead
 // of the 411 MB fp32 activation): uint16 [B][49 pixels][2 channel tiles], bit j of word
 // (p, t) = output channel 16 t + j of pixel p > 0.  Lane (g, i16) holds channels
@@ -1482,35 +1475,53 @@ __device__ __forceinline__ void conv3_mask_store(const f32x4& y, int g, uint16_t
   if (g == 0) *dst = (uint16_t)w;
 }
 
+// conv3 forward of output 48 = (6, 6) for 16 images per tile: tiles t0, t0 + tstep, ...
+// of the images base + stride * i (i < nimg; row i16 of the B operand is image base +
+// stride * (16 t + i16)); the same operands, MFMA sequence, K-half sum and epilogue as
+// the compact kernel (bit-identical).  Waves 0-3 compute (co tile w & 1, K half w >> 1,
+// their weight fragments bw), every thread of the NT stages.  As conv2's lone tiles,
+// the tile's 16 patches (3 rows of 3 pixels x 64 channels, 768 contiguous bytes per
+// row) are loaded once per block, the next tile's in registers during this tile's
+// MFMAs, and staged in LDS (two stages, image rows padded by 16 B).
 template <int NP, int NT>
 __device__ __forceinline__ void conv3_lone_tiles(const float* __restrict__ a2, const bf16x8 (&bw)[9][3],
                                                  const float* __restrict__ bias, float* __restrict__ out,
                                                  uint8_t* __restrict__ lds, long long base, long long stride,
                                                  int nimg, int t0, int tstep, uint16_t* __restrict__ m3 = nullptr) {
-  constexpr int KS = 9, M = 48, IR = C3L_IR, NPIECE = 16 * 144, NPC = (NPIECE + NT - 1) / NT;
-  f32x4 (*const P)[16 * IR] = reinterpret_cast<f32x4 (*)[16 * IR]>(lds);
-  f32x4* const R = reinterpret_cast<f32x4*>(lds + 2 * 16 * IR * 16);
+  constexpr int KS = 9, M = 48, IR = C3L_IR, PL = C3L_PL, NCH = 16 * 72, NPC = (NCH + NT - 1) / NT;
+  uint4 (*const P)[3 * PL] = reinterpret_cast<uint4 (*)[3 * PL]>(lds);
+  f32x4* const R = reinterpret_cast<f32x4*>(lds + 2 * 3 * PL * 16);
   const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nt = wave & 1, kh = (wave >> 1) & 1;
   const int ntile = (nimg + 15) / 16;
-  // piece q = tid + NT j: image q / 144, f32x4 f = q % 144 of its patch = ky * 48 +
-  // kx * 16 + channel quad; a2 offset ((6 + ky) * 9 + 6) * 64 + (f % 48) * 4
-  f32x4 pc[NPC];
+  // chunk c = tid + NT j: image c / 72, 8-channel chunk u = c % 72 of its patch = tap
+  // (3 ky + kx) * 8 + channel octet; a2 offset ((6 + ky) * 9 + 6) * 64 + (u % 24) * 8.
+  // Round 6: split into the bf16 planes once here, not by each computing wave at
+  // fragment read (as conv2_lone_tiles)
+  f32x4 pc[NPC][2];
   auto fetch = [&](int T) {   // past the last tile / image: zeros, nothing loaded
 #pragma unroll
     for (int j = 0; j < NPC; ++j) {
-      const int q = tid + NT * j, im = q / 144, f = q - 144 * im, ky = f / 48, i = 16 * T + im;
-      const bool live = q < NPIECE && T < ntile && i < nimg;
-      const float* src = a2 + (size_t)(base + stride * (live ? i : 0)) * 5184 + ((6 + ky) * 9 + 6) * 64 + (f - 48 * ky) * 4;
-      pc[j] = live ? *reinterpret_cast<const f32x4*>(src) : zero4();
+      const int c = tid + NT * j, im = c / 72, u = c - 72 * im, ky = u / 24, i = 16 * T + im;
+      const bool live = c < NCH && T < ntile && i < nimg;
+      const float* src = a2 + (size_t)(base + stride * (live ? i : 0)) * 5184 + ((6 + ky) * 9 + 6) * 64 + (u - 24 * ky) * 8;
+      pc[j][0] = live ? *reinterpret_cast<const f32x4*>(src) : zero4();
+      pc[j][1] = live ? *reinterpret_cast<const f32x4*>(src + 4) : zero4();
     }
   };
   auto put = [&](int st) {
 #pragma unroll
     for (int j = 0; j < NPC; ++j) {
-      const int q = tid + NT * j, im = q / 144;
-      if (q < NPIECE) P[st][im * IR + (q - 144 * im)] = pc[j];
+      const int c = tid + NT * j, im = c / 72;
+      if (c < NCH) {
+        const int o = im * IR + (c - 72 * im);
+        Frag3 f;
+        split8(pc[j][0], pc[j][1], f, false);
+        P[st][o] = __builtin_bit_cast(uint4, f.h);
+        P[st][PL + o] = __builtin_bit_cast(uint4, f.m);
+        P[st][2 * PL + o] = __builtin_bit_cast(uint4, f.l);
+      }
     }
   };
   fetch(t0);
@@ -1525,10 +1536,11 @@ __device__ __forceinline__ void conv3_lone_tiles(const float* __restrict__ a2, c
     if (wave < 4) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const int ks = 9 * kh + s, tap = ks >> 1, c = 4 * (ks & 1) + g;
-        const f32x4* x = &P[cur][i16 * IR + tap * 16 + 2 * c];
+        const int ks = 9 * kh + s, tap = ks >> 1, c = 4 * (ks & 1) + g, o = i16 * IR + tap * 8 + c;
         Frag3 a;
-        split8(x[0], x[1], a, false);
+        a.h = __builtin_bit_cast(bf16x8, P[cur][o]);
+        a.m = __builtin_bit_cast(bf16x8, P[cur][PL + o]);
+        a.l = __builtin_bit_cast(bf16x8, P[cur][2 * PL + o]);
         const Frag3 w = {bw[s][0], bw[s][1], bw[s][2]};
 #define PPO_PART(X, Y) acc = mma(w.Y, a.X, acc);
         PPO_PRODUCTS(NP, PPO_PART)
@@ -1722,6 +1734,7 @@ __global__ __launch_bounds__(256) void conv3_fwd_lone_kernel(const float* __rest
 // (the largest phase, conv2: 154,368 B).
 constexpr int TRUNK_LDS = C2F_LDS > C3F_LDS ? (C2F_LDS > 2 * 4 * C1S * 2 ? C2F_LDS : 2 * 4 * C1S * 2)
                                             : (C3F_LDS > 2 * 4 * C1S * 2 ? C3F_LDS : 2 * 4 * C1S * 2);
+static_assert(C3L_LDS <= TRUNK_LDS, "the trunk's conv3 phase runs its lone tiles in the shared LDS");
 __device__ __forceinline__ void trunk_phase_sync() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's output stores are in L2
   __syncthreads();
