@@ -1459,7 +1459,7 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
 constexpr int C3L_IR = 73;    // 16-B units per staged lone patch and plane (72 + pad)
 constexpr int C3L_PL = 16 * C3L_IR;
 constexpr int C3L_LDS = 2 * 3 * C3L_PL * 16 + 2 * 64 * 16;   // two 3-plane patch stages + K-half partials (114,176 B)
-constexpr int C3C_LDS0 = 2 * 3 * C3F_PL * 2 + 2 * 2 * 3 * 64 * 16;   // the image loop: stages + K-half partials (76,800 B)
+constexpr int C3C_LDS0 = 2 * 3 * 84 * 80 * 2 + 2 * 2 * 3 * 64 * 16;   // the image loop: stages + K-half partials (92,928 B)
 constexpr int C3C_LDS = C3C_LDS0 > C3L_LDS ? C3C_LDS0 : C3L_LDS;   // the lone tiles after it reuse the LDS
 
 // ReLU mask bits of conv3's output (the training forward; read by the fc dgrad instead
@@ -1571,7 +1571,13 @@ __device__ __forceinline__ void conv3_fwd_c3_body(const float* __restrict__ a2, 
                                                   float* __restrict__ out, uint8_t* __restrict__ lds,
                                                   uint16_t* __restrict__ m3 = nullptr) {
   static_assert(NT == 512 || NT == 768, "8 or 12 waves");
-  constexpr int NPX = 84, PL = NPX * 64, KS = 9, WN = 32 * 576, UNITS = 81 * 8, UPER = (UNITS + NT - 1) / NT;
+  // pixel rows of 80 bf16 (160 B, 16-B chunk c of pixel p at 16-B slot 10 p + c): round 6,
+  // for the compact rows' tap reads, whose 16 lanes of a ds_read_b128 group are 16
+  // pixels 9 oy + ox + tap apart: 2-way bank conflicts at most, against up to 3-way with
+  // 128-B rows and the chunk swizzle c ^ ((p >> 1) & 7) (55 % of the LDS-active cycles
+  // conflicted, profiles/r06_s19_conv_fwd_sq.json; tools-free model in DESIGN §A.0)
+  constexpr int NPX = 84, PR = 80, PL = NPX * PR, KS = 9, WN = 32 * 576, UNITS = 81 * 8,
+                UPER = (UNITS + NT - 1) / NT;
   uint16_t (*const S)[3 * PL] = reinterpret_cast<uint16_t (*)[3 * PL]>(lds);
   f32x4 (*const R)[2][3][64] = reinterpret_cast<f32x4 (*)[2][3][64]>(lds + 2 * 3 * PL * 2);   // [stage][co tile][row tile][lane]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, i16 = lane & 15, g = lane >> 4;
@@ -1600,7 +1606,7 @@ __device__ __forceinline__ void conv3_fwd_c3_body(const float* __restrict__ a2, 
     for (int j = 0; j < UPER; ++j) {
       const int u = tid + NT * j;
       if (u < UNITS) {
-        const int p = u >> 3, off = p * 64 + 8 * ((u & 7) ^ ((p >> 1) & 7));
+        const int p = u >> 3, off = p * PR + 8 * (u & 7);
         Frag3 f;
         split8(stg[j][0], stg[j][1], f, false);
         *reinterpret_cast<bf16x8*>(&S[buf][off]) = f.h;
@@ -1644,7 +1650,7 @@ __device__ __forceinline__ void conv3_fwd_c3_body(const float* __restrict__ a2, 
 #pragma unroll
         for (int t = 0; t < NTL; ++t) {
           const int p = p0[t] + 9 * ky + kx;
-          const uint16_t* q = Sc + p * 64 + 8 * (c ^ ((p >> 1) & 7));
+          const uint16_t* q = Sc + p * PR + 8 * c;
           a[t].h = *reinterpret_cast<const bf16x8*>(q);
           a[t].m = *reinterpret_cast<const bf16x8*>(q + PL);
           a[t].l = *reinterpret_cast<const bf16x8*>(q + 2 * PL);
@@ -1734,7 +1740,7 @@ __global__ __launch_bounds__(256) void conv3_fwd_lone_kernel(const float* __rest
 // (the largest phase, conv2: 154,368 B).
 constexpr int TRUNK_LDS = C2F_LDS > C3F_LDS ? (C2F_LDS > 2 * 4 * C1S * 2 ? C2F_LDS : 2 * 4 * C1S * 2)
                                             : (C3F_LDS > 2 * 4 * C1S * 2 ? C3F_LDS : 2 * 4 * C1S * 2);
-static_assert(C3L_LDS <= TRUNK_LDS, "the trunk's conv3 phase runs its lone tiles in the shared LDS");
+static_assert(C3L_LDS <= TRUNK_LDS && C3C_LDS0 <= TRUNK_LDS, "the trunk's conv3 phase in the shared LDS");
 __device__ __forceinline__ void trunk_phase_sync() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's output stores are in L2
   __syncthreads();
