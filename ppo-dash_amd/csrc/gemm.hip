@@ -1443,7 +1443,8 @@ __global__ __launch_bounds__(512) void conv3_fwd_x9_kernel(const float* __restri
   conv3_fwd_x9_body<NP>(a2, B, wpl, bias, out, lds);
 }
 
-// conv3 forward with compact rows (round 5): GEMM row m = 7 oy + ox over the 49 real
+// conv3 forward with compact rows (round 5; the row -> output map c3_row_q since round 6,
+// the original order is described below): GEMM row m = 7 oy + ox over the 49 real
 // outputs (the 9-wide grid above issues 64 rows for them), row tiles 0-2 (m < 48)
 // and output 48 = (6, 6) left to conv3_lone_tiles.  Wave w: co tile w & 1, K half
 // (w >> 1) & 1; with NT = 768 threads (the standalone launch, 3 waves per SIMD) row
@@ -1461,6 +1462,19 @@ constexpr int C3L_PL = 16 * C3L_IR;
 constexpr int C3L_LDS = 2 * 3 * C3L_PL * 16 + 2 * 64 * 16;   // two 3-plane patch stages + K-half partials (114,176 B)
 constexpr int C3C_LDS0 = 2 * 3 * 84 * 80 * 2 + 2 * 2 * 3 * 64 * 16;   // the image loop: stages + K-half partials (92,928 B)
 constexpr int C3C_LDS = C3C_LDS0 > C3L_LDS ? C3C_LDS0 : C3L_LDS;   // the lone tiles after it reuse the LDS
+
+// Compact rows of conv3's forward (round 6): tile row 16 t + r computes output pixel
+// q = c3_row_q[16 t + r] (q = 7 oy + ox), the 49th, (6, 0), is the lone output.  With
+// 160-B pixel rows (16-B slot 10 p + c of input pixel p = 9 oy + ox + tap, chunk c) the
+// 16 lanes of a ds_read_b128 group — rows {0-3, 12-15} at chunk c0 and rows {4-11} at
+// c0 + 1, or the reverse — hit distinct slots for every tap iff each of those two row
+// sets covers the 8 residues p mod 8 once: this table does that for all 3 tiles (the
+// residue of (6, 6) would have left one set a duplicate, hence the lone (6, 0)); the
+// oy-major order before it met 2-way conflicts in most groups (tools/conv3_bank_model.py)
+constexpr int C3_LONE_Y = 6, C3_LONE_X = 0, C3_LONE_Q = 7 * C3_LONE_Y + C3_LONE_X;
+__constant__ uint8_t c3_row_q[48] = {0,  1,  2,  3,  20, 7,  8,  9,  10, 11, 12, 19, 4,  5,  6,  13,
+                                     26, 27, 14, 15, 32, 33, 34, 21, 22, 23, 24, 31, 16, 17, 18, 25,
+                                     38, 39, 40, 41, 44, 45, 46, 47, 48, 35, 36, 43, 28, 29, 30, 37};
 
 // ReLU mask bits of conv3's output (the training forward; read by the fc dgrad instead
 // of the 411 MB fp32 activation): uint16 [B][49 pixels][2 channel tiles], bit j of word
@@ -1488,7 +1502,7 @@ __device__ __forceinline__ void conv3_lone_tiles(const float* __restrict__ a2, c
                                                  const float* __restrict__ bias, float* __restrict__ out,
                                                  uint8_t* __restrict__ lds, long long base, long long stride,
                                                  int nimg, int t0, int tstep, uint16_t* __restrict__ m3 = nullptr) {
-  constexpr int KS = 9, M = 48, IR = C3L_IR, PL = C3L_PL, NCH = 16 * 72, NPC = (NCH + NT - 1) / NT;
+  constexpr int KS = 9, M = C3_LONE_Q, IR = C3L_IR, PL = C3L_PL, NCH = 16 * 72, NPC = (NCH + NT - 1) / NT;
   uint4 (*const P)[3 * PL] = reinterpret_cast<uint4 (*)[3 * PL]>(lds);
   f32x4* const R = reinterpret_cast<f32x4*>(lds + 2 * 3 * PL * 16);
   const int tid = threadIdx.x, lane = tid & 63, i16 = lane & 15, g = lane >> 4;
@@ -1496,7 +1510,8 @@ __device__ __forceinline__ void conv3_lone_tiles(const float* __restrict__ a2, c
   const int nt = wave & 1, kh = (wave >> 1) & 1;
   const int ntile = (nimg + 15) / 16;
   // chunk c = tid + NT j: image c / 72, 8-channel chunk u = c % 72 of its patch = tap
-  // (3 ky + kx) * 8 + channel octet; a2 offset ((6 + ky) * 9 + 6) * 64 + (u % 24) * 8.
+  // (3 ky + kx) * 8 + channel octet; a2 offset ((LY + ky) * 9 + LX) * 64 + (u % 24) * 8 for
+  // the lone output (LY, LX) = (C3_LONE_Y, C3_LONE_X).
   // Round 6: split into the bf16 planes once here, not by each computing wave at
   // fragment read (as conv2_lone_tiles)
   f32x4 pc[NPC][2];
@@ -1505,7 +1520,8 @@ __device__ __forceinline__ void conv3_lone_tiles(const float* __restrict__ a2, c
     for (int j = 0; j < NPC; ++j) {
       const int c = tid + NT * j, im = c / 72, u = c - 72 * im, ky = u / 24, i = 16 * T + im;
       const bool live = c < NCH && T < ntile && i < nimg;
-      const float* src = a2 + (size_t)(base + stride * (live ? i : 0)) * 5184 + ((6 + ky) * 9 + 6) * 64 + (u - 24 * ky) * 8;
+      const float* src = a2 + (size_t)(base + stride * (live ? i : 0)) * 5184 + ((C3_LONE_Y + ky) * 9 + C3_LONE_X) * 64 +
+                         (u - 24 * ky) * 8;
       pc[j][0] = live ? *reinterpret_cast<const f32x4*>(src) : zero4();
       pc[j][1] = live ? *reinterpret_cast<const f32x4*>(src + 4) : zero4();
     }
@@ -1629,11 +1645,12 @@ __device__ __forceinline__ void conv3_fwd_c3_body(const float* __restrict__ a2, 
   // every wave), the barriers stay outside the wave-dependent branch
   const int mt0 = NT == 768 ? (wave >> 2) : (wave < 4 ? 0 : 2);
   const int ntl = NT == 768 || wave >= 4 ? 1 : 2;
-  int p0[2];
+  int p0[2], q0[2];   // tap-(0, 0) input pixel and output pixel of this lane's row per tile
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const int m = 16 * (mt0 + t) + i16, oy = m / 7;
-    p0[t] = 9 * oy + (m - 7 * oy);
+    const int q = c3_row_q[mt0 + t < 3 ? 16 * (mt0 + t) + i16 : 0], oy = q / 7;   // (no tile 3: unused)
+    q0[t] = q;
+    p0[t] = 9 * oy + (q - 7 * oy);
   }
   for (; b < B; b += G) {
     put(cur ^ 1);   // unconditional (past the end: a copy of this image into the idle stage)
@@ -1682,8 +1699,8 @@ __device__ __forceinline__ void conv3_fwd_c3_body(const float* __restrict__ a2, 
           f32x4 y;
 #pragma unroll
           for (int r = 0; r < 4; ++r) y[r] = fmaxf(v[r] + bv4[r], 0.f);
-          bstore_f32x4(y, rs, 4 * ((16 * (mt0 + t) + i16) * 32 + 16 * nt + 4 * g));
-          if (m3) conv3_mask_store(y, g, m3 + (size_t)b * 98 + (16 * (mt0 + t) + i16) * 2 + nt);
+          bstore_f32x4(y, rs, 4 * (q0[t] * 32 + 16 * nt + 4 * g));
+          if (m3) conv3_mask_store(y, g, m3 + (size_t)b * 98 + q0[t] * 2 + nt);
         }
       }
     }
