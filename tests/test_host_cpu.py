@@ -62,6 +62,35 @@ def test_host_only_queries():
     assert _hip.call("ppo_heads_train_blocks", 65536) == 65536 // 128
 
 
+def test_tune_knobs_accept_listed_values_only():
+    """ppo_tune_set (include/ppo_hip.h, run-time knobs): each key takes its listed
+    values, anything else is refused with PPO_EARG and leaves the knob unchanged;
+    unknown keys read -1.  Host-only: no GPU call."""
+    from a2c_ppo_acktr import _hip
+    listed = {"conv1_fwd": (0, 9), "conv1_wgrad": (9, 10, 8, 5), "x9": (1, 0, 2), "fc_splitk": (4, 0, 8),
+              "fc_splitk_tile": (1, 0), "rgb_aff": (1, 0), "stagger": (2, 0, 15), "products": (6, 9, 1)}
+    refused = {"conv1_fwd": (1, 2, 10), "conv1_wgrad": (0, 7, 11), "x9": (-1, 3), "fc_splitk": (-1, 9),
+               "fc_splitk_tile": (2,), "rgb_aff": (2,), "stagger": (16, 255, -1), "products": (0, 2, 5)}
+    for key, vals in listed.items():
+        k = key.encode()
+        old = _hip.call("ppo_tune_get", k)
+        assert old == vals[0], (key, old)   # the documented default
+        try:
+            for v in vals:
+                _hip.call("ppo_tune_set", k, v)
+                assert _hip.call("ppo_tune_get", k) == v
+            _hip.call("ppo_tune_set", k, old)
+            for v in refused[key]:
+                with pytest.raises(_hip.HipError, match="1001"):
+                    _hip.call("ppo_tune_set", k, v)
+                assert _hip.call("ppo_tune_get", k) == old
+        finally:
+            _hip.call("ppo_tune_set", k, old)
+    assert _hip.call("ppo_tune_get", b"no_such_knob") == -1
+    with pytest.raises(_hip.HipError):
+        _hip.call("ppo_tune_set", b"no_such_knob", 0)
+
+
 def test_u8_decode_exact_for_all_codes():
     from oracle import ppo_oracle as O
     lib = O._lib()
